@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""bench.py -- RC-pass throughput (Mpixel*cascades/s) and full-pipeline fps of the MI355X
+DoRC2DGI() at 4096^2, cascadeCount=6 (BASELINE.json metric).
+
+One step = one DoRC2DGI() frame (RC2DGI.cs:267-406: ScreenUV, 12 JFA steps + distance
+field, 6 cascade levels, blur + copy-back, merge + copy-back) over a synthetic painted
+scene already resident in HBM (the reference's demo scene scaled to 4096^2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 4096] [--cascades 6]
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank renders its own scene
+(the path has no exchange step at this size: replicas, "scaling": "weak"); rank 0 prints
+the JSON line with the max-over-ranks time.
+
+value = sum over ranks of CW*CH*N per frame * K / max-over-ranks( sum of the K RC-pass
+HIP-event times ) -- t_RC as SURVEY.md §8d defines it: the hipEvent time of the N level
+launches, recorded on the stream the kernels run on.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def b_rc(W, H, CW, CH, N):
+    """Algorithmic bytes of one RC pass: write G_L, read G_{L+1} once,
+    read the distance field once per level."""
+    return 16 * CW * CH * (2 * N - 1) + 4 * W * H * N
+
+
+def cpu_baseline(W, H, N, rr, budget_s=12.0):
+    """The CPU port of the RC pass (oracle/, OpenMP on this host's cores), timed on a
+    bounded sample of the same workload: whole-width row bands of every level."""
+    import numpy as np
+
+    import oracle
+    from radiancecascade2dglobalillumination_amd import scenes
+
+    p = oracle.Params(W=W, H=H, N=N, ray_range=rr)
+    CW, CH, S = oracle.dims(p)
+    color, emis = scenes.demo(W, H)
+    j = oracle.screen_uv(color)
+    mx = max(W, H)
+    step = np.float32(1.0)
+    for _ in range(S):
+        step = np.float32(step * np.float32(0.5))
+        j = oracle.jfa_step(j, float(step), float(np.float32(W) / mx), float(np.float32(H) / mx))
+    dist = oracle.distance_field(j)
+    dirs, sky = oracle.dir_tables(p), oracle.sky_table(p)
+    offs, o = [], 0
+    for L in range(N):
+        offs.append(o)
+        o += 4 << (2 * L)
+    upper = np.zeros((CH, CW, 4), np.float32)
+    upper[..., 3] = 1.0
+    out = np.zeros((CH, CW, 4), np.float32)
+    rows = 8
+    done_px, spent = 0, 0.0
+    while True:
+        t0 = time.perf_counter()
+        for L in range(N - 1, -1, -1):
+            r0 = (CH // 2) - rows // 2
+            oracle.rc_level(p, L, upper if L < N - 1 else None, color, emis, dist, out,
+                            np.ascontiguousarray(dirs[offs[L]:]), sky, r0, r0 + rows)
+        dt = time.perf_counter() - t0
+        done_px += CW * rows * N
+        spent += dt
+        if spent >= budget_s or rows >= CH:
+            break
+        rows = min(CH, int(rows * max(2.0, min(8.0, (budget_s - spent) / max(dt, 1e-3) / 2))))
+    return dict(value=round(done_px / spent / 1e6, 3), unit="Mpixel*cascades/s", cores=oracle.num_threads(),
+                kind="port",
+                sample=f"RC pass of the same {W}x{H} N={N} demo frame, whole-width row bands through all {N} "
+                       f"levels ({done_px / (CW * N):.0f} rows/level in total, {spent:.1f} s, CPU restatement "
+                       f"oracle/rc2dgi_oracle.c, {platform.processor() or platform.machine()})")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--cascades", type=int, default=6)
+    ap.add_argument("--ray-range", type=float, default=2.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    a = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from radiancecascade2dglobalillumination_amd import RC2DGI, scenes
+
+    W = a.size
+    H = a.height or a.size
+    N = a.cascades
+    color, emis = scenes.demo(W, H, t=3.0 + 0.25 * rank)  # one independent scene per rank
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local)
+    CW, CH = ctx.cascade_resolution
+    # inputs resident in HBM before the timed region
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    ctx.set_timing(True)
+    for _ in range(a.warmup):
+        ctx.do_rc2dgi()
+    ctx.sync()
+
+    rc_ms, tot_ms, lvl_ms = [], [], np.zeros(N)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctx.do_rc2dgi()
+        t = ctx.pass_times(levels=N)  # waits for this frame's last event
+        rc_ms.append(t["rc"])
+        tot_ms.append(t["total"])
+        lvl_ms += np.array(t["levels"])
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+
+    stats = torch.tensor([sum(rc_ms), sum(tot_ms), wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    t_rc, t_tot, wall = (float(x) for x in stats.tolist())
+    units = CW * CH * N * a.steps * world
+    value = units / (t_rc / 1e3) / 1e6
+    bytes_launch = b_rc(W, H, CW, CH, N) / N
+    avg_launch_s = (t_rc / 1e3) / (a.steps * N)
+    achieved = bytes_launch / avg_launch_s / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "rc_level_pmc.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f)
+        if rec.get("config") == f"{W}x{H}_N{N}":
+            traffic = rec.get("hbm_bytes_per_launch")
+    line = {
+        "metric": "Mpixel*cascades/s (RC pass) at 4096^2, cascadeCount=6",
+        "value": round(value, 1),
+        "unit": "Mpixel*cascades/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(wall * 1e3 / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (reference demo scene painted at 4096^2, resident in HBM)",
+        "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}", "screen": [W, H],
+                   "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
+                   "parallelism": f"replicas{world}"},
+        "rc_ms_per_frame": round(t_rc / a.steps, 4),
+        "rc_level_ms": [round(x / a.steps, 4) for x in lvl_ms.tolist()],
+        "full_pipeline_ms": round(t_tot / a.steps, 4),
+        "full_pipeline_fps": round(1e3 * a.steps / t_tot, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_rc_level", "bytes_per_launch": bytes_launch,
+                     "avg_launch_ms": round(avg_launch_s * 1e3, 5)},
+    }
+    if rank == 0 and not a.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(W, H, N, a.ray_range, a.cpu_budget)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

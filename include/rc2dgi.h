@@ -1,0 +1,147 @@
+/*
+ * rc2dgi.h -- C ABI of librc2dgi.so, the MI355X-native DoRC2DGI() pass chain.
+ *
+ * Drop-in boundary for the reference's per-frame GI path:
+ *   DoRC2DGI()           RC2DGI.cs:267-406   -> rc2dgi_do()
+ *   SetGIShaderValues()  RC2DGI.cs:408-433   -> rc2dgi_set_uniform() / rc2dgi_set_uniform_i()
+ *   RT set + knobs       RC2DGI.cs:28-41, 66-98 -> rc2dgi_config + rc2dgi_create()
+ *   ClearAllRTs()        RC2DGI.cs:450-483   -> folded into rc2dgi_do() (every target the
+ *                                               frame reads is rewritten before it is read)
+ *   painted colorRT/emissiveRT (RenderScene RC2DGI.cs:224-264, RedrawSceneToRTs
+ *                       RC2DGI.cs:528-545)  -> rc2dgi_upload()
+ *   debug thumbnails / final blit (RC2DGI.cs:135-163, 435-448) -> rc2dgi_download()
+ *
+ * Conventions:
+ *   - plain C, blittable arguments (P/Invoke int/float/IntPtr), UTF-8 uniform names;
+ *   - every entry point returns 0 (RC2DGI_OK) or a negative rc2dgi_status; nothing
+ *     aborts or throws across the ABI; rc2dgi_last_error() explains the last failure;
+ *   - the context owns every device buffer; host buffers are caller-owned and only
+ *     touched during the call (upload/download are synchronous w.r.t. the host pointer);
+ *   - images are RGBA, rows in GL texture order (row 0 = bottom), the memory layout of
+ *     rlReadTexturePixels / UpdateTexture for a render texture;
+ *   - one context per thread at a time (the reference drives one GL context from its
+ *     main thread); independent contexts may run concurrently on different streams or
+ *     devices (batch / replica mode);
+ *   - the ping-pong identities of the reference are preserved: jumpRT1 holds the
+ *     ScreenUV seeds and every other JFA step; giRT1 receives level N-1; the final GI
+ *     texture is giRT2 when N is even and giRT1 when N is odd (RC2DGI.cs:365).
+ *
+ * Storage: f32 semantics (RGBA32F render textures, the reference's own commented intent,
+ * RC2DGI.cs:100-107).  RC2DGI_STORAGE_RGBA8_COMPAT (the literal 8-bit app) is reserved
+ * and currently returns RC2DGI_E_UNSUPPORTED.
+ */
+#ifndef RC2DGI_H
+#define RC2DGI_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RC2DGI_ABI_VERSION 1
+
+typedef struct rc2dgi_ctx rc2dgi_ctx;
+
+typedef enum rc2dgi_status {
+  RC2DGI_OK = 0,
+  RC2DGI_E_ARG = -1,          /* bad argument (null pointer, size, enum value) */
+  RC2DGI_E_UNIFORM = -2,      /* unknown or read-only uniform name / wrong component count */
+  RC2DGI_E_HIP = -3,          /* HIP runtime error (message in rc2dgi_last_error) */
+  RC2DGI_E_OOM = -4,          /* device allocation failed */
+  RC2DGI_E_UNSUPPORTED = -5,  /* valid request this build does not implement */
+  RC2DGI_E_STATE = -6         /* call not valid in the current state */
+} rc2dgi_status;
+
+typedef enum rc2dgi_storage {
+  RC2DGI_STORAGE_F32 = 0,
+  RC2DGI_STORAGE_RGBA8_COMPAT = 1
+} rc2dgi_storage;
+
+/* render textures of the reference (RC2DGI.cs:19-25) */
+typedef enum rc2dgi_rt {
+  RC2DGI_RT_COLOR = 0,     /* colorRT: painted scene in, merged result out      (W x H) */
+  RC2DGI_RT_EMISSIVE = 1,  /* emissiveRT                                        (W x H) */
+  RC2DGI_RT_JUMP1 = 2,     /* jumpRT1                                           (W x H) */
+  RC2DGI_RT_JUMP2 = 3,     /* jumpRT2                                           (W x H) */
+  RC2DGI_RT_DIST = 4,      /* distRT (16-bit distance packed into R,G)          (W x H) */
+  RC2DGI_RT_GI1 = 5,       /* giRT1                                             (CW x CH) */
+  RC2DGI_RT_GI2 = 6,       /* giRT2                                             (CW x CH) */
+  RC2DGI_RT_TEMP = 7,      /* tempRT                                            (W x H) */
+  RC2DGI_RT_BLUR = 8,      /* cascadeBlurRT                                     (CW x CH) */
+  RC2DGI_RT_FINAL_GI = 9   /* alias of giRT1 / giRT2 per RC2DGI.cs:365          (CW x CH) */
+} rc2dgi_rt;
+
+typedef enum rc2dgi_format {
+  RC2DGI_FMT_RGBA8 = 0,    /* 4 x uint8, unorm (k/255) */
+  RC2DGI_FMT_RGBA32F = 1   /* 4 x float32 */
+} rc2dgi_format;
+
+typedef struct rc2dgi_config {
+  int screen_width;        /* screenWidth  (RC2DGI.cs:7) */
+  int screen_height;       /* screenHeight (RC2DGI.cs:8) */
+  int cascade_count;       /* cascadeCount (RC2DGI.cs:66), 1..15 */
+  float render_scale;      /* renderScale  (RC2DGI.cs:67), > 0 */
+  float ray_range;         /* rayRange     (RC2DGI.cs:68) -> _RayRange */
+  int storage;             /* rc2dgi_storage */
+  int device;              /* HIP device ordinal */
+  int reserved[5];         /* must be zero */
+} rc2dgi_config;
+
+/* ---- lifetime (RC2DGI.cs:57-109) */
+int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out);
+int rc2dgi_destroy(rc2dgi_ctx *ctx);
+
+/* ---- uniforms (SetGIShaderValues RC2DGI.cs:408-433, Blur RC2DGI.cs:373-374).
+ * Accepted names (reference spelling): _RayRange(1) _SkyRadiance(1) _SkyColor(3)
+ * _SunColor(3) _SunAngle(1) _Reflectivity(1) _BlurRadius(1).  The per-pass uniforms the
+ * reference derives itself (_StepSize _Aspect _CascadeResolution _CascadeLevel _Resolution)
+ * are computed inside rc2dgi_do() and are rejected here with RC2DGI_E_UNIFORM. */
+int rc2dgi_set_uniform(rc2dgi_ctx *ctx, const char *name, const float *v, int n);
+/* _CascadeCount (reallocates the cascade textures, like re-running RC2DGI.cs:66-98) */
+int rc2dgi_set_uniform_i(rc2dgi_ctx *ctx, const char *name, int v);
+int rc2dgi_get_uniform(rc2dgi_ctx *ctx, const char *name, float *v, int n);
+
+/* ---- inputs: the painted colorRT / emissiveRT (W x H).  Host source: synchronous copy.
+ * Device source (a HIP device pointer on the context's device): enqueued on the context
+ * stream, the caller keeps the source alive until rc2dgi_sync(). */
+int rc2dgi_upload(rc2dgi_ctx *ctx, int which, const void *host, int pitch_bytes, int format);
+int rc2dgi_upload_device(rc2dgi_ctx *ctx, int which, const void *dev, int pitch_bytes, int format);
+
+/* ---- one DoRC2DGI() frame: enqueues every pass on the context stream and returns. */
+int rc2dgi_do(rc2dgi_ctx *ctx);
+int rc2dgi_sync(rc2dgi_ctx *ctx);
+
+/* ---- outputs: any render texture, in the reference's RGBA encoding (synchronous). */
+int rc2dgi_download(rc2dgi_ctx *ctx, int which, void *host, int pitch_bytes, int format);
+
+/* cascade resolution (RC2DGI.cs:70-77), JFA step count (RC2DGI.cs:289-292) and which
+ * giRT holds the final GI (1 or 2, RC2DGI.cs:365) */
+int rc2dgi_query(rc2dgi_ctx *ctx, int *cascade_w, int *cascade_h, int *jfa_steps, int *final_gi);
+const char *rc2dgi_last_error(rc2dgi_ctx *ctx);
+int rc2dgi_abi_version(void);
+
+/* ---- stream / timing.  rc2dgi_set_stream: run on a caller-owned hipStream_t on the
+ * context's device (NULL = back to the context's own stream).  With timing enabled,
+ * rc2dgi_do() records HIP events around each pass; rc2dgi_pass_times() returns the last
+ * frame's milliseconds in the order {screenuv, jfa (all steps, DF fused into the last),
+ * rc (all N levels), blur (+copy-back), merge (+copy-back), total} and, when
+ * level_ms != NULL, the N per-level RC times indexed by level. */
+int rc2dgi_set_stream(rc2dgi_ctx *ctx, void *hip_stream);
+int rc2dgi_set_timing(rc2dgi_ctx *ctx, int enable);
+int rc2dgi_pass_times(rc2dgi_ctx *ctx, float *pass_ms, int n_pass, float *level_ms, int n_level);
+
+/* ---- transcendental tables.  rc2dgi_do() evaluates cos/sin (RadianceCascades.fs:117-121)
+ * and the sky integral (RadianceCascades.fs:48-57, 150-154) as correctly rounded fp32
+ * tables.  A host may instead supply the exact values its GL implementation produces
+ * (used by the parity tests to reproduce llvmpipe bit-for-bit); pass NULL to revert. */
+int rc2dgi_set_direction_table(rc2dgi_ctx *ctx, int level, const float *cos_sin, int n);
+int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
+
+/* ---- debug views beyond the reference's thumbnails: keep a copy of every cascade level G_L
+ * as stored by its pass (costs N extra cascade textures and one copy per level). */
+int rc2dgi_set_keep_levels(rc2dgi_ctx *ctx, int enable);
+int rc2dgi_download_level(rc2dgi_ctx *ctx, int level, void *host, int pitch_bytes, int format);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RC2DGI_H */

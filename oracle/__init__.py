@@ -73,6 +73,14 @@ def lib():
         L.orc_sky_table.argtypes = [ctypes.POINTER(_Cfg), _f32p]
         L.orc_dims.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                ctypes.POINTER(ctypes.c_int)]
+        L.orc_screen_uv.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
+        L.orc_jfa_step.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                   ctypes.c_float, _f32p]
+        L.orc_distance_field.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
+        L.orc_blur.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_float, _f32p]
+        L.orc_blur_copyback.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
+        L.orc_merge.argtypes = [_f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                _f32p]
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_set_num_threads.argtypes = [ctypes.c_int]
         _lib = L
@@ -181,6 +189,65 @@ def rc_level(p: Params, level: int, upper, color, emissive, dist, out, dir_table
     _, CH, _ = dims(p)
     lib().orc_rc_level(ctypes.byref(p.c()), level, _p(upper), _p(color), _p(emissive), _p(dist), _p(out),
                        _p(dir_table), _p(sky_tab), None, row0, CH if row1 is None else row1)
+
+
+def _c(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+def screen_uv(color, tc=None):
+    """ScreenUV.fs over a cleared jumpRT1 -> (H, W, 4)."""
+    color = _c(color)
+    H, W = color.shape[:2]
+    out = np.empty((H, W, 4), np.float32)
+    lib().orc_screen_uv(_p(color), _p(out), W, H, _p(None if tc is None else _c(tc)))
+    return out
+
+
+def jfa_step(src, step: float, aspx: float, aspy: float, tc=None):
+    """One JumpFlood.fs step (the source alpha is 1, so dst is fully overwritten)."""
+    src = _c(src)
+    H, W = src.shape[:2]
+    out = np.zeros((H, W, 4), np.float32)
+    out[..., 3] = 1.0
+    lib().orc_jfa_step(_p(src), _p(out), W, H, step, aspx, aspy, _p(None if tc is None else _c(tc)))
+    return out
+
+
+def distance_field(jump, tc=None):
+    jump = _c(jump)
+    H, W = jump.shape[:2]
+    out = np.zeros((H, W, 4), np.float32)
+    out[..., 3] = 1.0
+    lib().orc_distance_field(_p(jump), _p(out), W, H, _p(None if tc is None else _c(tc)))
+    return out
+
+
+def blur(gi, radius: float, tc=None):
+    gi = _c(gi)
+    CH, CW = gi.shape[:2]
+    out = np.empty_like(gi)
+    lib().orc_blur(_p(gi), _p(out), CW, CH, radius, _p(None if tc is None else _c(tc)))
+    return out
+
+
+def blur_copyback(blur_img, gi, tc=None):
+    """Returns the blended copy of blur_img onto (a copy of) gi."""
+    blur_img = _c(blur_img)
+    g = _c(gi).copy()
+    CH, CW = g.shape[:2]
+    lib().orc_blur_copyback(_p(blur_img), _p(g), CW, CH, _p(None if tc is None else _c(tc)))
+    return g
+
+
+def merge(color, gi, tc=None):
+    color, gi = _c(color), _c(gi)
+    H, W = color.shape[:2]
+    CH, CW = gi.shape[:2]
+    temp = np.empty_like(color)
+    out = np.empty_like(color)
+    lib().orc_merge(_p(color), _p(gi), _p(temp), _p(out), W, H, CW, CH, _p(None if tc is None else _c(tc)))
+    return temp, out
 
 
 def num_threads() -> int:

@@ -1,0 +1,54 @@
+"""In-tree build of librc2dgi.so (HIP kernels + C ABI) for gfx950 with hipcc.
+
+The library lands next to this file so that it travels with the repository snapshot to
+the GPU box (built ``.so`` files are git-ignored but not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "librc2dgi.so")
+SOURCES = ["rc2dgi_kernels.hip", "rc2dgi_capi.cpp"]
+HEADERS = ["rc2dgi_device.h", "rc2dgi_kernels.h"]
+ARCH = os.environ.get("RC2DGI_OFFLOAD_ARCH", "gfx950")
+
+# -ffp-contract=off: each a*b+c in the kernels is two IEEE roundings, exactly as the GLSL
+# expressions they restate; the GL lerp's fused multiply-add is written as fmaf explicitly.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+         f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm is required to build librc2dgi.so)")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "rc2dgi.h")]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    cmd = [hipcc()] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"]
+    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

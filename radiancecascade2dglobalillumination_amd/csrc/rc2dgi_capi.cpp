@@ -1,0 +1,675 @@
+// rc2dgi_capi.cpp -- the C ABI (include/rc2dgi.h): context, uniforms, tables, I/O and the
+// DoRC2DGI() orchestrator.  Mirrors RC2DGI.cs:57-109 (resources), :267-406 (pass order,
+// ping-pong identities) and :408-433 (uniform binding).
+#include "../../include/rc2dgi.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rc2dgi_kernels.h"
+
+using namespace rc2dgi;
+
+namespace {
+
+constexpr float kTau = 6.28318530718f;  // RadianceCascades.fs:27
+
+enum Pass { P_SCREENUV = 0, P_JFA, P_RC, P_BLUR, P_MERGE, P_TOTAL, P_COUNT };
+
+inline bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+}  // namespace
+
+struct rc2dgi_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  // knobs (RC2DGI.cs:28-41, 66-68)
+  int W = 0, H = 0, N = 0;
+  float render_scale = 1.0f;
+  float ray_range = 2.0f;
+  float sky_radiance = 1.0f, sky_color[3] = {0.5f, 0.6f, 0.8f}, sun_color[3] = {1.0f, 0.9f, 0.6f};
+  float sun_angle = 0.3f, reflectivity = 0.0f, blur_radius = 1.5f;
+  // derived sizes
+  int CW = 0, CH = 0, S = 0;
+  ScreenDims sd{};
+  CascadeDims cd{};
+  // device buffers (the reference's render textures)
+  float4 *color_in = nullptr, *emissive = nullptr, *temp = nullptr, *color_out = nullptr;
+  float2 *jump1 = nullptr, *jump2 = nullptr;
+  float *dist = nullptr;
+  float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
+  float2 *dirs = nullptr;  // concatenated per level
+  float4 *sky = nullptr;
+  // state
+  bool tables_dirty = true;
+  std::vector<std::vector<float>> dir_override;  // per level, empty = computed
+  std::vector<float> sky_override;
+  bool frame_done = false;   // colorRT holds the merged result
+  bool have_frame = false;
+  int final_gi = 1;
+  bool timing = false;
+  hipEvent_t ev[P_COUNT + 1] = {};
+  std::vector<hipEvent_t> ev_level;  // N + 1
+  bool keep_levels = false;
+  std::vector<float4 *> level_bufs;  // debug copies of G_L
+  std::string err;
+};
+
+namespace {
+
+int fail(rc2dgi_ctx *c, int code, const std::string &msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(rc2dgi_ctx *c, hipError_t e, const char *what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(c, e == hipErrorOutOfMemory ? RC2DGI_E_OOM : RC2DGI_E_HIP, m);
+}
+
+#define HIPCHK(ctx, expr)                                 \
+  do {                                                    \
+    hipError_t e_ = (expr);                               \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
+  } while (0)
+
+// RC2DGI.cs:70-77 and :289-292 (double arithmetic as in C#)
+void derive_sizes(int W, int H, int N, float rs, int &CW, int &CH, int &S) {
+  const double powVal = std::pow(2.0, N);
+  CW = (int)std::ceil((double)((float)W * rs) / powVal) * (int)powVal;
+  CH = (int)std::ceil((double)((float)H * rs) / powVal) * (int)powVal;
+  const int mx = W > H ? W : H;
+  S = (int)std::ceil(std::log((double)mx) / std::log(2.0));
+  if (S < 1) S = 1;
+}
+
+size_t dir_table_len(int N) {  // sum over levels of 4^(L+1)
+  size_t n = 0;
+  for (int L = 0; L < N; ++L) n += (size_t)4 << (2 * L);
+  return n;
+}
+size_t dir_table_offset(int L) {
+  size_t n = 0;
+  for (int q = 0; q < L; ++q) n += (size_t)4 << (2 * q);
+  return n;
+}
+
+void free_level_bufs(rc2dgi_ctx *c) {
+  for (float4 *p : c->level_bufs)
+    if (p) (void)hipFree(p);
+  c->level_bufs.clear();
+}
+
+void free_buffers(rc2dgi_ctx *c) {
+  free_level_bufs(c);
+  void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist,
+                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky};
+  for (void *p : bufs)
+    if (p) (void)hipFree(p);
+  c->color_in = c->emissive = c->temp = c->color_out = nullptr;
+  c->jump1 = c->jump2 = nullptr;
+  c->dist = nullptr;
+  c->gi1 = c->gi2 = c->blur = nullptr;
+  c->dirs = nullptr;
+  c->sky = nullptr;
+}
+
+template <class T>
+hipError_t alloc(T **p, size_t bytes) {
+  return hipMalloc(reinterpret_cast<void **>(p), bytes);
+}
+
+// (re)allocate every render texture for the current W, H, N (RC2DGI.cs:79-98)
+int allocate(rc2dgi_ctx *c) {
+  free_buffers(c);
+  derive_sizes(c->W, c->H, c->N, c->render_scale, c->CW, c->CH, c->S);
+  const int sp = round_up(c->W, 64), cp = round_up(c->CW, 64);
+  c->sd = ScreenDims{c->W, c->H, sp, is_pow2(c->W), is_pow2(c->H)};
+  c->cd = CascadeDims{c->CW, c->CH, cp, is_pow2(c->CW), is_pow2(c->CH)};
+  const size_t ns = (size_t)sp * c->H, nc = (size_t)cp * c->CH;
+  HIPCHK(c, alloc(&c->color_in, ns * sizeof(float4)));
+  HIPCHK(c, alloc(&c->emissive, ns * sizeof(float4)));
+  HIPCHK(c, alloc(&c->temp, ns * sizeof(float4)));
+  HIPCHK(c, alloc(&c->color_out, ns * sizeof(float4)));
+  HIPCHK(c, alloc(&c->jump1, ns * sizeof(float2)));
+  HIPCHK(c, alloc(&c->jump2, ns * sizeof(float2)));
+  HIPCHK(c, alloc(&c->dist, ns * sizeof(float)));
+  HIPCHK(c, alloc(&c->gi1, nc * sizeof(float4)));
+  HIPCHK(c, alloc(&c->gi2, nc * sizeof(float4)));
+  HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
+  HIPCHK(c, alloc(&c->dirs, dir_table_len(c->N) * sizeof(float2)));
+  HIPCHK(c, alloc(&c->sky, ((size_t)4 << (2 * (c->N - 1))) * sizeof(float4)));
+  // initial contents: ClearAllRTs (RC2DGI.cs:109) -> (0,0,0,1) is implied by the frame
+  // itself; zero everything so never-written texels (cascadeBlurRT with blur off) read as a
+  // fresh texture does.
+  HIPCHK(c, hipMemsetAsync(c->color_in, 0, ns * sizeof(float4), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->emissive, 0, ns * sizeof(float4), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->blur, 0, nc * sizeof(float4), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->dir_override.assign(c->N, {});
+  c->tables_dirty = true;
+  c->have_frame = c->frame_done = false;
+  c->ev_level.resize(c->N + 1);
+  if (c->keep_levels) {
+    c->level_bufs.assign(c->N, nullptr);
+    for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, nc * sizeof(float4)));
+  }
+  return RC2DGI_OK;
+}
+
+// correctly rounded tables for RadianceCascades.fs:117-121 and :48-57/:150-154
+void build_tables(const rc2dgi_ctx *c, std::vector<float2> &dirs, std::vector<float4> &sky) {
+  dirs.resize(dir_table_len(c->N));
+  for (int L = 0; L < c->N; ++L) {
+    const int b = 1 << L, n = 4 * b * b;
+    const size_t off = dir_table_offset(L);
+    if (!c->dir_override[L].empty()) {
+      for (int a = 0; a < n; ++a) dirs[off + a] = make_float2(c->dir_override[L][2 * a], c->dir_override[L][2 * a + 1]);
+      continue;
+    }
+    const float angleStep = kTau / (float)(b * b * 4);
+    for (int a = 0; a < n; ++a) {
+      const float angle = ((float)a + 0.5f) * angleStep;
+      dirs[off + a] = make_float2((float)std::cos((double)angle), (float)std::sin((double)angle));
+    }
+  }
+  const int b = 1 << (c->N - 1), n = 4 * b * b;
+  sky.resize(n);
+  if (!c->sky_override.empty()) {
+    for (int a = 0; a < n; ++a)
+      sky[a] = make_float4(c->sky_override[3 * a], c->sky_override[3 * a + 1], c->sky_override[3 * a + 2], 0.0f);
+    return;
+  }
+  const float angleStep = kTau / (float)(b * b * 4);
+  const float SSunS = 8.0f, ISSunS = 1.0f / 8.0f;
+  for (int a = 0; a < n; ++a) {
+    const float a0 = ((float)a + 0.5f) * angleStep;
+    const float a1 = a0 + angleStep;
+    const float ca1 = (float)std::cos((double)a1), ca0 = (float)std::cos((double)a0);
+    const float sky_term = a1 - a0 - 0.5f * (ca1 - ca0);
+    const float at0 = (float)std::atan((double)(SSunS * (c->sun_angle - a0)));
+    const float at1 = (float)std::atan((double)(SSunS * (c->sun_angle - a1)));
+    const float sun_term = at0 - at1;
+    float v[3];
+    for (int k = 0; k < 3; ++k) {
+      float SI = c->sky_color[k] * sky_term;
+      SI = SI + c->sun_color[k] * sun_term * ISSunS;
+      float s = SI * 0.16f;
+      s = s * c->sky_radiance;
+      v[k] = (s / angleStep) * 2.0f;
+    }
+    sky[a] = make_float4(v[0], v[1], v[2], 0.0f);
+  }
+}
+
+int upload_tables(rc2dgi_ctx *c) {
+  if (!c->tables_dirty) return RC2DGI_OK;
+  std::vector<float2> dirs;
+  std::vector<float4> sky;
+  build_tables(c, dirs, sky);
+  HIPCHK(c, hipMemcpyAsync(c->dirs, dirs.data(), dirs.size() * sizeof(float2), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->sky, sky.data(), sky.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  // the host vectors die here: make the pageable copies complete first
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->tables_dirty = false;
+  return RC2DGI_OK;
+}
+
+bool screen_rt(int which) {
+  return which == RC2DGI_RT_COLOR || which == RC2DGI_RT_EMISSIVE || which == RC2DGI_RT_JUMP1 ||
+         which == RC2DGI_RT_JUMP2 || which == RC2DGI_RT_DIST || which == RC2DGI_RT_TEMP;
+}
+
+inline unsigned char to_unorm8(float x) {  // GL readback conversion: clamp, round to nearest even
+  float v = x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
+  return (unsigned char)std::nearbyint(v * 255.0f);
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+int rc2dgi_abi_version(void) { return RC2DGI_ABI_VERSION; }
+
+int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
+  if (!cfg || !out) return RC2DGI_E_ARG;
+  *out = nullptr;
+  if (cfg->screen_width <= 0 || cfg->screen_height <= 0 || cfg->screen_width > 32768 ||
+      cfg->screen_height > 32768 || cfg->cascade_count < 1 || cfg->cascade_count > 15 ||
+      !(cfg->render_scale > 0.0f))
+    return RC2DGI_E_ARG;
+  for (int r : cfg->reserved)
+    if (r != 0) return RC2DGI_E_ARG;
+  if (cfg->storage == RC2DGI_STORAGE_RGBA8_COMPAT) return RC2DGI_E_UNSUPPORTED;
+  if (cfg->storage != RC2DGI_STORAGE_F32) return RC2DGI_E_ARG;
+  rc2dgi_ctx *c = new (std::nothrow) rc2dgi_ctx();
+  if (!c) return RC2DGI_E_OOM;
+  c->device = cfg->device;
+  c->W = cfg->screen_width;
+  c->H = cfg->screen_height;
+  c->N = cfg->cascade_count;
+  c->render_scale = cfg->render_scale;
+  c->ray_range = cfg->ray_range;
+  int rc = RC2DGI_OK;
+  hipError_t e = hipSetDevice(c->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    fprintf(stderr, "rc2dgi_create: %s\n", hipGetErrorString(e));
+    delete c;
+    return e == hipErrorOutOfMemory ? RC2DGI_E_OOM : RC2DGI_E_HIP;
+  }
+  c->stream = c->own_stream;
+  for (auto &ev : c->ev) (void)hipEventCreate(&ev);
+  rc = allocate(c);
+  if (rc != RC2DGI_OK) {
+    fprintf(stderr, "rc2dgi_create: %s\n", c->err.c_str());
+    rc2dgi_destroy(c);
+    return rc;
+  }
+  for (auto &ev : c->ev_level) (void)hipEventCreate(&ev);
+  *out = c;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_destroy(rc2dgi_ctx *c) {
+  if (!c) return RC2DGI_E_ARG;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_buffers(c);
+  for (auto &ev : c->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto &ev : c->ev_level)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return RC2DGI_OK;
+}
+
+const char *rc2dgi_last_error(rc2dgi_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int rc2dgi_set_uniform(rc2dgi_ctx *c, const char *name, const float *v, int n) {
+  if (!c || !name || !v) return fail(c, RC2DGI_E_ARG, "null argument");
+  std::string s(name);
+  auto scalar = [&](float &dst, bool affects_sky) -> int {
+    if (n != 1) return fail(c, RC2DGI_E_UNIFORM, s + " takes 1 component");
+    dst = v[0];
+    if (affects_sky) c->tables_dirty = true;
+    return RC2DGI_OK;
+  };
+  auto vec3 = [&](float *dst) -> int {
+    if (n != 3) return fail(c, RC2DGI_E_UNIFORM, s + " takes 3 components");
+    for (int k = 0; k < 3; ++k) dst[k] = v[k];
+    c->tables_dirty = true;
+    return RC2DGI_OK;
+  };
+  if (s == "_RayRange") return scalar(c->ray_range, false);
+  if (s == "_SkyRadiance") return scalar(c->sky_radiance, true);
+  if (s == "_SunAngle") return scalar(c->sun_angle, true);
+  if (s == "_Reflectivity") return scalar(c->reflectivity, false);
+  if (s == "_BlurRadius") return scalar(c->blur_radius, false);
+  if (s == "_SkyColor") return vec3(c->sky_color);
+  if (s == "_SunColor") return vec3(c->sun_color);
+  if (s == "_StepSize" || s == "_Aspect" || s == "_CascadeResolution" || s == "_CascadeLevel" ||
+      s == "_Resolution" || s == "_CascadeCount")
+    return fail(c, RC2DGI_E_UNIFORM, s + " is derived per pass by rc2dgi_do (or use rc2dgi_set_uniform_i)");
+  return fail(c, RC2DGI_E_UNIFORM, "unknown uniform " + s);
+}
+
+int rc2dgi_get_uniform(rc2dgi_ctx *c, const char *name, float *v, int n) {
+  if (!c || !name || !v) return fail(c, RC2DGI_E_ARG, "null argument");
+  std::string s(name);
+  const float *src = nullptr;
+  int k = 1;
+  if (s == "_RayRange") src = &c->ray_range;
+  else if (s == "_SkyRadiance") src = &c->sky_radiance;
+  else if (s == "_SunAngle") src = &c->sun_angle;
+  else if (s == "_Reflectivity") src = &c->reflectivity;
+  else if (s == "_BlurRadius") src = &c->blur_radius;
+  else if (s == "_SkyColor") { src = c->sky_color; k = 3; }
+  else if (s == "_SunColor") { src = c->sun_color; k = 3; }
+  else return fail(c, RC2DGI_E_UNIFORM, "unknown uniform " + s);
+  if (n != k) return fail(c, RC2DGI_E_UNIFORM, s + " has " + std::to_string(k) + " components");
+  for (int q = 0; q < k; ++q) v[q] = src[q];
+  return RC2DGI_OK;
+}
+
+int rc2dgi_set_uniform_i(rc2dgi_ctx *c, const char *name, int v) {
+  if (!c || !name) return fail(c, RC2DGI_E_ARG, "null argument");
+  std::string s(name);
+  if (s != "_CascadeCount") return fail(c, RC2DGI_E_UNIFORM, "unknown integer uniform " + s);
+  if (v < 1 || v > 15) return fail(c, RC2DGI_E_ARG, "_CascadeCount must be in 1..15");
+  if (v == c->N) return RC2DGI_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (auto &ev : c->ev_level)
+    if (ev) (void)hipEventDestroy(ev);
+  c->ev_level.clear();
+  c->N = v;
+  // the painted inputs survive the reallocation
+  std::vector<float4> col((size_t)c->sd.pitch * c->H), em((size_t)c->sd.pitch * c->H);
+  HIPCHK(c, hipMemcpy(col.data(), c->color_in, col.size() * sizeof(float4), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(em.data(), c->emissive, em.size() * sizeof(float4), hipMemcpyDeviceToHost));
+  c->sky_override.clear();
+  int rc = allocate(c);
+  if (rc != RC2DGI_OK) return rc;
+  for (auto &ev : c->ev_level) (void)hipEventCreate(&ev);
+  HIPCHK(c, hipMemcpy(c->color_in, col.data(), col.size() * sizeof(float4), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->emissive, em.data(), em.size() * sizeof(float4), hipMemcpyHostToDevice));
+  return RC2DGI_OK;
+}
+
+int rc2dgi_upload(rc2dgi_ctx *c, int which, const void *host, int pitch_bytes, int format) {
+  if (!c || !host) return fail(c, RC2DGI_E_ARG, "null argument");
+  if (which != RC2DGI_RT_COLOR && which != RC2DGI_RT_EMISSIVE)
+    return fail(c, RC2DGI_E_ARG, "only COLOR and EMISSIVE are inputs");
+  const int W = c->W, H = c->H;
+  const int row = format == RC2DGI_FMT_RGBA32F ? W * 16 : (format == RC2DGI_FMT_RGBA8 ? W * 4 : -1);
+  if (row < 0) return fail(c, RC2DGI_E_ARG, "bad format");
+  if (pitch_bytes == 0) pitch_bytes = row;
+  if (pitch_bytes < row) return fail(c, RC2DGI_E_ARG, "pitch smaller than a row");
+  HIPCHK(c, hipSetDevice(c->device));
+  float4 *dst = which == RC2DGI_RT_COLOR ? c->color_in : c->emissive;
+  if (format == RC2DGI_FMT_RGBA32F) {
+    HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)c->sd.pitch * 16, host, pitch_bytes, (size_t)W * 16, H,
+                               hipMemcpyHostToDevice, c->stream));
+  } else {
+    std::vector<float4> tmp((size_t)W * H);
+    const unsigned char *src = static_cast<const unsigned char *>(host);
+    for (int j = 0; j < H; ++j)
+      for (int i = 0; i < W; ++i) {
+        const unsigned char *p = src + (size_t)j * pitch_bytes + 4 * (size_t)i;
+        tmp[(size_t)j * W + i] = make_float4((float)p[0] / 255.0f, (float)p[1] / 255.0f, (float)p[2] / 255.0f,
+                                             (float)p[3] / 255.0f);
+      }
+    HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)c->sd.pitch * 16, tmp.data(), (size_t)W * 16, (size_t)W * 16, H,
+                               hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (which == RC2DGI_RT_COLOR) c->frame_done = false;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_upload_device(rc2dgi_ctx *c, int which, const void *dev, int pitch_bytes, int format) {
+  if (!c || !dev) return fail(c, RC2DGI_E_ARG, "null argument");
+  if (which != RC2DGI_RT_COLOR && which != RC2DGI_RT_EMISSIVE)
+    return fail(c, RC2DGI_E_ARG, "only COLOR and EMISSIVE are inputs");
+  const int W = c->W, H = c->H;
+  const int row = format == RC2DGI_FMT_RGBA32F ? W * 16 : (format == RC2DGI_FMT_RGBA8 ? W * 4 : -1);
+  if (row < 0) return fail(c, RC2DGI_E_ARG, "bad format");
+  if (pitch_bytes == 0) pitch_bytes = row;
+  if (pitch_bytes < row) return fail(c, RC2DGI_E_ARG, "pitch smaller than a row");
+  HIPCHK(c, hipSetDevice(c->device));
+  float4 *dst = which == RC2DGI_RT_COLOR ? c->color_in : c->emissive;
+  if (format == RC2DGI_FMT_RGBA32F) {
+    HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)c->sd.pitch * 16, dev, pitch_bytes, (size_t)W * 16, H,
+                               hipMemcpyDeviceToDevice, c->stream));
+  } else {
+    HIPCHK(c, launch_unorm8_to_f32(static_cast<const unsigned char *>(dev), pitch_bytes, dst, c->sd.pitch, W, H,
+                                   c->stream));
+  }
+  if (which == RC2DGI_RT_COLOR) c->frame_done = false;
+  return RC2DGI_OK;
+}
+
+// ------------------------------------------------------------------ DoRC2DGI()
+int rc2dgi_do(rc2dgi_ctx *c) {
+  if (!c) return RC2DGI_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = upload_tables(c);
+  if (rc != RC2DGI_OK) return rc;
+  hipStream_t st = c->stream;
+  const bool T = c->timing;
+  if (T) HIPCHK(c, hipEventRecord(c->ev[0], st));
+
+  // aspect = (W, H) / max(W, H)  (RC2DGI.cs:273)
+  const int mx = c->W > c->H ? c->W : c->H;
+  const float aspx = (float)c->W / (float)mx, aspy = (float)c->H / (float)mx;
+
+  // 1. ScreenUV -> jumpRT1 (RC2DGI.cs:276-285)
+  HIPCHK(c, launch_screen_uv(c->color_in, c->jump1, c->sd, st));
+  if (T) HIPCHK(c, hipEventRecord(c->ev[1], st));
+
+  // 2. JumpFlood ping-pong (RC2DGI.cs:287-326); 3. DistanceField fused into the last step
+  bool j1final = true;
+  float stepSize = 1.0f;
+  for (int i = 0; i < c->S; ++i) {
+    stepSize *= 0.5f;
+    float ox[3], oy[3];
+    for (int k = 0; k < 3; ++k) {  // vec2(x, y) * _Aspect.yx * _StepSize
+      ox[k] = ((float)(k - 1) * aspy) * stepSize;
+      oy[k] = ((float)(k - 1) * aspx) * stepSize;
+    }
+    const bool last = i == c->S - 1;
+    const float2 *src = j1final ? c->jump1 : c->jump2;
+    float2 *dst = j1final ? c->jump2 : c->jump1;
+    HIPCHK(c, launch_jfa_step(src, dst, last ? c->dist : nullptr, c->sd, ox, oy, st));
+    j1final = !j1final;
+  }
+  if (T) HIPCHK(c, hipEventRecord(c->ev[2], st));
+
+  // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362)
+  bool gi1final = false;
+  for (int L = c->N - 1; L >= 0; --L) {
+    float4 *srcGI = gi1final ? c->gi1 : c->gi2;
+    float4 *dstGI = gi1final ? c->gi2 : c->gi1;
+    if (T) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
+    RcLevelArgs a;
+    a.upper = (L == c->N - 1) ? nullptr : srcGI;
+    a.out = dstGI;
+    a.dist = c->dist;
+    a.color = c->color_in;
+    a.emissive = c->emissive;
+    a.dirs = c->dirs + dir_table_offset(L);
+    a.sky = c->sky;
+    a.level = L;
+    a.N = c->N;
+    a.ray_range = c->ray_range;
+    a.reflectivity = c->reflectivity;
+    HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
+    if (c->keep_levels)
+      HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], dstGI, (size_t)c->cd.pitch * c->CH * sizeof(float4),
+                               hipMemcpyDeviceToDevice, st));
+    gi1final = !gi1final;
+  }
+  if (T) HIPCHK(c, hipEventRecord(c->ev_level[0], st));
+  if (T) HIPCHK(c, hipEventRecord(c->ev[3], st));
+  float4 *finalGI = gi1final ? c->gi1 : c->gi2;  // RC2DGI.cs:365
+  c->final_gi = gi1final ? 1 : 2;
+
+  // 5. blur + blended copy-back (RC2DGI.cs:367-387)
+  if (c->blur_radius > 0.0f) {
+    HIPCHK(c, launch_blur(finalGI, c->blur, c->cd, c->blur_radius, st));
+    HIPCHK(c, launch_blur_copyback(c->blur, finalGI, c->cd, st));
+  }
+  if (T) HIPCHK(c, hipEventRecord(c->ev[4], st));
+
+  // 6. merge + copy-back (RC2DGI.cs:389-404)
+  HIPCHK(c, launch_merge(c->color_in, finalGI, c->temp, c->color_out, c->sd, c->cd, st));
+  if (T) HIPCHK(c, hipEventRecord(c->ev[5], st));
+  c->frame_done = true;
+  c->have_frame = true;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_sync(rc2dgi_ctx *c) {
+  if (!c) return RC2DGI_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RC2DGI_OK;
+}
+
+int rc2dgi_set_stream(rc2dgi_ctx *c, void *s) {
+  if (!c) return RC2DGI_E_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_set_timing(rc2dgi_ctx *c, int enable) {
+  if (!c) return RC2DGI_E_ARG;
+  c->timing = enable != 0;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_pass_times(rc2dgi_ctx *c, float *pass_ms, int n_pass, float *level_ms, int n_level) {
+  if (!c) return RC2DGI_E_ARG;
+  if (!c->timing || !c->have_frame) return fail(c, RC2DGI_E_STATE, "enable timing and run a frame first");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipEventSynchronize(c->ev[5]));
+  float t[P_COUNT];
+  for (int p = 0; p < P_TOTAL; ++p) HIPCHK(c, hipEventElapsedTime(&t[p], c->ev[p], c->ev[p + 1]));
+  HIPCHK(c, hipEventElapsedTime(&t[P_TOTAL], c->ev[0], c->ev[5]));
+  if (pass_ms)
+    for (int p = 0; p < n_pass && p < P_COUNT; ++p) pass_ms[p] = t[p];
+  if (level_ms)
+    for (int L = 0; L < n_level && L < c->N; ++L)
+      HIPCHK(c, hipEventElapsedTime(&level_ms[L], c->ev_level[L + 1], c->ev_level[L]));
+  return RC2DGI_OK;
+}
+
+int rc2dgi_query(rc2dgi_ctx *c, int *cw, int *ch, int *jfa_steps, int *final_gi) {
+  if (!c) return RC2DGI_E_ARG;
+  if (cw) *cw = c->CW;
+  if (ch) *ch = c->CH;
+  if (jfa_steps) *jfa_steps = c->S;
+  if (final_gi) *final_gi = (c->N % 2 == 0) ? 2 : 1;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_set_direction_table(rc2dgi_ctx *c, int level, const float *cos_sin, int n) {
+  if (!c) return RC2DGI_E_ARG;
+  if (level < 0 || level >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+  if (!cos_sin) {
+    c->dir_override[level].clear();
+  } else {
+    if (n != (4 << (2 * level))) return fail(c, RC2DGI_E_ARG, "direction table must hold 4^(level+1) entries");
+    c->dir_override[level].assign(cos_sin, cos_sin + 2 * (size_t)n);
+  }
+  c->tables_dirty = true;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_set_sky_table(rc2dgi_ctx *c, const float *rgb, int n) {
+  if (!c) return RC2DGI_E_ARG;
+  if (!rgb) {
+    c->sky_override.clear();
+  } else {
+    if (n != (4 << (2 * (c->N - 1)))) return fail(c, RC2DGI_E_ARG, "sky table must hold 4^N entries");
+    c->sky_override.assign(rgb, rgb + 3 * (size_t)n);
+  }
+  c->tables_dirty = true;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_set_keep_levels(rc2dgi_ctx *c, int enable) {
+  if (!c) return RC2DGI_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  free_level_bufs(c);
+  c->keep_levels = enable != 0;
+  if (c->keep_levels) {
+    c->level_bufs.assign(c->N, nullptr);
+    for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, (size_t)c->cd.pitch * c->CH * sizeof(float4)));
+  }
+  return RC2DGI_OK;
+}
+
+int rc2dgi_download_level(rc2dgi_ctx *c, int level, void *host, int pitch_bytes, int format) {
+  if (!c || !host) return fail(c, RC2DGI_E_ARG, "null argument");
+  if (!c->keep_levels || !c->have_frame) return fail(c, RC2DGI_E_STATE, "enable keep_levels and run a frame first");
+  if (level < 0 || level >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+  if (format != RC2DGI_FMT_RGBA32F) return fail(c, RC2DGI_E_UNSUPPORTED, "levels download as RGBA32F");
+  const int row = c->CW * 16;
+  if (pitch_bytes == 0) pitch_bytes = row;
+  if (pitch_bytes < row) return fail(c, RC2DGI_E_ARG, "pitch smaller than a row");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy2D(host, pitch_bytes, c->level_bufs[level], (size_t)c->cd.pitch * 16, row, c->CH,
+                        hipMemcpyDeviceToHost));
+  return RC2DGI_OK;
+}
+
+int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int format) {
+  if (!c || !host) return fail(c, RC2DGI_E_ARG, "null argument");
+  if (which == RC2DGI_RT_FINAL_GI) which = (c->N % 2 == 0) ? RC2DGI_RT_GI2 : RC2DGI_RT_GI1;
+  if (which < RC2DGI_RT_COLOR || which > RC2DGI_RT_BLUR) return fail(c, RC2DGI_E_ARG, "bad render texture id");
+  if (format != RC2DGI_FMT_RGBA32F && format != RC2DGI_FMT_RGBA8) return fail(c, RC2DGI_E_ARG, "bad format");
+  const bool scr = screen_rt(which);
+  const int w = scr ? c->W : c->CW, h = scr ? c->H : c->CH;
+  const int pitch = scr ? c->sd.pitch : c->cd.pitch;
+  const int row = format == RC2DGI_FMT_RGBA32F ? w * 16 : w * 4;
+  if (pitch_bytes == 0) pitch_bytes = row;
+  if (pitch_bytes < row) return fail(c, RC2DGI_E_ARG, "pitch smaller than a row");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<float4> img((size_t)w * h);
+  auto fetch4 = [&](const float4 *src) -> int {
+    HIPCHK(c, hipMemcpy2D(img.data(), (size_t)w * 16, src, (size_t)pitch * 16, (size_t)w * 16, h,
+                          hipMemcpyDeviceToHost));
+    return RC2DGI_OK;
+  };
+  int rc = RC2DGI_OK;
+  const bool n1 = c->N == 1;
+  switch (which) {
+    case RC2DGI_RT_COLOR: rc = fetch4(c->frame_done ? c->color_out : c->color_in); break;
+    case RC2DGI_RT_EMISSIVE: rc = fetch4(c->emissive); break;
+    case RC2DGI_RT_TEMP: rc = fetch4(c->temp); break;
+    case RC2DGI_RT_GI1: rc = fetch4(c->gi1); break;
+    case RC2DGI_RT_BLUR: rc = fetch4(c->blur); break;
+    case RC2DGI_RT_GI2:
+      if (n1) {  // giRT2 is never drawn with one cascade: ClearAllRTs content
+        for (auto &p : img) p = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+      } else {
+        rc = fetch4(c->gi2);
+      }
+      break;
+    case RC2DGI_RT_JUMP1:
+    case RC2DGI_RT_JUMP2: {
+      std::vector<float2> s((size_t)w * h);
+      HIPCHK(c, hipMemcpy2D(s.data(), (size_t)w * 8, which == RC2DGI_RT_JUMP1 ? c->jump1 : c->jump2,
+                            (size_t)pitch * 8, (size_t)w * 8, h, hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < s.size(); ++k) img[k] = make_float4(s[k].x, s[k].y, 0.0f, 1.0f);
+      break;
+    }
+    case RC2DGI_RT_DIST: {
+      std::vector<float> d((size_t)w * h);
+      HIPCHK(c, hipMemcpy2D(d.data(), (size_t)w * 4, c->dist, (size_t)pitch * 4, (size_t)w * 4, h,
+                            hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < d.size(); ++k) {  // re-pack q = 65535 * (q / 65535) (exact)
+        const unsigned q = (unsigned)(d[k] * 65535.0f + 0.5f);
+        img[k] = make_float4((float)((q >> 8) & 255u) / 255.0f, (float)(q & 255u) / 255.0f, 0.0f, 1.0f);
+      }
+      break;
+    }
+    default: return fail(c, RC2DGI_E_ARG, "bad render texture id");
+  }
+  if (rc != RC2DGI_OK) return rc;
+  unsigned char *dst = static_cast<unsigned char *>(host);
+  for (int j = 0; j < h; ++j) {
+    if (format == RC2DGI_FMT_RGBA32F) {
+      std::memcpy(dst + (size_t)j * pitch_bytes, img.data() + (size_t)j * w, (size_t)w * 16);
+    } else {
+      for (int i = 0; i < w; ++i) {
+        const float4 p = img[(size_t)j * w + i];
+        unsigned char *o = dst + (size_t)j * pitch_bytes + 4 * (size_t)i;
+        o[0] = to_unorm8(p.x);
+        o[1] = to_unorm8(p.y);
+        o[2] = to_unorm8(p.z);
+        o[3] = to_unorm8(p.w);
+      }
+    }
+  }
+  return RC2DGI_OK;
+}
+
+}  // extern "C"

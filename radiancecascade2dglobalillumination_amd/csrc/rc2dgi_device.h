@@ -1,0 +1,74 @@
+// rc2dgi_device.h -- device-side GL texture semantics shared by the rc2dgi kernels.
+//
+// The reference samples its render textures through GL (raylib 5.5 state, SURVEY.md
+// Appendix A): NEAREST or LINEAR filtering, REPEAT wrap, fragTexCoord = (i+0.5)/n.
+// These helpers restate that sampling for pitch-linear HBM buffers.  The exact forms
+// (fract-then-scale for non-power-of-two axes, fma lerp, x before y) are the ones the
+// pinned GL implementation uses; every kernel is compiled with -ffp-contract=off so
+// each a*b+c written below is two IEEE roundings, as in the shaders.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace rc2dgi {
+
+struct Axis {
+  int n;     // texels
+  int pow2;  // n is a power of two
+};
+
+__device__ __forceinline__ float texcoord(int i, int n) { return ((float)i + 0.5f) / (float)n; }
+
+// NEAREST + REPEAT texel index
+__device__ __forceinline__ int wrap_nearest(float u, Axis a) {
+  if (a.pow2) return ((int)floorf(u * (float)a.n)) & (a.n - 1);
+  float fr = fminf(u - floorf(u), 0.99999994f);
+  int i = (int)(fr * (float)a.n);
+  return min(i, a.n - 1);
+}
+
+// LINEAR + REPEAT: taps i0/i1 and lerp weight w along one axis
+__device__ __forceinline__ void wrap_linear(float u, Axis a, int &i0, int &i1, float &w) {
+  float x = a.pow2 ? u * (float)a.n - 0.5f : (u - floorf(u)) * (float)a.n - 0.5f;
+  float fl = floorf(x);
+  w = x - fl;
+  int t0 = (int)fl, t1 = t0 + 1;
+  if (a.pow2) {
+    i0 = t0 & (a.n - 1);
+    i1 = t1 & (a.n - 1);
+  } else {
+    i0 = t0 < 0 ? t0 + a.n : (t0 >= a.n ? t0 - a.n : t0);
+    i1 = t1 < 0 ? t1 + a.n : (t1 >= a.n ? t1 - a.n : t1);
+  }
+}
+
+__device__ __forceinline__ float lerp_gl(float a, float b, float w) { return __builtin_fmaf(w, b - a, a); }
+
+__device__ __forceinline__ float4 lerp_gl(float4 a, float4 b, float w) {
+  return make_float4(lerp_gl(a.x, b.x, w), lerp_gl(a.y, b.y, w), lerp_gl(a.z, b.z, w), lerp_gl(a.w, b.w, w));
+}
+
+// texture(T, (u, v)) with LINEAR filtering on a pitch-linear float4 image
+__device__ __forceinline__ float4 sample_bilinear(const float4 *__restrict__ T, int pitch, Axis ax, Axis ay,
+                                                  float u, float v) {
+  int x0, x1, y0, y1;
+  float wx, wy;
+  wrap_linear(u, ax, x0, x1, wx);
+  wrap_linear(v, ay, y0, y1, wy);
+  const float4 t00 = T[(size_t)y0 * pitch + x0], t10 = T[(size_t)y0 * pitch + x1];
+  const float4 t01 = T[(size_t)y1 * pitch + x0], t11 = T[(size_t)y1 * pitch + x1];
+  return lerp_gl(lerp_gl(t00, t10, wx), lerp_gl(t01, t11, wx), wy);
+}
+
+// blend-on-store (SRC_ALPHA, ONE_MINUS_SRC_ALPHA, FUNC_ADD on all four channels)
+__device__ __forceinline__ float4 blend(float4 src, float4 dst) {
+  const float a = src.w, ia = 1.0f - a;
+  return make_float4(src.x * a + dst.x * ia, src.y * a + dst.y * ia, src.z * a + dst.z * ia, src.w * a + dst.w * ia);
+}
+
+// blend over a target cleared to ClearBackground(Black) = (0,0,0,1)
+__device__ __forceinline__ float4 blend_over_black(float4 src) {
+  const float a = src.w, ia = 1.0f - a;
+  return make_float4(src.x * a + 0.0f * ia, src.y * a + 0.0f * ia, src.z * a + 0.0f * ia, src.w * a + 1.0f * ia);
+}
+
+}  // namespace rc2dgi

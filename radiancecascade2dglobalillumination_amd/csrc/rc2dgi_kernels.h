@@ -1,0 +1,55 @@
+// rc2dgi_kernels.h -- host-side launchers for the DoRC2DGI() pass kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace rc2dgi {
+
+struct ScreenDims {
+  int W, H;        // screen texels
+  int pitch;       // row pitch in texels (all screen-size buffers share it)
+  int powW, powH;  // power-of-two flags (GL wrap arithmetic differs)
+};
+
+struct CascadeDims {
+  int CW, CH;
+  int pitch;
+  int powW, powH;
+};
+
+// ScreenUV (shaders/ScreenUV.fs) -> seeds (u, v); (0,0) = no seed
+hipError_t launch_screen_uv(const float4 *color, float2 *seeds, ScreenDims s, hipStream_t st);
+
+// one JumpFlood step (shaders/JumpFlood.fs).  off_x/off_y = vec2(k,k)*_Aspect.yx*_StepSize for
+// k = -1,0,1 (host-computed).  dist != nullptr fuses DistanceField.fs into the step: the stored
+// value is the unpacked 16-bit distance q/65535 the RC pass reads.
+hipError_t launch_jfa_step(const float2 *src, float2 *dst, float *dist, ScreenDims s, const float off_x[3],
+                           const float off_y[3], hipStream_t st);
+
+struct RcLevelArgs {
+  const float4 *upper;   // G_{L+1} (nullptr at the top level)
+  float4 *out;           // G_L
+  const float *dist;     // unpacked distance (screen)
+  const float4 *color;   // colorRT (screen)
+  const float4 *emissive;
+  const float2 *dirs;    // 4^(L+1) (cos, sin)
+  const float4 *sky;     // 4^N sky terms (top level)
+  int level, N;
+  float ray_range, reflectivity;
+};
+
+// one RadianceCascades.fs level
+hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);
+
+// Blur.fs into blur_out, then the default-shader blended copy-back into gi (RC2DGI.cs:367-387)
+hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st);
+hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st);
+
+// merge.fs into temp, then tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
+hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,
+                        CascadeDims c, hipStream_t st);
+
+// format conversion for uploads from device memory: RGBA8 unorm -> float4 (k/255)
+hipError_t launch_unorm8_to_f32(const unsigned char *src, int src_pitch_bytes, float4 *dst, int dst_pitch, int W,
+                                int H, hipStream_t st);
+
+}  // namespace rc2dgi

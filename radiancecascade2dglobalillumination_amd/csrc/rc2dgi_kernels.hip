@@ -1,0 +1,327 @@
+// rc2dgi_kernels.hip -- CDNA4 (gfx950) kernels for the DoRC2DGI() pass chain.
+//
+// Pass  <-  reference
+//   k_screen_uv     shaders/ScreenUV.fs:10-28          (RC2DGI.cs:278-285)
+//   k_jfa_step      shaders/JumpFlood.fs:11-38         (RC2DGI.cs:296-326)
+//                   + shaders/DistanceField.fs:12-34 fused into the last step (RC2DGI.cs:328-340)
+//   k_rc_level      shaders/RadianceCascades.fs:30-161 (RC2DGI.cs:342-362, 408-433)
+//   k_blur          shaders/Blur.fs:11-37              (RC2DGI.cs:367-379)
+//   k_blur_copyback default shader, blended            (RC2DGI.cs:381-386)
+//   k_merge         shaders/merge.fs:10-15 + copy-back (RC2DGI.cs:389-404)
+//
+// Storage in HBM (pitch-linear, GL row order, row 0 = bottom):
+//   colorRT/emissiveRT/tempRT/colorRT_out  float4  (the reference's RGBA, f32 mode)
+//   jumpRT1/2                              float2  (u, v); the reference's B=0, A=1 are implicit
+//   distRT                                 float   q/65535, q = packUNorm16(d): the value
+//                                                  RadianceCascades.fs:30-33 unpacks
+//   giRT1/2, cascadeBlurRT                 float4
+// The floating-point arithmetic follows the shader expressions operation by operation
+// (compiled with -ffp-contract=off), so results are reproducible against the CPU oracle.
+#include "rc2dgi_device.h"
+#include "rc2dgi_kernels.h"
+
+namespace rc2dgi {
+
+static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- ScreenUV
+__global__ __launch_bounds__(256) void k_screen_uv(const float4 *__restrict__ color, float2 *__restrict__ seeds,
+                                                   ScreenDims s) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= s.W || j >= s.H) return;
+  const float u = texcoord(i, s.W), v = texcoord(j, s.H);
+  // fragTexCoord samples its own texel (identity mapping)
+  const float4 c = color[(size_t)j * s.pitch + i];
+  const bool occ = c.x > 0.0f || c.y > 0.0f || c.z > 0.0f;
+  seeds[(size_t)j * s.pitch + i] = occ ? make_float2(u, v) : make_float2(0.0f, 0.0f);
+}
+
+// ---------------------------------------------------------------- JumpFlood (+ DistanceField)
+struct JfaOffsets {
+  float ox[3], oy[3];
+};
+
+__global__ __launch_bounds__(256) void k_jfa_step(const float2 *__restrict__ src, float2 *__restrict__ dst,
+                                                  float *__restrict__ dist, ScreenDims s, JfaOffsets o) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= s.W || j >= s.H) return;
+  const Axis ax{s.W, s.powW}, ay{s.H, s.powH};
+  const float u = texcoord(i, s.W), v = texcoord(j, s.H);
+  float minDist = 1.0f, bx = 0.0f, by = 0.0f;
+#pragma unroll
+  for (int y = 0; y < 3; ++y) {
+    const int tj = wrap_nearest(v + o.oy[y], ay);
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      const int ti = wrap_nearest(u + o.ox[x], ax);
+      const float2 p = src[(size_t)tj * s.pitch + ti];
+      if (p.x != 0.0f && p.y != 0.0f) {
+        const float dx = p.x - u, dy = p.y - v;
+        const float d = dx * dx + dy * dy;
+        if (d < minDist) {
+          minDist = d;
+          bx = p.x;
+          by = p.y;
+        }
+      }
+    }
+  }
+  dst[(size_t)j * s.pitch + i] = make_float2(bx, by);
+  if (dist) {
+    // DistanceField.fs: distance(fragTexCoord, seed) -> packUNorm16 -> (as read back by
+    // RadianceCascades.fs unpackUNorm16) q / 65535
+    const float dx = u - bx, dy = v - by;
+    const float d = sqrtf(dx * dx + dy * dy);
+    const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
+    const unsigned q = (unsigned)(cl * 65535.0f + 0.5f);
+    dist[(size_t)j * s.pitch + i] = (float)q / 65535.0f;
+  }
+}
+
+// ---------------------------------------------------------------- RadianceCascades
+struct RcParams {
+  ScreenDims s;
+  CascadeDims c;
+  int level, bsc, bdx, bdy, tiles_x, tiles_per_block;
+  float CRx, CRy, bdxf, bdyf, bs2;
+  float aspx, aspy, t0, t1, reflectivity;
+};
+
+constexpr int RC_TX = 16, RC_TY = 16;
+
+// SampleRadianceSDF (RadianceCascades.fs:60-92)
+__device__ __forceinline__ float4 sample_radiance_sdf(const RcParams &P, const float *__restrict__ dist,
+                                                      const float4 *__restrict__ color,
+                                                      const float4 *__restrict__ emis, float ox, float oy,
+                                                      float dx, float dy) {
+  const Axis ax{P.s.W, P.s.powW}, ay{P.s.H, P.s.powH};
+  float t = P.t0;
+  float4 hit = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+  for (int it = 0; it < 32; ++it) {
+    const float px = ox + (t * dx) * P.aspy;
+    const float py = oy + (t * dy) * P.aspx;
+    if (t > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f) break;
+    const size_t idx = (size_t)wrap_nearest(py, ay) * P.s.pitch + wrap_nearest(px, ax);
+    const float d = dist[idx];
+    if (d < 0.001f) {
+      const float4 e = emis[idx];
+      if (sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f) {
+        hit = make_float4(e.x, e.y, e.z, 1.0f);
+      } else {
+        const float4 c = color[idx];
+        hit = make_float4(c.x, c.y, c.z, P.reflectivity);
+      }
+      break;
+    }
+    t += d;
+  }
+  return hit;
+}
+
+template <bool TOP>
+__global__ __launch_bounds__(256) void k_rc_level(RcParams P, const float4 *__restrict__ upper,
+                                                  float4 *__restrict__ out, const float *__restrict__ dist,
+                                                  const float4 *__restrict__ color,
+                                                  const float4 *__restrict__ emis,
+                                                  const float2 *__restrict__ dirs,
+                                                  const float4 *__restrict__ sky) {
+  // one workgroup = one RC_TX x RC_TY tile of probes inside one direction block: every
+  // lane traces the same four directions (wave-uniform table loads, coherent rays)
+  const int wg = blockIdx.x;
+  const int bi = wg / P.tiles_per_block;   // blockIndex = blk.x + blk.y * blockSqrtCount
+  const int tile = wg - bi * P.tiles_per_block;
+  const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
+  const int ty = tile / P.tiles_x, tx = tile - ty * P.tiles_x;
+  const int cx = tx * RC_TX + (threadIdx.x & (RC_TX - 1));
+  const int cy = ty * RC_TY + (threadIdx.x / RC_TX);
+  if (cx >= P.bdx || cy >= P.bdy) return;
+  const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
+  const float cxf = (float)cx, cyf = (float)cy;            // coordsInBlock
+  // rayOrigin / _CascadeResolution
+  const float ox = ((cxf + 0.5f) * (float)P.bsc) / P.CRx;
+  const float oy = ((cyf + 0.5f) * (float)P.bsc) / P.CRy;
+  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll 1
+  for (int r = 0; r < 4; ++r) {
+    const int ai = bi * 4 + r;  // angleIndex
+    const float2 dir = dirs[ai];
+    float4 rad = sample_radiance_sdf(P, dist, color, emis, ox, oy, dir.x, dir.y);
+    if (rad.w != 0.0f) {
+      if (!TOP) {
+        // merge with the upper cascade (RadianceCascades.fs:127-148)
+        float px = cxf * 0.5f + 0.25f, py = cyf * 0.5f + 0.25f;
+        const float aif = (float)ai;
+        const float offx = aif - P.bs2 * floorf(aif / P.bs2);
+        const float offy = floorf(aif / P.bs2);
+        px = fminf(fmaxf(px, 0.5f), P.bdxf * 0.5f - 0.5f);
+        py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
+        const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
+        const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
+        const float4 up = sample_bilinear(upper, P.c.pitch, Axis{P.c.CW, P.c.powW}, Axis{P.c.CH, P.c.powH}, sx, sy);
+        rad.x = rad.x + up.x * rad.w;
+        rad.y = rad.y + up.y * rad.w;
+        rad.z = rad.z + up.z * rad.w;
+        rad.w = rad.w * up.w;
+      } else {
+        // top cascade: analytic sky (RadianceCascades.fs:150-154), tabulated per angleIndex
+        const float4 sk = sky[ai];
+        rad.x = rad.x + sk.x;
+        rad.y = rad.y + sk.y;
+        rad.z = rad.z + sk.z;
+      }
+    }
+    acc.x = acc.x + rad.x * 0.25f;
+    acc.y = acc.y + rad.y * 0.25f;
+    acc.z = acc.z + rad.z * 0.25f;
+    acc.w = acc.w + rad.w * 0.25f;
+  }
+  out[(size_t)j * P.c.pitch + i] = blend_over_black(acc);
+}
+
+// ---------------------------------------------------------------- Blur + copy-back
+__global__ __launch_bounds__(256) void k_blur(const float4 *__restrict__ gi, float4 *__restrict__ blur_out,
+                                              CascadeDims c, float radius) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= c.CW || j >= c.CH) return;
+  const Axis ax{c.CW, c.powW}, ay{c.CH, c.powH};
+  const float u = texcoord(i, c.CW), v = texcoord(j, c.CH);
+  const float tsx = 1.0f / (float)c.CW, tsy = 1.0f / (float)c.CH;
+  // Blur.fs:22-34 order: 4 corners, 4 edges, centre
+  const float kx[8] = {-1.f, 1.f, -1.f, 1.f, 0.f, 0.f, -1.f, 1.f};
+  const float ky[8] = {-1.f, -1.f, 1.f, 1.f, -1.f, 1.f, 0.f, 0.f};
+  float4 res = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    float su = u, sv = v, w = 0.250f;
+    if (k < 8) {
+      su = u + (kx[k] * tsx) * radius;
+      sv = v + (ky[k] * tsy) * radius;
+      w = k < 4 ? 0.0625f : 0.125f;
+    }
+    const float4 t = sample_bilinear(gi, c.pitch, ax, ay, su, sv);
+    res.x = res.x + t.x * w;
+    res.y = res.y + t.y * w;
+    res.z = res.z + t.z * w;
+    res.w = res.w + t.w * w;
+  }
+  blur_out[(size_t)j * c.pitch + i] = blend_over_black(res);
+}
+
+__global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict__ blur, float4 *__restrict__ gi,
+                                                       CascadeDims c) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= c.CW || j >= c.CH) return;
+  const float u = texcoord(i, c.CW), v = texcoord(j, c.CH);
+  const float4 s = sample_bilinear(blur, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
+  const size_t o = (size_t)j * c.pitch + i;
+  gi[o] = blend(s, gi[o]);
+}
+
+// ---------------------------------------------------------------- Merge + copy-back
+__global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_in, const float4 *__restrict__ gi,
+                                               float4 *__restrict__ temp, float4 *__restrict__ color_out,
+                                               ScreenDims s, CascadeDims c) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= s.W || j >= s.H) return;
+  const float u = texcoord(i, s.W), v = texcoord(j, s.H);
+  const size_t o = (size_t)j * s.pitch + i;
+  const float4 col = color_in[o];
+  const float4 g = sample_bilinear(gi, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
+  const float4 src = make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
+  const float4 t = blend_over_black(src);  // tempRT as cleared by ClearAllRTs
+  temp[o] = t;
+  color_out[o] = blend(t, col);            // tempRT -> colorRT, default shader, blended
+}
+
+__global__ __launch_bounds__(256) void k_unorm8_to_f32(const unsigned char *__restrict__ src, int src_pitch,
+                                                       float4 *__restrict__ dst, int dst_pitch, int W, int H) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= W || j >= H) return;
+  const uchar4 b = *reinterpret_cast<const uchar4 *>(src + (size_t)j * src_pitch + 4 * (size_t)i);
+  dst[(size_t)j * dst_pitch + i] =
+      make_float4((float)b.x / 255.0f, (float)b.y / 255.0f, (float)b.z / 255.0f, (float)b.w / 255.0f);
+}
+
+// ---------------------------------------------------------------- launchers
+static dim3 grid2d(int w, int h) { return dim3(ceil_div(w, 64), ceil_div(h, 4)); }
+
+hipError_t launch_screen_uv(const float4 *color, float2 *seeds, ScreenDims s, hipStream_t st) {
+  hipLaunchKernelGGL(k_screen_uv, grid2d(s.W, s.H), dim3(256), 0, st, color, seeds, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_jfa_step(const float2 *src, float2 *dst, float *dist, ScreenDims s, const float off_x[3],
+                           const float off_y[3], hipStream_t st) {
+  JfaOffsets o;
+  for (int k = 0; k < 3; ++k) {
+    o.ox[k] = off_x[k];
+    o.oy[k] = off_y[k];
+  }
+  hipLaunchKernelGGL(k_jfa_step, grid2d(s.W, s.H), dim3(256), 0, st, src, dst, dist, s, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
+  RcParams P;
+  P.s = s;
+  P.c = c;
+  P.level = a.level;
+  P.bsc = 1 << a.level;
+  P.bdx = c.CW >> a.level;
+  P.bdy = c.CH >> a.level;
+  P.tiles_x = ceil_div(P.bdx, RC_TX);
+  P.tiles_per_block = P.tiles_x * ceil_div(P.bdy, RC_TY);
+  P.CRx = (float)c.CW;
+  P.CRy = (float)c.CH;
+  P.bdxf = P.CRx / (float)P.bsc;  // blockDim = _CascadeResolution / float(blockSqrtCount)
+  P.bdyf = P.CRy / (float)P.bsc;
+  P.bs2 = (float)(P.bsc * 2);
+  const int mx = s.W > s.H ? s.W : s.H;
+  P.aspx = (float)s.W / (float)mx;  // RC2DGI.cs:273
+  P.aspy = (float)s.H / (float)mx;
+  // CalculateRayRange (RadianceCascades.fs:38-46)
+  const int maxValue = (1 << (a.N * 2)) - 1;
+  const int start = (1 << (a.level * 2)) - 1;
+  const int end = (1 << (a.level * 2 + 2)) - 1;
+  P.t0 = ((float)start / (float)maxValue) * a.ray_range;
+  P.t1 = ((float)end / (float)maxValue) * a.ray_range;
+  P.reflectivity = a.reflectivity;
+  const int nwg = P.tiles_per_block * P.bsc * P.bsc;
+  if (a.level == a.N - 1)
+    hipLaunchKernelGGL(k_rc_level<true>, dim3(nwg), dim3(RC_TX * RC_TY), 0, st, P, a.upper, a.out, a.dist, a.color,
+                       a.emissive, a.dirs, a.sky);
+  else
+    hipLaunchKernelGGL(k_rc_level<false>, dim3(nwg), dim3(RC_TX * RC_TY), 0, st, P, a.upper, a.out, a.dist,
+                       a.color, a.emissive, a.dirs, a.sky);
+  return hipGetLastError();
+}
+
+hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st) {
+  hipLaunchKernelGGL(k_blur, grid2d(c.CW, c.CH), dim3(256), 0, st, gi, blur_out, c, radius);
+  return hipGetLastError();
+}
+
+hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st) {
+  hipLaunchKernelGGL(k_blur_copyback, grid2d(c.CW, c.CH), dim3(256), 0, st, blur, gi, c);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,
+                        CascadeDims c, hipStream_t st) {
+  hipLaunchKernelGGL(k_merge, grid2d(s.W, s.H), dim3(256), 0, st, color_in, gi, temp, color_out, s, c);
+  return hipGetLastError();
+}
+
+hipError_t launch_unorm8_to_f32(const unsigned char *src, int src_pitch_bytes, float4 *dst, int dst_pitch, int W,
+                                int H, hipStream_t st) {
+  hipLaunchKernelGGL(k_unorm8_to_f32, grid2d(W, H), dim3(256), 0, st, src, src_pitch_bytes, dst, dst_pitch, W, H);
+  return hipGetLastError();
+}
+
+}  // namespace rc2dgi

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures (tests/golden/*.npz + manifest.json).
+
+Each fixture is the output of the REFERENCE's own GLSL shaders (read at run time from
+``--ref-shaders``, default /root/reference/shaders) executed by ``oracle/_ref/glref`` on
+Mesa llvmpipe, replaying DoRC2DGI() (RC2DGI.cs:267-406) with raylib's GL state, in the
+fp32 render-texture mode.  Stored per fixture (float32, GL row order):
+
+* inputs        color, emissive (the painted colorRT / emissiveRT)
+* llvmpipe data tc_screen, tc_cascade (interpolated fragTexCoord), dir_tables (cos/sin
+                per level), sky_table (top-level sky term) -- the values the reference
+                shaders actually used, captured with glref --capture-tables
+* outputs       jump_s<k> (every JFA step, small fixtures only), jump1, jump2, dist,
+                gi_L<l> (every cascade level as stored), blur, gi_final (after the
+                blur copy-back), gi1, gi2, temp, color_out
+
+Re-run:  python tests/golden/make_golden.py [--ref-shaders DIR]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from radiancecascade2dglobalillumination_amd import scenes  # noqa: E402
+
+GLREF = os.path.join(ROOT, "oracle", "_ref", "glref")
+
+DEFAULT_UNIFORMS = dict(sky_radiance=1.0, sky_color=(0.5, 0.6, 0.8), sun_color=(1.0, 0.9, 0.6),
+                        sun_angle=0.3, reflectivity=0.0, blur_radius=1.5)
+
+# name, W, H, N, rayRange, scene, uniform overrides, keep JFA steps
+FIXTURES = [
+    ("c0_demo_256", 256, 256, 2, 8.0, "demo", {}, False),
+    ("rand64_n2", 64, 64, 2, 8.0, "rand:0", {}, True),
+    ("rand128x96_n3_refl", 128, 96, 3, 2.0, "rand:1", dict(reflectivity=0.5, sun_angle=1.2), True),
+    ("rand96x64_n2_noblur", 96, 64, 2, 4.0, "rand:2", dict(blur_radius=0.0, sky_radiance=2.0), True),
+    ("rand64x128_n4", 64, 128, 4, 2.0, "rand:3", dict(sky_color=(0.2, 0.9, 0.4), blur_radius=2.5), True),
+    ("empty64_n3", 64, 64, 3, 2.0, "empty", {}, True),
+]
+
+
+def make_scene(spec: str, W: int, H: int):
+    if spec == "demo":
+        return scenes.demo(W, H)
+    if spec == "empty":
+        return scenes.empty(W, H)
+    kind, seed = spec.split(":")
+    assert kind == "rand"
+    return scenes.random_scene(W, H, int(seed))
+
+
+def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
+    u = dict(DEFAULT_UNIFORMS)
+    u.update(over)
+    color, emis = make_scene(scene, W, H)
+    with tempfile.TemporaryDirectory() as d:
+        color.tofile(os.path.join(d, "c.f32"))
+        emis.tofile(os.path.join(d, "e.f32"))
+        uargs = ["--sky-radiance", str(u["sky_radiance"]), "--sky-color", ",".join(map(str, u["sky_color"])),
+                 "--sun-color", ",".join(map(str, u["sun_color"])), "--sun-angle", str(u["sun_angle"]),
+                 "--reflectivity", str(u["reflectivity"]), "--blur-radius", str(u["blur_radius"])]
+        base = ["--w", str(W), "--h", str(H), "--n", str(N), "--out", d]
+        subprocess.run([GLREF, "--ref-shaders", shaders, "--ray-range", str(rr), "--in-color", d + "/c.f32",
+                        "--in-emissive", d + "/e.f32", "--dump", "all"] + base + uargs, check=True)
+        subprocess.run([GLREF, "--capture-tables"] + base + uargs, check=True)
+        meta = json.load(open(os.path.join(d, "glref.json")))
+        CW, CH = meta["CW"], meta["CH"]
+        ld = lambda n, w, h, c=4: np.fromfile(os.path.join(d, n + ".f32"), np.float32).reshape(h, w, c)  # noqa
+        arrs = dict(color=color, emissive=emis,
+                    tc_screen=ld("tc_screen", W, H, 2), tc_cascade=ld("tc_cascade", CW, CH, 2),
+                    dir_tables=np.fromfile(os.path.join(d, "dir_tables.f32"), np.float32).reshape(-1, 2),
+                    sky_table=np.fromfile(os.path.join(d, "sky_table.f32"), np.float32).reshape(-1, 3))
+        for n in ("jump1", "jump2", "dist", "temp", "color_out"):
+            arrs[n] = ld(n, W, H)
+        for n in ("gi1", "gi2", "gi_final"):
+            arrs[n] = ld(n, CW, CH)
+        if u["blur_radius"] > 0:
+            arrs["blur"] = ld("blur", CW, CH)
+        for L in range(N):
+            arrs[f"gi_L{L}"] = ld(f"gi_L{L}", CW, CH)
+        if keep_steps:
+            for k in range(meta["jfa_steps"] + 1):
+                arrs[f"jump_s{k}"] = ld(f"jump_s{k}", W, H)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+    entry = dict(name=name, W=W, H=H, N=N, ray_range=rr, render_scale=1.0, scene=scene, CW=CW, CH=CH,
+                 jfa_steps=meta["jfa_steps"], final_gi=meta["final_gi"], renderer=meta["renderer"],
+                 gl_version=meta["version"], mode=meta["mode"], **u)
+    entry["sky_color"] = list(u["sky_color"])
+    entry["sun_color"] = list(u["sun_color"])
+    return entry
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref-shaders", default="/root/reference/shaders")
+    a = ap.parse_args()
+    if not os.path.exists(GLREF):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    manifest = [run(*f, shaders=a.ref_shaders) for f in FIXTURES]
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    for m in manifest:
+        p = os.path.join(HERE, m["name"] + ".npz")
+        print(f"{m['name']:24s} {os.path.getsize(p) / 1e6:6.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
