@@ -44,7 +44,7 @@ struct rc2dgi_ctx {
   // device buffers (the reference's render textures)
   float4 *color_in = nullptr, *emissive = nullptr, *temp = nullptr, *color_out = nullptr;
   float2 *jump1 = nullptr, *jump2 = nullptr;
-  float *dist = nullptr;
+  unsigned short *dist = nullptr;  // packUNorm16 q
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float2 *dirs = nullptr;  // concatenated per level
   float4 *sky = nullptr;
@@ -141,7 +141,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->color_out, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->jump1, ns * sizeof(float2)));
   HIPCHK(c, alloc(&c->jump2, ns * sizeof(float2)));
-  HIPCHK(c, alloc(&c->dist, ns * sizeof(float)));
+  HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->gi1, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->gi2, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
@@ -642,11 +642,11 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
       break;
     }
     case RC2DGI_RT_DIST: {
-      std::vector<float> d((size_t)w * h);
-      HIPCHK(c, hipMemcpy2D(d.data(), (size_t)w * 4, c->dist, (size_t)pitch * 4, (size_t)w * 4, h,
+      std::vector<unsigned short> d((size_t)w * h);
+      HIPCHK(c, hipMemcpy2D(d.data(), (size_t)w * 2, c->dist, (size_t)pitch * 2, (size_t)w * 2, h,
                             hipMemcpyDeviceToHost));
-      for (size_t k = 0; k < d.size(); ++k) {  // re-pack q = 65535 * (q / 65535) (exact)
-        const unsigned q = (unsigned)(d[k] * 65535.0f + 0.5f);
+      for (size_t k = 0; k < d.size(); ++k) {  // DistanceField.fs packUNorm16 encoding of q
+        const unsigned q = d[k];
         img[k] = make_float4((float)((q >> 8) & 255u) / 255.0f, (float)(q & 255u) / 255.0f, 0.0f, 1.0f);
       }
       break;

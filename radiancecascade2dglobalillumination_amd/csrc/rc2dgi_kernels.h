@@ -21,14 +21,14 @@ hipError_t launch_screen_uv(const float4 *color, float2 *seeds, ScreenDims s, hi
 
 // one JumpFlood step (shaders/JumpFlood.fs).  off_x/off_y = vec2(k,k)*_Aspect.yx*_StepSize for
 // k = -1,0,1 (host-computed).  dist != nullptr fuses DistanceField.fs into the step: the stored
-// value is the unpacked 16-bit distance q/65535 the RC pass reads.
-hipError_t launch_jfa_step(const float2 *src, float2 *dst, float *dist, ScreenDims s, const float off_x[3],
+// value is the 16-bit q of packUNorm16 (the RC pass reads q/65535).
+hipError_t launch_jfa_step(const float2 *src, float2 *dst, unsigned short *dist, ScreenDims s, const float off_x[3],
                            const float off_y[3], hipStream_t st);
 
 struct RcLevelArgs {
   const float4 *upper;   // G_{L+1} (nullptr at the top level)
   float4 *out;           // G_L
-  const float *dist;     // unpacked distance (screen)
+  const unsigned short *dist;  // 16-bit distance q (screen)
   const float4 *color;   // colorRT (screen)
   const float4 *emissive;
   const float2 *dirs;    // 4^(L+1) (cos, sin)

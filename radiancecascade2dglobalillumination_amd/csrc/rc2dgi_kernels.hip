@@ -12,8 +12,8 @@
 // Storage in HBM (pitch-linear, GL row order, row 0 = bottom):
 //   colorRT/emissiveRT/tempRT/colorRT_out  float4  (the reference's RGBA, f32 mode)
 //   jumpRT1/2                              float2  (u, v); the reference's B=0, A=1 are implicit
-//   distRT                                 float   q/65535, q = packUNorm16(d): the value
-//                                                  RadianceCascades.fs:30-33 unpacks
+//   distRT                                 uint16  q = packUNorm16(d) (DistanceField.fs:12-19);
+//                                                  RadianceCascades.fs:30-33 reads q / 65535
 //   giRT1/2, cascadeBlurRT                 float4
 // The floating-point arithmetic follows the shader expressions operation by operation
 // (compiled with -ffp-contract=off), so results are reproducible against the CPU oracle.
@@ -43,7 +43,7 @@ struct JfaOffsets {
 };
 
 __global__ __launch_bounds__(256) void k_jfa_step(const float2 *__restrict__ src, float2 *__restrict__ dst,
-                                                  float *__restrict__ dist, ScreenDims s, JfaOffsets o) {
+                                                  unsigned short *__restrict__ dist, ScreenDims s, JfaOffsets o) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= s.H) return;
@@ -70,13 +70,12 @@ __global__ __launch_bounds__(256) void k_jfa_step(const float2 *__restrict__ src
   }
   dst[(size_t)j * s.pitch + i] = make_float2(bx, by);
   if (dist) {
-    // DistanceField.fs: distance(fragTexCoord, seed) -> packUNorm16 -> (as read back by
-    // RadianceCascades.fs unpackUNorm16) q / 65535
+    // DistanceField.fs: distance(fragTexCoord, seed) -> packUNorm16: store the 16-bit q
+    // (RadianceCascades.fs unpackUNorm16 recovers exactly q / 65535)
     const float dx = u - bx, dy = v - by;
     const float d = sqrtf(dx * dx + dy * dy);
     const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
-    const unsigned q = (unsigned)(cl * 65535.0f + 0.5f);
-    dist[(size_t)j * s.pitch + i] = (float)q / 65535.0f;
+    dist[(size_t)j * s.pitch + i] = (unsigned short)(unsigned)(cl * 65535.0f + 0.5f);
   }
 }
 
@@ -89,68 +88,122 @@ struct RcParams {
   float aspx, aspy, t0, t1, reflectivity;
 };
 
-constexpr int RC_TX = 16, RC_TY = 16;
+// q / 65535 exactly as fp32 division would give it: the double product rounds to the same
+// float for every q in [0, 65535] (checked exhaustively, tests/test_kernels_cpu.py)
+__device__ __forceinline__ float decode_dist(unsigned q) { return (float)((double)q * (1.0 / 65535.0)); }
 
-// SampleRadianceSDF (RadianceCascades.fs:60-92)
-__device__ __forceinline__ float4 sample_radiance_sdf(const RcParams &P, const float *__restrict__ dist,
-                                                      const float4 *__restrict__ color,
-                                                      const float4 *__restrict__ emis, float ox, float oy,
-                                                      float dx, float dy) {
-  const Axis ax{P.s.W, P.s.powW}, ay{P.s.H, P.s.powH};
-  float t = P.t0;
-  float4 hit = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-  for (int it = 0; it < 32; ++it) {
-    const float px = ox + (t * dx) * P.aspy;
-    const float py = oy + (t * dy) * P.aspx;
-    if (t > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f) break;
-    const size_t idx = (size_t)wrap_nearest(py, ay) * P.s.pitch + wrap_nearest(px, ax);
-    const float d = dist[idx];
-    if (d < 0.001f) {
-      const float4 e = emis[idx];
-      if (sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f) {
-        hit = make_float4(e.x, e.y, e.z, 1.0f);
-      } else {
-        const float4 c = color[idx];
-        hit = make_float4(c.x, c.y, c.z, P.reflectivity);
-      }
-      break;
-    }
-    t += d;
-  }
-  return hit;
-}
+// One workgroup = one TX x TY tile of probes (coordsInBlock) inside ONE direction block:
+// every lane traces the same four directions (wave-uniform scalar table loads, parallel
+// rays).  The four rays of a lane are marched in lockstep so each iteration keeps up to
+// four independent distance gathers in flight.  The level-(L+1) bilinear footprint of the
+// tile -- block-local by the reference's clamp -- is staged in LDS once per ray direction.
+template <int TX, int TY, bool TOP>
+__global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *__restrict__ upper,
+                                                     float4 *__restrict__ out,
+                                                     const unsigned short *__restrict__ dist,
+                                                     const float4 *__restrict__ color,
+                                                     const float4 *__restrict__ emis,
+                                                     const float2 *__restrict__ dirs,
+                                                     const float4 *__restrict__ sky) {
+  constexpr int NT = TX * TY;
+  constexpr int RW = TX / 2 + 4, RH = TY / 2 + 4;  // staged footprint (+1 texel margin each side)
+  __shared__ float4 s_up[TOP ? 1 : 4 * RH * RW];
 
-template <bool TOP>
-__global__ __launch_bounds__(256) void k_rc_level(RcParams P, const float4 *__restrict__ upper,
-                                                  float4 *__restrict__ out, const float *__restrict__ dist,
-                                                  const float4 *__restrict__ color,
-                                                  const float4 *__restrict__ emis,
-                                                  const float2 *__restrict__ dirs,
-                                                  const float4 *__restrict__ sky) {
-  // one workgroup = one RC_TX x RC_TY tile of probes inside one direction block: every
-  // lane traces the same four directions (wave-uniform table loads, coherent rays)
   const int wg = blockIdx.x;
-  const int bi = wg / P.tiles_per_block;   // blockIndex = blk.x + blk.y * blockSqrtCount
+  const int bi = wg / P.tiles_per_block;  // blockIndex = blk.x + blk.y * blockSqrtCount
   const int tile = wg - bi * P.tiles_per_block;
   const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
   const int ty = tile / P.tiles_x, tx = tile - ty * P.tiles_x;
-  const int cx = tx * RC_TX + (threadIdx.x & (RC_TX - 1));
-  const int cy = ty * RC_TY + (threadIdx.x / RC_TX);
-  if (cx >= P.bdx || cy >= P.bdy) return;
+  const int cx0 = tx * TX, cy0 = ty * TY;
+  const int cx = cx0 + (int)(threadIdx.x % TX), cy = cy0 + (int)(threadIdx.x / TX);
+  const bool valid = cx < P.bdx && cy < P.bdy;
+
+  // upper block of angleIndex a = 4*bi + r: (a mod 2b, a div 2b) in blocks of (bdx/2, bdy/2)
+  const int ubx = P.bdx >> 1, uby = P.bdy >> 1;
+  const int umask = 2 * P.bsc - 1, ushift = P.level + 1;
+  if (!TOP) {
+    for (int k = threadIdx.x; k < 4 * RH * RW; k += NT) {
+      const int r = k / (RH * RW), rem = k - r * (RH * RW);
+      const int yy = rem / RW, xx = rem - yy * RW;
+      const int a = bi * 4 + r;
+      int gx = (a & umask) * ubx + (cx0 >> 1) - 2 + xx;
+      int gy = (a >> ushift) * uby + (cy0 >> 1) - 2 + yy;
+      gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
+      gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
+      s_up[k] = upper[(size_t)gy * P.c.pitch + gx];
+    }
+    __syncthreads();
+  }
+  if (!valid) return;
+
   const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
   const float cxf = (float)cx, cyf = (float)cy;            // coordsInBlock
-  // rayOrigin / _CascadeResolution
-  const float ox = ((cxf + 0.5f) * (float)P.bsc) / P.CRx;
+  const float ox = ((cxf + 0.5f) * (float)P.bsc) / P.CRx;  // rayOrigin / _CascadeResolution
   const float oy = ((cyf + 0.5f) * (float)P.bsc) / P.CRy;
-  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll 1
+  const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
+
+  // ---- SampleRadianceSDF (RadianceCascades.fs:60-92), four rays in lockstep
+  float rdx[4], rdy[4], t[4];
+  int hit_idx[4];
+  bool act[4];
+#pragma unroll
   for (int r = 0; r < 4; ++r) {
+    const float2 d = dirs[bi * 4 + r];
+    rdx[r] = d.x;
+    rdy[r] = d.y;
+    t[r] = P.t0;
+    hit_idx[r] = -1;
+    act[r] = true;
+  }
+#pragma unroll 1
+  for (int it = 0; it < 32; ++it) {
+    int idx[4];
+    bool live[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float px = ox + (t[r] * rdx[r]) * P.aspy;
+      const float py = oy + (t[r] * rdy[r]) * P.aspx;
+      live[r] = act[r] && !(t[r] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+      act[r] = live[r];
+      idx[r] = live[r] ? wrap_nearest(py, say) * P.s.pitch + wrap_nearest(px, sax) : 0;
+    }
+    unsigned q[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q[r] = dist[idx[r]];
+    bool any = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (live[r]) {
+        const float d = decode_dist(q[r]);
+        if (d < 0.001f) {
+          hit_idx[r] = idx[r];
+          act[r] = false;
+        } else {
+          t[r] += d;
+        }
+      }
+      any |= act[r];
+    }
+    if (!any) break;
+  }
+
+  // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
+  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float4 rad = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+    if (hit_idx[r] >= 0) {
+      const float4 e = emis[hit_idx[r]];
+      if (sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f) {
+        rad = make_float4(e.x, e.y, e.z, 1.0f);
+      } else {
+        const float4 c = color[hit_idx[r]];
+        rad = make_float4(c.x, c.y, c.z, P.reflectivity);
+      }
+    }
     const int ai = bi * 4 + r;  // angleIndex
-    const float2 dir = dirs[ai];
-    float4 rad = sample_radiance_sdf(P, dist, color, emis, ox, oy, dir.x, dir.y);
     if (rad.w != 0.0f) {
       if (!TOP) {
-        // merge with the upper cascade (RadianceCascades.fs:127-148)
         float px = cxf * 0.5f + 0.25f, py = cyf * 0.5f + 0.25f;
         const float aif = (float)ai;
         const float offx = aif - P.bs2 * floorf(aif / P.bs2);
@@ -159,14 +212,26 @@ __global__ __launch_bounds__(256) void k_rc_level(RcParams P, const float4 *__re
         py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
         const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
         const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
-        const float4 up = sample_bilinear(upper, P.c.pitch, Axis{P.c.CW, P.c.powW}, Axis{P.c.CH, P.c.powH}, sx, sy);
+        int x0, x1, y0, y1;
+        float wx, wy;
+        wrap_linear(sx, Axis{P.c.CW, P.c.powW}, x0, x1, wx);
+        wrap_linear(sy, Axis{P.c.CH, P.c.powH}, y0, y1, wy);
+        // taps from the staged footprint (global fallback if rounding ever steps outside it)
+        const int rx0 = (ai & umask) * ubx + (cx0 >> 1) - 2, ry0 = (ai >> ushift) * uby + (cy0 >> 1) - 2;
+        auto tap = [&](int gx, int gy) -> float4 {
+          int lx = gx - rx0, ly = gy - ry0;
+          lx = lx < 0 ? lx + P.c.CW : (lx >= P.c.CW ? lx - P.c.CW : lx);
+          ly = ly < 0 ? ly + P.c.CH : (ly >= P.c.CH ? ly - P.c.CH : ly);
+          if ((unsigned)lx < (unsigned)RW && (unsigned)ly < (unsigned)RH) return s_up[(r * RH + ly) * RW + lx];
+          return upper[(size_t)gy * P.c.pitch + gx];
+        };
+        const float4 up = lerp_gl(lerp_gl(tap(x0, y0), tap(x1, y0), wx), lerp_gl(tap(x0, y1), tap(x1, y1), wx), wy);
         rad.x = rad.x + up.x * rad.w;
         rad.y = rad.y + up.y * rad.w;
         rad.z = rad.z + up.z * rad.w;
         rad.w = rad.w * up.w;
       } else {
-        // top cascade: analytic sky (RadianceCascades.fs:150-154), tabulated per angleIndex
-        const float4 sk = sky[ai];
+        const float4 sk = sky[ai];  // top cascade: analytic sky, tabulated per angleIndex
         rad.x = rad.x + sk.x;
         rad.y = rad.y + sk.y;
         rad.z = rad.z + sk.z;
@@ -256,7 +321,7 @@ hipError_t launch_screen_uv(const float4 *color, float2 *seeds, ScreenDims s, hi
   return hipGetLastError();
 }
 
-hipError_t launch_jfa_step(const float2 *src, float2 *dst, float *dist, ScreenDims s, const float off_x[3],
+hipError_t launch_jfa_step(const float2 *src, float2 *dst, unsigned short *dist, ScreenDims s, const float off_x[3],
                            const float off_y[3], hipStream_t st) {
   JfaOffsets o;
   for (int k = 0; k < 3; ++k) {
@@ -267,6 +332,19 @@ hipError_t launch_jfa_step(const float2 *src, float2 *dst, float *dist, ScreenDi
   return hipGetLastError();
 }
 
+template <int TX, int TY>
+static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
+  P.tiles_x = ceil_div(P.bdx, TX);
+  P.tiles_per_block = P.tiles_x * ceil_div(P.bdy, TY);
+  const int nwg = P.tiles_per_block * P.bsc * P.bsc;
+  if (a.level == a.N - 1)
+    hipLaunchKernelGGL((k_rc_level<TX, TY, true>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out, a.dist,
+                       a.color, a.emissive, a.dirs, a.sky);
+  else
+    hipLaunchKernelGGL((k_rc_level<TX, TY, false>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out, a.dist,
+                       a.color, a.emissive, a.dirs, a.sky);
+}
+
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
   RcParams P;
   P.s = s;
@@ -275,8 +353,6 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.bsc = 1 << a.level;
   P.bdx = c.CW >> a.level;
   P.bdy = c.CH >> a.level;
-  P.tiles_x = ceil_div(P.bdx, RC_TX);
-  P.tiles_per_block = P.tiles_x * ceil_div(P.bdy, RC_TY);
   P.CRx = (float)c.CW;
   P.CRy = (float)c.CH;
   P.bdxf = P.CRx / (float)P.bsc;  // blockDim = _CascadeResolution / float(blockSqrtCount)
@@ -292,13 +368,7 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.t0 = ((float)start / (float)maxValue) * a.ray_range;
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
-  const int nwg = P.tiles_per_block * P.bsc * P.bsc;
-  if (a.level == a.N - 1)
-    hipLaunchKernelGGL(k_rc_level<true>, dim3(nwg), dim3(RC_TX * RC_TY), 0, st, P, a.upper, a.out, a.dist, a.color,
-                       a.emissive, a.dirs, a.sky);
-  else
-    hipLaunchKernelGGL(k_rc_level<false>, dim3(nwg), dim3(RC_TX * RC_TY), 0, st, P, a.upper, a.out, a.dist,
-                       a.color, a.emissive, a.dirs, a.sky);
+  launch_rc_tiles<16, 16>(a, P, st);
   return hipGetLastError();
 }
 
