@@ -84,6 +84,36 @@ def cpu_baseline(W, H, N, rr, budget_s=12.0):
                        f"oracle/rc2dgi_oracle.c, {platform.processor() or platform.machine()})")
 
 
+def sweep_rc(ctx, N, steps, rounds=3):
+    """Per-level HIP-event times of every RC tile variant, interleaved over rounds in one
+    process (cdna_hip_programming.md §5.4 rule 24); prints one JSON line."""
+    import numpy as np
+
+    nv = ctx.get_tuning("rc_variant_count")
+    times = {v: [] for v in range(nv)}
+    for _ in range(rounds):
+        for v in range(nv):
+            ctx.set_tuning("rc_variant", v)
+            ctx.do_rc2dgi()
+            ctx.sync()
+            for _ in range(steps):
+                ctx.do_rc2dgi()
+                times[v].append(ctx.pass_times(levels=N)["levels"])
+    from radiancecascade2dglobalillumination_amd.rc2dgi import load_library
+
+    lib = load_library()
+    med = {v: np.median(np.array(t), axis=0).tolist() for v, t in times.items()}
+    best = [min(range(nv), key=lambda v: med[v][L]) for L in range(N)]
+    print(json.dumps({"sweep": "rc_variant", "levels_ms": {str(v): [round(x, 4) for x in m] for v, m in med.items()},
+                      "best_per_level": best, "best_total_ms": round(sum(med[best[L]][L] for L in range(N)), 4),
+                      "names": [lib_variant_name(v) for v in range(nv)]}), flush=True)
+
+
+def lib_variant_name(v):
+    names = ["16x16x1", "16x8x2", "16x16x2", "32x8x1", "64x4x1", "8x8x1", "32x8x2", "16x4x4", "64x4x2"]
+    return names[v] if v < len(names) else str(v)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,6 +125,9 @@ def main():
     ap.add_argument("--ray-range", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--sweep-rc", action="store_true",
+                    help="time every RC tile variant per level (interleaved rounds) instead of the bench line")
+    ap.add_argument("--scene", default="demo", help="demo | random:<seed>")
     a = ap.parse_args()
 
     import numpy as np
@@ -113,13 +146,19 @@ def main():
     W = a.size
     H = a.height or a.size
     N = a.cascades
-    color, emis = scenes.demo(W, H, t=3.0 + 0.25 * rank)  # one independent scene per rank
+    if a.scene == "demo":
+        color, emis = scenes.demo(W, H, t=3.0 + 0.25 * rank)  # one independent scene per rank
+    else:
+        color, emis = scenes.random_scene(W, H, seed=int(a.scene.split(":")[1]) + rank)
     ctx = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local)
     CW, CH = ctx.cascade_resolution
     # inputs resident in HBM before the timed region
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
     ctx.set_timing(True)
+    if a.sweep_rc:
+        sweep_rc(ctx, N, a.steps, rounds=3)
+        return
     for _ in range(a.warmup):
         ctx.do_rc2dgi()
     ctx.sync()

@@ -136,6 +136,13 @@ int rc2dgi_pass_times(rc2dgi_ctx *ctx, float *pass_ms, int n_pass, float *level_
 int rc2dgi_set_direction_table(rc2dgi_ctx *ctx, int level, const float *cos_sin, int n);
 int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
 
+/* ---- tuning knobs (performance only; results are identical for every value).
+ *   "rc_variant"      RC workgroup tile shape for every level (0 .. rc_variant_count-1)
+ *   "rc_variant_L<n>" the same for level n only
+ * rc2dgi_get_tuning also answers "rc_variant_count". */
+int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
+int rc2dgi_get_tuning(rc2dgi_ctx *ctx, const char *key, int *value);
+
 /* ---- debug views beyond the reference's thumbnails: keep a copy of every cascade level G_L
  * as stored by its pass (costs N extra cascade textures and one copy per level). */
 int rc2dgi_set_keep_levels(rc2dgi_ctx *ctx, int enable);

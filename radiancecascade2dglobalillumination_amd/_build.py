@@ -19,8 +19,10 @@ ARCH = os.environ.get("RC2DGI_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: each a*b+c in the kernels is two IEEE roundings, exactly as the GLSL
 # expressions they restate; the GL lerp's fused multiply-add is written as fmaf explicitly.
+# -disable-promote-alloca-to-lds: per-thread staging arrays stay in VGPRs (the AMDGPU
+# promote-alloca pass would otherwise move them to LDS and serialise the staging loads).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
-         f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
+         f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result", "-mllvm", "-disable-promote-alloca-to-lds"]
 
 
 def hipcc() -> str:

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -58,6 +59,7 @@ struct rc2dgi_ctx {
   bool timing = false;
   hipEvent_t ev[P_COUNT + 1] = {};
   std::vector<hipEvent_t> ev_level;  // N + 1
+  std::vector<int> rc_variant;  // per level tile shape (tuning)
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
   std::string err;
@@ -127,6 +129,12 @@ hipError_t alloc(T **p, size_t bytes) {
   return hipMalloc(reinterpret_cast<void **>(p), bytes);
 }
 
+// measured default tile shape per level (profiles/, bench.py --sweep-rc)
+int default_rc_variant(int level) {
+  (void)level;
+  return 0;
+}
+
 // (re)allocate every render texture for the current W, H, N (RC2DGI.cs:79-98)
 int allocate(rc2dgi_ctx *c) {
   free_buffers(c);
@@ -158,6 +166,8 @@ int allocate(rc2dgi_ctx *c) {
   c->tables_dirty = true;
   c->have_frame = c->frame_done = false;
   c->ev_level.resize(c->N + 1);
+  c->rc_variant.resize(c->N, default_rc_variant(c->N - 1));
+  for (int L = 0; L < c->N; ++L) c->rc_variant[L] = default_rc_variant(L);
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
     for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, nc * sizeof(float4)));
@@ -475,6 +485,7 @@ int rc2dgi_do(rc2dgi_ctx *c) {
     a.N = c->N;
     a.ray_range = c->ray_range;
     a.reflectivity = c->reflectivity;
+    a.variant = c->rc_variant[L];
     HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
     if (c->keep_levels)
       HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], dstGI, (size_t)c->cd.pitch * c->CH * sizeof(float4),
@@ -569,6 +580,39 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *c, const float *rgb, int n) {
   }
   c->tables_dirty = true;
   return RC2DGI_OK;
+}
+
+int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
+  if (!c || !key) return fail(c, RC2DGI_E_ARG, "null argument");
+  std::string k(key);
+  if (k == "rc_variant" || k.rfind("rc_variant_L", 0) == 0) {
+    if (value < 0 || value >= rc_variant_count()) return fail(c, RC2DGI_E_ARG, "rc_variant out of range");
+    if (k == "rc_variant") {
+      for (int &v : c->rc_variant) v = value;
+      return RC2DGI_OK;
+    }
+    const int L = std::atoi(k.c_str() + 12);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    c->rc_variant[L] = value;
+    return RC2DGI_OK;
+  }
+  return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);
+}
+
+int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
+  if (!c || !key || !value) return fail(c, RC2DGI_E_ARG, "null argument");
+  std::string k(key);
+  if (k == "rc_variant_count") {
+    *value = rc_variant_count();
+    return RC2DGI_OK;
+  }
+  if (k.rfind("rc_variant_L", 0) == 0) {
+    const int L = std::atoi(k.c_str() + 12);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    *value = c->rc_variant[L];
+    return RC2DGI_OK;
+  }
+  return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);
 }
 
 int rc2dgi_set_keep_levels(rc2dgi_ctx *c, int enable) {

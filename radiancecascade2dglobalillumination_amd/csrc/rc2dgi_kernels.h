@@ -35,7 +35,11 @@ struct RcLevelArgs {
   const float4 *sky;     // 4^N sky terms (top level)
   int level, N;
   float ray_range, reflectivity;
+  int variant;           // tile shape (rc_variant_name)
 };
+
+int rc_variant_count();
+const char *rc_variant_name(int v);
 
 // one RadianceCascades.fs level
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);

@@ -92,12 +92,26 @@ struct RcParams {
 // float for every q in [0, 65535] (checked exhaustively, tests/test_kernels_cpu.py)
 __device__ __forceinline__ float decode_dist(unsigned q) { return (float)((double)q * (1.0 / 65535.0)); }
 
-// One workgroup = one TX x TY tile of probes (coordsInBlock) inside ONE direction block:
-// every lane traces the same four directions (wave-uniform scalar table loads, parallel
-// rays).  The four rays of a lane are marched in lockstep so each iteration keeps up to
-// four independent distance gathers in flight.  The level-(L+1) bilinear footprint of the
-// tile -- block-local by the reference's clamp -- is staged in LDS once per ray direction.
-template <int TX, int TY, bool TOP>
+// Workgroup order.  Hardware deals consecutive workgroup ids round-robin over the 8 XCDs
+// (each with its own L2), so the physical id is remapped so that every XCD walks one
+// contiguous chunk of the logical order (bijective for any count, cdna_hip_programming.md
+// §5.5 T1).  Logical order is tile-major, direction-minor: the workgroups an XCD runs
+// together trace ALL directions of neighbouring probe tiles, so their distance-field
+// samples stay in a ring around those tiles (L2-resident) instead of sweeping the whole
+// field once per direction.
+__device__ __forceinline__ int xcd_logical_id(int p, int n) {
+  const int q = n >> 3, r = n & 7, x = p & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (p >> 3);
+}
+
+// One workgroup = one TX x (TY*PY) tile of probes (coordsInBlock) inside ONE direction
+// block: every lane traces the same four directions (wave-uniform scalar table loads,
+// parallel rays).  Each lane owns PY probes (TY rows apart) and marches their 4*PY rays in
+// lockstep, so each iteration keeps up to 4*PY independent distance gathers in flight.
+// The level-(L+1) bilinear footprint of the tile -- block-local by the reference's clamp --
+// is staged in LDS once per ray direction; its loads are issued before the march and
+// written to LDS after it (their latency hides under the march).
+template <int TX, int TY, int PY, bool TOP>
 __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *__restrict__ upper,
                                                      float4 *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
@@ -105,144 +119,185 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
                                                      const float4 *__restrict__ emis,
                                                      const float2 *__restrict__ dirs,
                                                      const float4 *__restrict__ sky) {
-  constexpr int NT = TX * TY;
-  constexpr int RW = TX / 2 + 4, RH = TY / 2 + 4;  // staged footprint (+1 texel margin each side)
-  __shared__ float4 s_up[TOP ? 1 : 4 * RH * RW];
+  constexpr int NT = TX * TY, THY = TY * PY, NR = 4 * PY;
+  // staged footprint: taps of c in [c0, c0+T) lie in [c0/2 - 1, c0/2 + T/2]
+  constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
+  constexpr int NSTAGE = 4 * RH * RW;
+  constexpr int PT = (NSTAGE + NT - 1) / NT;
+  __shared__ float4 s_up[TOP ? 1 : NSTAGE];
 
-  const int wg = blockIdx.x;
-  const int bi = wg / P.tiles_per_block;  // blockIndex = blk.x + blk.y * blockSqrtCount
-  const int tile = wg - bi * P.tiles_per_block;
+  const int nblk = P.bsc * P.bsc;
+  const int logical = xcd_logical_id((int)blockIdx.x, (int)gridDim.x);
+  const int tile = logical / nblk;
+  const int bi = logical - tile * nblk;  // blockIndex = blk.x + blk.y * blockSqrtCount
   const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
   const int ty = tile / P.tiles_x, tx = tile - ty * P.tiles_x;
-  const int cx0 = tx * TX, cy0 = ty * TY;
-  const int cx = cx0 + (int)(threadIdx.x % TX), cy = cy0 + (int)(threadIdx.x / TX);
-  const bool valid = cx < P.bdx && cy < P.bdy;
+  const int cx0 = tx * TX, cy0 = ty * THY;
+  const int cx = cx0 + (int)(threadIdx.x % TX);
+  const int cyb = cy0 + (int)(threadIdx.x / TX);
+  const bool xok = cx < P.bdx;
 
   // upper block of angleIndex a = 4*bi + r: (a mod 2b, a div 2b) in blocks of (bdx/2, bdy/2)
   const int ubx = P.bdx >> 1, uby = P.bdy >> 1;
   const int umask = 2 * P.bsc - 1, ushift = P.level + 1;
+  // staged texels as plain float components (HIP's float4 union defeats SROA -> scratch)
+  float stx[TOP ? 1 : PT], sty[TOP ? 1 : PT], stz[TOP ? 1 : PT], stw[TOP ? 1 : PT];
   if (!TOP) {
-    for (int k = threadIdx.x; k < 4 * RH * RW; k += NT) {
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      // unconditional (clamped) loads keep st[] in registers
+      const int k = min((int)threadIdx.x + q * NT, NSTAGE - 1);
       const int r = k / (RH * RW), rem = k - r * (RH * RW);
       const int yy = rem / RW, xx = rem - yy * RW;
       const int a = bi * 4 + r;
-      int gx = (a & umask) * ubx + (cx0 >> 1) - 2 + xx;
-      int gy = (a >> ushift) * uby + (cy0 >> 1) - 2 + yy;
+      int gx = (a & umask) * ubx + (cx0 >> 1) - 1 + xx;
+      int gy = (a >> ushift) * uby + (cy0 >> 1) - 1 + yy;
       gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
       gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
-      s_up[k] = upper[(size_t)gy * P.c.pitch + gx];
+      const float4 v = upper[(size_t)gy * P.c.pitch + gx];  // issued now, consumed after the march
+      stx[q] = v.x;
+      sty[q] = v.y;
+      stz[q] = v.z;
+      stw[q] = v.w;
     }
-    __syncthreads();
   }
-  if (!valid) return;
 
-  const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
-  const float cxf = (float)cx, cyf = (float)cy;            // coordsInBlock
+  const float cxf = (float)cx;
   const float ox = ((cxf + 0.5f) * (float)P.bsc) / P.CRx;  // rayOrigin / _CascadeResolution
-  const float oy = ((cyf + 0.5f) * (float)P.bsc) / P.CRy;
+  float oy[PY];
+  bool pok[PY];
+#pragma unroll
+  for (int p = 0; p < PY; ++p) {
+    const int cy = cyb + p * TY;
+    pok[p] = xok && cy < P.bdy;
+    oy[p] = (((float)cy + 0.5f) * (float)P.bsc) / P.CRy;
+  }
   const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
 
-  // ---- SampleRadianceSDF (RadianceCascades.fs:60-92), four rays in lockstep
-  float rdx[4], rdy[4], t[4];
-  int hit_idx[4];
-  bool act[4];
+  // ---- SampleRadianceSDF (RadianceCascades.fs:60-92), 4*PY rays in lockstep
+  float rdx[4], rdy[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float2 d = dirs[bi * 4 + r];
     rdx[r] = d.x;
     rdy[r] = d.y;
-    t[r] = P.t0;
-    hit_idx[r] = -1;
-    act[r] = true;
+  }
+  float t[NR];
+  int hit_idx[NR];
+  bool act[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    t[k] = P.t0;
+    hit_idx[k] = -1;
+    act[k] = pok[k >> 2];
   }
 #pragma unroll 1
   for (int it = 0; it < 32; ++it) {
-    int idx[4];
-    bool live[4];
+    int idx[NR];
+    bool live[NR];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float px = ox + (t[r] * rdx[r]) * P.aspy;
-      const float py = oy + (t[r] * rdy[r]) * P.aspx;
-      live[r] = act[r] && !(t[r] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
-      act[r] = live[r];
-      idx[r] = live[r] ? wrap_nearest(py, say) * P.s.pitch + wrap_nearest(px, sax) : 0;
+    for (int k = 0; k < NR; ++k) {
+      const int r = k & 3, p = k >> 2;
+      const float px = ox + (t[k] * rdx[r]) * P.aspy;
+      const float py = oy[p] + (t[k] * rdy[r]) * P.aspx;
+      live[k] = act[k] && !(t[k] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+      act[k] = live[k];
+      idx[k] = live[k] ? wrap_nearest(py, say) * P.s.pitch + wrap_nearest(px, sax) : 0;
     }
-    unsigned q[4];
+    unsigned q[NR];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) q[r] = dist[idx[r]];
+    for (int k = 0; k < NR; ++k) q[k] = dist[idx[k]];
     bool any = false;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (live[r]) {
-        const float d = decode_dist(q[r]);
+    for (int k = 0; k < NR; ++k) {
+      if (live[k]) {
+        const float d = decode_dist(q[k]);
         if (d < 0.001f) {
-          hit_idx[r] = idx[r];
-          act[r] = false;
+          hit_idx[k] = idx[k];
+          act[k] = false;
         } else {
-          t[r] += d;
+          t[k] += d;
         }
       }
-      any |= act[r];
+      any |= act[k];
     }
     if (!any) break;
   }
 
-  // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
-  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (!TOP) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float4 rad = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-    if (hit_idx[r] >= 0) {
-      const float4 e = emis[hit_idx[r]];
-      if (sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f) {
-        rad = make_float4(e.x, e.y, e.z, 1.0f);
-      } else {
-        const float4 c = color[hit_idx[r]];
-        rad = make_float4(c.x, c.y, c.z, P.reflectivity);
-      }
+    for (int q = 0; q < PT; ++q) {
+      const int k = (int)threadIdx.x + q * NT;
+      if (k < NSTAGE) s_up[k] = make_float4(stx[q], sty[q], stz[q], stw[q]);
     }
-    const int ai = bi * 4 + r;  // angleIndex
-    if (rad.w != 0.0f) {
-      if (!TOP) {
-        float px = cxf * 0.5f + 0.25f, py = cyf * 0.5f + 0.25f;
-        const float aif = (float)ai;
-        const float offx = aif - P.bs2 * floorf(aif / P.bs2);
-        const float offy = floorf(aif / P.bs2);
-        px = fminf(fmaxf(px, 0.5f), P.bdxf * 0.5f - 0.5f);
-        py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
-        const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
-        const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
-        int x0, x1, y0, y1;
-        float wx, wy;
-        wrap_linear(sx, Axis{P.c.CW, P.c.powW}, x0, x1, wx);
-        wrap_linear(sy, Axis{P.c.CH, P.c.powH}, y0, y1, wy);
-        // taps from the staged footprint (global fallback if rounding ever steps outside it)
-        const int rx0 = (ai & umask) * ubx + (cx0 >> 1) - 2, ry0 = (ai >> ushift) * uby + (cy0 >> 1) - 2;
-        auto tap = [&](int gx, int gy) -> float4 {
-          int lx = gx - rx0, ly = gy - ry0;
-          lx = lx < 0 ? lx + P.c.CW : (lx >= P.c.CW ? lx - P.c.CW : lx);
-          ly = ly < 0 ? ly + P.c.CH : (ly >= P.c.CH ? ly - P.c.CH : ly);
-          if ((unsigned)lx < (unsigned)RW && (unsigned)ly < (unsigned)RH) return s_up[(r * RH + ly) * RW + lx];
-          return upper[(size_t)gy * P.c.pitch + gx];
-        };
-        const float4 up = lerp_gl(lerp_gl(tap(x0, y0), tap(x1, y0), wx), lerp_gl(tap(x0, y1), tap(x1, y1), wx), wy);
-        rad.x = rad.x + up.x * rad.w;
-        rad.y = rad.y + up.y * rad.w;
-        rad.z = rad.z + up.z * rad.w;
-        rad.w = rad.w * up.w;
-      } else {
-        const float4 sk = sky[ai];  // top cascade: analytic sky, tabulated per angleIndex
-        rad.x = rad.x + sk.x;
-        rad.y = rad.y + sk.y;
-        rad.z = rad.z + sk.z;
-      }
-    }
-    acc.x = acc.x + rad.x * 0.25f;
-    acc.y = acc.y + rad.y * 0.25f;
-    acc.z = acc.z + rad.z * 0.25f;
-    acc.w = acc.w + rad.w * 0.25f;
+    __syncthreads();
   }
-  out[(size_t)j * P.c.pitch + i] = blend_over_black(acc);
+
+  // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
+#pragma unroll
+  for (int p = 0; p < PY; ++p) {
+    if (!pok[p]) continue;
+    const int cy = cyb + p * TY;
+    const float cyf = (float)cy;
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = p * 4 + r;
+      float4 rad = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+      if (hit_idx[k] >= 0) {
+        const float4 e = emis[hit_idx[k]];
+        if (sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f) {
+          rad = make_float4(e.x, e.y, e.z, 1.0f);
+        } else {
+          const float4 c = color[hit_idx[k]];
+          rad = make_float4(c.x, c.y, c.z, P.reflectivity);
+        }
+      }
+      const int ai = bi * 4 + r;  // angleIndex
+      if (rad.w != 0.0f) {
+        if (!TOP) {
+          float px = cxf * 0.5f + 0.25f, py = cyf * 0.5f + 0.25f;
+          const float aif = (float)ai;
+          const float offx = aif - P.bs2 * floorf(aif / P.bs2);
+          const float offy = floorf(aif / P.bs2);
+          px = fminf(fmaxf(px, 0.5f), P.bdxf * 0.5f - 0.5f);
+          py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
+          const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
+          const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
+          int x0, x1, y0, y1;
+          float wx, wy;
+          wrap_linear(sx, Axis{P.c.CW, P.c.powW}, x0, x1, wx);
+          wrap_linear(sy, Axis{P.c.CH, P.c.powH}, y0, y1, wy);
+          // taps from the staged footprint (global fallback if rounding ever steps outside it)
+          const int rx0 = (ai & umask) * ubx + (cx0 >> 1) - 1, ry0 = (ai >> ushift) * uby + (cy0 >> 1) - 1;
+          auto tap = [&](int gx, int gy) -> float4 {
+            int lx = gx - rx0, ly = gy - ry0;
+            lx = lx < 0 ? lx + P.c.CW : (lx >= P.c.CW ? lx - P.c.CW : lx);
+            ly = ly < 0 ? ly + P.c.CH : (ly >= P.c.CH ? ly - P.c.CH : ly);
+            if ((unsigned)lx < (unsigned)RW && (unsigned)ly < (unsigned)RH) return s_up[(r * RH + ly) * RW + lx];
+            return upper[(size_t)gy * P.c.pitch + gx];
+          };
+          const float4 up =
+              lerp_gl(lerp_gl(tap(x0, y0), tap(x1, y0), wx), lerp_gl(tap(x0, y1), tap(x1, y1), wx), wy);
+          rad.x = rad.x + up.x * rad.w;
+          rad.y = rad.y + up.y * rad.w;
+          rad.z = rad.z + up.z * rad.w;
+          rad.w = rad.w * up.w;
+        } else {
+          const float4 sk = sky[ai];  // top cascade: analytic sky, tabulated per angleIndex
+          rad.x = rad.x + sk.x;
+          rad.y = rad.y + sk.y;
+          rad.z = rad.z + sk.z;
+        }
+      }
+      acc.x = acc.x + rad.x * 0.25f;
+      acc.y = acc.y + rad.y * 0.25f;
+      acc.z = acc.z + rad.z * 0.25f;
+      acc.w = acc.w + rad.w * 0.25f;
+    }
+    const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
+    out[(size_t)j * P.c.pitch + i] = blend_over_black(acc);
+  }
 }
 
 // ---------------------------------------------------------------- Blur + copy-back
@@ -332,18 +387,24 @@ hipError_t launch_jfa_step(const float2 *src, float2 *dst, unsigned short *dist,
   return hipGetLastError();
 }
 
-template <int TX, int TY>
+template <int TX, int TY, int PY>
 static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
-  P.tiles_per_block = P.tiles_x * ceil_div(P.bdy, TY);
+  P.tiles_per_block = P.tiles_x * ceil_div(P.bdy, TY * PY);
   const int nwg = P.tiles_per_block * P.bsc * P.bsc;
   if (a.level == a.N - 1)
-    hipLaunchKernelGGL((k_rc_level<TX, TY, true>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out, a.dist,
+    hipLaunchKernelGGL((k_rc_level<TX, TY, PY, true>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out, a.dist,
                        a.color, a.emissive, a.dirs, a.sky);
   else
-    hipLaunchKernelGGL((k_rc_level<TX, TY, false>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out, a.dist,
-                       a.color, a.emissive, a.dirs, a.sky);
+    hipLaunchKernelGGL((k_rc_level<TX, TY, PY, false>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out,
+                       a.dist, a.color, a.emissive, a.dirs, a.sky);
 }
+
+// RC tile variants (tuning knob "rc_variant"): probes per workgroup = TX x (TY*PY)
+static const char *kRcVariantNames[] = {"16x16x1", "16x8x2", "16x16x2", "32x8x1", "64x4x1", "8x8x1", "32x8x2",
+                                        "16x4x4", "64x4x2"};
+int rc_variant_count() { return (int)(sizeof(kRcVariantNames) / sizeof(kRcVariantNames[0])); }
+const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
   RcParams P;
@@ -368,7 +429,17 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.t0 = ((float)start / (float)maxValue) * a.ray_range;
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
-  launch_rc_tiles<16, 16>(a, P, st);
+  switch (a.variant) {
+    case 1: launch_rc_tiles<16, 8, 2>(a, P, st); break;
+    case 2: launch_rc_tiles<16, 16, 2>(a, P, st); break;
+    case 3: launch_rc_tiles<32, 8, 1>(a, P, st); break;
+    case 4: launch_rc_tiles<64, 4, 1>(a, P, st); break;
+    case 5: launch_rc_tiles<8, 8, 1>(a, P, st); break;
+    case 6: launch_rc_tiles<32, 8, 2>(a, P, st); break;
+    case 7: launch_rc_tiles<16, 4, 4>(a, P, st); break;
+    case 8: launch_rc_tiles<64, 4, 2>(a, P, st); break;
+    default: launch_rc_tiles<16, 16, 1>(a, P, st); break;
+  }
   return hipGetLastError();
 }
 

@@ -87,6 +87,8 @@ def load_library(path: Optional[str] = None):
         "rc2dgi_set_direction_table": ([vp, ctypes.c_int, fp, ctypes.c_int], ctypes.c_int),
         "rc2dgi_set_sky_table": ([vp, fp, ctypes.c_int], ctypes.c_int),
         "rc2dgi_set_keep_levels": ([vp, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_set_tuning": ([vp, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_get_tuning": ([vp, ctypes.c_char_p, ip], ctypes.c_int),
         "rc2dgi_download_level": ([vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
@@ -255,6 +257,15 @@ class RC2DGI:
         self._check(self._L.rc2dgi_download(self._h, w, out.ctypes.data_as(ctypes.c_void_p),
                                             shape[1] * (4 if fmt == FMT_RGBA8 else 16), fmt), f"download {which}")
         return out
+
+    def set_tuning(self, key: str, value: int) -> None:
+        """Performance knobs (results are identical for every value), e.g. rc_variant."""
+        self._check(self._L.rc2dgi_set_tuning(self._h, key.encode(), int(value)), f"set_tuning {key}")
+
+    def get_tuning(self, key: str) -> int:
+        v = ctypes.c_int()
+        self._check(self._L.rc2dgi_get_tuning(self._h, key.encode(), ctypes.byref(v)), f"get_tuning {key}")
+        return v.value
 
     def set_keep_levels(self, enable: bool = True) -> None:
         """Debug: keep every cascade level G_L as stored by its pass."""
