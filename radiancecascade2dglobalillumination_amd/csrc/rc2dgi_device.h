@@ -18,6 +18,11 @@ struct Axis {
 
 __device__ __forceinline__ float texcoord(int i, int n) { return ((float)i + 0.5f) / (float)n; }
 
+// the same value without a division when n is a power of two ((i+0.5) * 2^-k is exact)
+__device__ __forceinline__ float texcoord(int i, Axis a) {
+  return a.pow2 ? ((float)i + 0.5f) * (1.0f / (float)a.n) : ((float)i + 0.5f) / (float)a.n;
+}
+
 // NEAREST + REPEAT texel index
 __device__ __forceinline__ int wrap_nearest(float u, Axis a) {
   if (a.pow2) return ((int)floorf(u * (float)a.n)) & (a.n - 1);

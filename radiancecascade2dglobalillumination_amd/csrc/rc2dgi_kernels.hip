@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void k_screen_uv(const float4 *__restrict__ co
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= s.H) return;
-  const float u = texcoord(i, s.W), v = texcoord(j, s.H);
+  const float u = texcoord(i, Axis{s.W, s.powW}), v = texcoord(j, Axis{s.H, s.powH});
   // fragTexCoord samples its own texel (identity mapping)
   const float4 c = color[(size_t)j * s.pitch + i];
   const bool occ = c.x > 0.0f || c.y > 0.0f || c.z > 0.0f;
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_jfa_step(const float2 *__restrict__ src
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= s.H) return;
   const Axis ax{s.W, s.powW}, ay{s.H, s.powH};
-  const float u = texcoord(i, s.W), v = texcoord(j, s.H);
+  const float u = texcoord(i, ax), v = texcoord(j, ay);
   float minDist = 1.0f, bx = 0.0f, by = 0.0f;
 #pragma unroll
   for (int y = 0; y < 3; ++y) {
@@ -84,13 +84,24 @@ struct RcParams {
   ScreenDims s;
   CascadeDims c;
   int level, bsc, bdx, bdy, tiles_x, tiles_per_block;
-  float CRx, CRy, bdxf, bdyf, bs2;
+  float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
   float aspx, aspy, t0, t1, reflectivity;
 };
 
-// q / 65535 exactly as fp32 division would give it: the double product rounds to the same
-// float for every q in [0, 65535] (checked exhaustively, tests/test_kernels_cpu.py)
-__device__ __forceinline__ float decode_dist(unsigned q) { return (float)((double)q * (1.0 / 65535.0)); }
+// q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
+// multiply and one fma residual correction reproduce the correctly rounded quotient for every
+// q in [0, 65535] (checked exhaustively with exact rational arithmetic, tests/test_kernels_cpu.py)
+__device__ __forceinline__ float decode_dist(unsigned q) {
+  const float c1 = 1.0f / 65535.0f;
+  const float qf = (float)q;
+  const float x = qf * c1;
+  const float r = __builtin_fmaf(-x, 65535.0f, qf);
+  return __builtin_fmaf(r, c1, x);
+}
+
+// a / n for the shader's divisions by a resolution: for a power-of-two n the quotient is
+// exactly a * (1/n) (both roundings are exact scalings), otherwise a true IEEE division
+__device__ __forceinline__ float div_res(float a, float n, float inv_n, int pow2) { return pow2 ? a * inv_n : a / n; }
 
 // Workgroup order.  Hardware deals consecutive workgroup ids round-robin over the 8 XCDs
 // (each with its own L2), so the physical id is remapped so that every XCD walks one
@@ -163,14 +174,14 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   }
 
   const float cxf = (float)cx;
-  const float ox = ((cxf + 0.5f) * (float)P.bsc) / P.CRx;  // rayOrigin / _CascadeResolution
+  const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P.c.powW);  // rayOrigin / _CascadeResolution
   float oy[PY];
   bool pok[PY];
 #pragma unroll
   for (int p = 0; p < PY; ++p) {
     const int cy = cyb + p * TY;
     pok[p] = xok && cy < P.bdy;
-    oy[p] = (((float)cy + 0.5f) * (float)P.bsc) / P.CRy;
+    oy[p] = div_res(((float)cy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P.c.powH);
   }
   const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
 
@@ -257,13 +268,14 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       if (rad.w != 0.0f) {
         if (!TOP) {
           float px = cxf * 0.5f + 0.25f, py = cyf * 0.5f + 0.25f;
-          const float aif = (float)ai;
-          const float offx = aif - P.bs2 * floorf(aif / P.bs2);
-          const float offy = floorf(aif / P.bs2);
+          // mod(float(angleIndex), 2b) and floor(float(angleIndex) / 2b): exact integers (2b is a
+          // power of two, angleIndex < 2^24)
+          const float offx = (float)(ai & umask);
+          const float offy = (float)(ai >> ushift);
           px = fminf(fmaxf(px, 0.5f), P.bdxf * 0.5f - 0.5f);
           py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
-          const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
-          const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
+          const float sx = div_res(px + offx * (P.bdxf * 0.5f), P.CRx, P.invCRx, P.c.powW);
+          const float sy = div_res(py + offy * (P.bdyf * 0.5f), P.CRy, P.invCRy, P.c.powH);
           int x0, x1, y0, y1;
           float wx, wy;
           wrap_linear(sx, Axis{P.c.CW, P.c.powW}, x0, x1, wx);
@@ -307,7 +319,7 @@ __global__ __launch_bounds__(256) void k_blur(const float4 *__restrict__ gi, flo
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= c.CW || j >= c.CH) return;
   const Axis ax{c.CW, c.powW}, ay{c.CH, c.powH};
-  const float u = texcoord(i, c.CW), v = texcoord(j, c.CH);
+  const float u = texcoord(i, ax), v = texcoord(j, ay);
   const float tsx = 1.0f / (float)c.CW, tsy = 1.0f / (float)c.CH;
   // Blur.fs:22-34 order: 4 corners, 4 edges, centre
   const float kx[8] = {-1.f, 1.f, -1.f, 1.f, 0.f, 0.f, -1.f, 1.f};
@@ -335,7 +347,7 @@ __global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict_
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= c.CW || j >= c.CH) return;
-  const float u = texcoord(i, c.CW), v = texcoord(j, c.CH);
+  const float u = texcoord(i, Axis{c.CW, c.powW}), v = texcoord(j, Axis{c.CH, c.powH});
   const float4 s = sample_bilinear(blur, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
   const size_t o = (size_t)j * c.pitch + i;
   gi[o] = blend(s, gi[o]);
@@ -348,7 +360,7 @@ __global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= s.H) return;
-  const float u = texcoord(i, s.W), v = texcoord(j, s.H);
+  const float u = texcoord(i, Axis{s.W, s.powW}), v = texcoord(j, Axis{s.H, s.powH});
   const size_t o = (size_t)j * s.pitch + i;
   const float4 col = color_in[o];
   const float4 g = sample_bilinear(gi, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
@@ -416,6 +428,8 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.bdy = c.CH >> a.level;
   P.CRx = (float)c.CW;
   P.CRy = (float)c.CH;
+  P.invCRx = 1.0f / P.CRx;  // used only when CW / CH are powers of two (then exact)
+  P.invCRy = 1.0f / P.CRy;
   P.bdxf = P.CRx / (float)P.bsc;  // blockDim = _CascadeResolution / float(blockSqrtCount)
   P.bdyf = P.CRy / (float)P.bsc;
   P.bs2 = (float)(P.bsc * 2);

@@ -322,3 +322,23 @@ def test_timing_reports_passes(RC2DGI):
     assert t["total"] > 0 and all(v >= 0 for k, v in t.items() if k != "levels")
     assert len(t["levels"]) == 4 and sum(t["levels"]) <= t["rc"] * 1.01 + 0.05
     ctx.close()
+
+
+@pytest.mark.parametrize("W,H,N,rr,scene", [(256, 192, 5, 2.0, "rand:40"), (333, 200, 4, 8.0, "demo"),
+                                            (512, 512, 6, 2.0, "demo")])
+def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene):
+    """The tile-shape tuning knob changes the schedule only, never a result."""
+    color, emis = make_scene(scene, W, H)
+    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr), color, emis, keep_levels=True)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
+    ctx.set_keep_levels(True)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    for v in range(ctx.get_tuning("rc_variant_count")):
+        ctx.set_tuning("rc_variant", v)
+        ctx.do_rc2dgi()
+        ctx.sync()
+        for L in range(N):
+            g = ctx.download_level(L)
+            assert np.array_equal(g, fr.gi_levels[L]), f"variant {v} level {L}: {np.count_nonzero(g != fr.gi_levels[L])}"
+    ctx.close()
