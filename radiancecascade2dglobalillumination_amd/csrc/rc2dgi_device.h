@@ -64,6 +64,13 @@ __device__ __forceinline__ float4 sample_bilinear(const float4 *__restrict__ T, 
   return lerp_gl(lerp_gl(t00, t10, wx), lerp_gl(t01, t11, wx), wy);
 }
 
+// a non-temporal 16-byte load (a distinct instruction the compiler will not merge with LDS reads)
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ntload4(const float4 *p) {
+  const v4f_t v = __builtin_nontemporal_load(reinterpret_cast<const v4f_t *>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // blend-on-store (SRC_ALPHA, ONE_MINUS_SRC_ALPHA, FUNC_ADD on all four channels)
 __device__ __forceinline__ float4 blend(float4 src, float4 dst) {
   const float a = src.w, ia = 1.0f - a;

@@ -220,16 +220,12 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
     for (int k = 0; k < NR; ++k) q[k] = dist[idx[k]];
     bool any = false;
 #pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      if (live[k]) {
-        const float d = decode_dist(q[k]);
-        if (d < 0.001f) {
-          hit_idx[k] = idx[k];
-          act[k] = false;
-        } else {
-          t[k] += d;
-        }
-      }
+    for (int k = 0; k < NR; ++k) {  // branch-free: selects, no exec-mask juggling
+      const float d = decode_dist(q[k]);
+      const bool hit = live[k] && d < 0.001f;
+      hit_idx[k] = hit ? idx[k] : hit_idx[k];
+      act[k] = live[k] && !hit;
+      t[k] = act[k] ? t[k] + d : t[k];
       any |= act[k];
     }
     if (!any) break;
@@ -245,11 +241,28 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   }
 
   // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
+  const bool pow2c = P.c.powW && P.c.powH;
 #pragma unroll
   for (int p = 0; p < PY; ++p) {
     if (!pok[p]) continue;
     const int cy = cyb + p * TY;
     const float cyf = (float)cy;
+    // upper sample position inside the level-(L+1) block (RadianceCascades.fs:131-139)
+    float px = cxf * 0.5f + 0.25f, py = cyf * 0.5f + 0.25f;
+    px = fminf(fmaxf(px, 0.5f), P.bdxf * 0.5f - 0.5f);
+    py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
+    // Power-of-two cascade resolution: every quantity below is an exact multiple of 1/4, so
+    // x = samplePos * CW - 0.5 = px - 0.5 + offset*blockDim/2 exactly: the four rays share
+    // the bilinear weights and (relative to their staged footprints) the tap coordinates.
+    int lx0 = 0, ly0 = 0;
+    float wx = 0.0f, wy = 0.0f;
+    if (!TOP && pow2c) {
+      const float fx = floorf(px - 0.5f), fy = floorf(py - 0.5f);
+      wx = (px - 0.5f) - fx;
+      wy = (py - 0.5f) - fy;
+      lx0 = (int)fx - ((cx0 >> 1) - 1);
+      ly0 = (int)fy - ((cy0 >> 1) - 1);
+    }
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -267,30 +280,46 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       const int ai = bi * 4 + r;  // angleIndex
       if (rad.w != 0.0f) {
         if (!TOP) {
-          float px = cxf * 0.5f + 0.25f, py = cyf * 0.5f + 0.25f;
-          // mod(float(angleIndex), 2b) and floor(float(angleIndex) / 2b): exact integers (2b is a
-          // power of two, angleIndex < 2^24)
-          const float offx = (float)(ai & umask);
-          const float offy = (float)(ai >> ushift);
-          px = fminf(fmaxf(px, 0.5f), P.bdxf * 0.5f - 0.5f);
-          py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
-          const float sx = div_res(px + offx * (P.bdxf * 0.5f), P.CRx, P.invCRx, P.c.powW);
-          const float sy = div_res(py + offy * (P.bdyf * 0.5f), P.CRy, P.invCRy, P.c.powH);
-          int x0, x1, y0, y1;
-          float wx, wy;
-          wrap_linear(sx, Axis{P.c.CW, P.c.powW}, x0, x1, wx);
-          wrap_linear(sy, Axis{P.c.CH, P.c.powH}, y0, y1, wy);
-          // taps from the staged footprint (global fallback if rounding ever steps outside it)
-          const int rx0 = (ai & umask) * ubx + (cx0 >> 1) - 1, ry0 = (ai >> ushift) * uby + (cy0 >> 1) - 1;
-          auto tap = [&](int gx, int gy) -> float4 {
-            int lx = gx - rx0, ly = gy - ry0;
-            lx = lx < 0 ? lx + P.c.CW : (lx >= P.c.CW ? lx - P.c.CW : lx);
-            ly = ly < 0 ? ly + P.c.CH : (ly >= P.c.CH ? ly - P.c.CH : ly);
-            if ((unsigned)lx < (unsigned)RW && (unsigned)ly < (unsigned)RH) return s_up[(r * RH + ly) * RW + lx];
-            return upper[(size_t)gy * P.c.pitch + gx];
-          };
-          const float4 up =
-              lerp_gl(lerp_gl(tap(x0, y0), tap(x1, y0), wx), lerp_gl(tap(x0, y1), tap(x1, y1), wx), wy);
+          float4 t00, t10, t01, t11;
+          float ux = wx, uy = wy;
+          if (pow2c) {
+            const float4 *sr = s_up + r * RH * RW;
+            t00 = sr[ly0 * RW + lx0];
+            t10 = sr[ly0 * RW + lx0 + 1];
+            t01 = sr[(ly0 + 1) * RW + lx0];
+            t11 = sr[(ly0 + 1) * RW + lx0 + 1];
+          } else {
+            // general GL path (mod(float(angleIndex), 2b), floor(float(angleIndex)/2b) are exact integers)
+            const float offx = (float)(ai & umask), offy = (float)(ai >> ushift);
+            const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
+            const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
+            int x0, x1, y0, y1;
+            wrap_linear(sx, Axis{P.c.CW, 0}, x0, x1, ux);
+            wrap_linear(sy, Axis{P.c.CH, 0}, y0, y1, uy);
+            const int rx0 = (ai & umask) * ubx + (cx0 >> 1) - 1, ry0 = (ai >> ushift) * uby + (cy0 >> 1) - 1;
+            auto rel = [](int g, int o, int n) {
+              int l = g - o;
+              return l < 0 ? l + n : (l >= n ? l - n : l);
+            };
+            const int a0 = rel(x0, rx0, P.c.CW), a1 = rel(x1, rx0, P.c.CW);
+            const int b0 = rel(y0, ry0, P.c.CH), b1 = rel(y1, ry0, P.c.CH);
+            if ((unsigned)a0 < (unsigned)RW && (unsigned)a1 < (unsigned)RW && (unsigned)b0 < (unsigned)RH &&
+                (unsigned)b1 < (unsigned)RH) {
+              const float4 *sr = s_up + r * RH * RW;
+              t00 = sr[b0 * RW + a0];
+              t10 = sr[b0 * RW + a1];
+              t01 = sr[b1 * RW + a0];
+              t11 = sr[b1 * RW + a1];
+            } else {
+              // rounding stepped outside the staged footprint: read HBM.  Non-temporal loads
+              // keep the compiler from fusing this path with the LDS path into flat loads.
+              t00 = ntload4(&upper[(size_t)y0 * P.c.pitch + x0]);
+              t10 = ntload4(&upper[(size_t)y0 * P.c.pitch + x1]);
+              t01 = ntload4(&upper[(size_t)y1 * P.c.pitch + x0]);
+              t11 = ntload4(&upper[(size_t)y1 * P.c.pitch + x1]);
+            }
+          }
+          const float4 up = lerp_gl(lerp_gl(t00, t10, ux), lerp_gl(t01, t11, ux), uy);
           rad.x = rad.x + up.x * rad.w;
           rad.y = rad.y + up.y * rad.w;
           rad.z = rad.z + up.z * rad.w;
