@@ -40,17 +40,26 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) -> str:
+    """extra: additional compiler flags (diagnostic builds go to a different `out`)."""
+    if not force and out == LIB and not _stale():
         return LIB
-    cmd = [hipcc()] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"]
+    cmd = [hipcc()] + FLAGS + list(extra) + ["-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"]
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+
+    if len(sys.argv) > 1 and sys.argv[1] == "diag":
+        # timing-only ablation build: march capped at N iterations (WRONG results by design)
+        n = sys.argv[2] if len(sys.argv) > 2 else "6"
+        print(build(force=True, verbose=True, extra=[f"-DRC2DGI_DIAG_MAX_ITERS={n}"],
+                    out=os.path.join(HERE, f"librc2dgi_diag{n}.so")))
+    else:
+        print(build(force=True, verbose=True))

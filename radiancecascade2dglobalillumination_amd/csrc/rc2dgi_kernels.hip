@@ -202,10 +202,14 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
     hit_idx[k] = -1;
     act[k] = pok[k >> 2];
   }
+#ifndef RC2DGI_DIAG_MAX_ITERS
+#define RC2DGI_DIAG_MAX_ITERS 32  // RadianceCascades.fs:64 (diagnostic builds may cap it; never shipped)
+#endif
 #pragma unroll 1
-  for (int it = 0; it < 32; ++it) {
+  for (int it = 0; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
     int idx[NR];
     bool live[NR];
+    bool any_live = false;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       const int r = k & 3, p = k >> 2;
@@ -213,8 +217,10 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       const float py = oy[p] + (t[k] * rdy[r]) * P.aspx;
       live[k] = act[k] && !(t[k] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
       act[k] = live[k];
+      any_live |= live[k];
       idx[k] = live[k] ? wrap_nearest(py, say) * P.s.pitch + wrap_nearest(px, sax) : 0;
     }
+    if (!any_live) break;  // every ray left its interval or the screen: no more samples
     unsigned q[NR];
 #pragma unroll
     for (int k = 0; k < NR; ++k) q[k] = dist[idx[k]];
