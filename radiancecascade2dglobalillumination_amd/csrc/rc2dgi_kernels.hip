@@ -115,14 +115,16 @@ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (p >> 3);
 }
 
-// One workgroup = one TX x (TY*PY) tile of probes (coordsInBlock) inside ONE direction
-// block: every lane traces the same four directions (wave-uniform scalar table loads,
-// parallel rays).  Each lane owns PY probes (TY rows apart) and marches their 4*PY rays in
-// lockstep, so each iteration keeps up to 4*PY independent distance gathers in flight.
-// The level-(L+1) bilinear footprint of the tile -- block-local by the reference's clamp --
-// is staged in LDS once per ray direction; its loads are issued before the march and
-// written to LDS after it (their latency hides under the march).
-template <int TX, int TY, int PY, bool TOP>
+// One workgroup = one TX x (TY*PY) tile of probes (coordsInBlock) and PD consecutive direction
+// blocks.  Every lane traces the same 4*PD directions (wave-uniform scalar table loads, parallel
+// rays); a lane owns PY probes (TY rows apart) and marches their 4*PY*PD rays in lockstep, so
+// each iteration keeps up to that many independent distance gathers in flight.  Rays of one
+// probe in neighbouring directions sample nearly the same texels (their lengths are highly
+// correlated too), so PD > 1 turns most of the extra gathers into L1 hits.
+// The level-(L+1) bilinear footprint of the tile -- block-local by the reference's clamp -- is
+// staged in LDS once per ray direction; its loads are issued before the march and written to
+// LDS after it (their latency hides under the march).
+template <int TX, int TY, int PY, int PD, bool TOP, bool MASKED>
 __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *__restrict__ upper,
                                                      float4 *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
@@ -130,18 +132,17 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
                                                      const float4 *__restrict__ emis,
                                                      const float2 *__restrict__ dirs,
                                                      const float4 *__restrict__ sky) {
-  constexpr int NT = TX * TY, THY = TY * PY, NR = 4 * PY;
+  constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
   // staged footprint: taps of c in [c0, c0+T) lie in [c0/2 - 1, c0/2 + T/2]
   constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
-  constexpr int NSTAGE = 4 * RH * RW;
+  constexpr int NSTAGE = ND * RH * RW;
   constexpr int PT = (NSTAGE + NT - 1) / NT;
   __shared__ float4 s_up[TOP ? 1 : NSTAGE];
 
-  const int nblk = P.bsc * P.bsc;
+  const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
   const int logical = xcd_logical_id((int)blockIdx.x, (int)gridDim.x);
-  const int tile = logical / nblk;
-  const int bi = logical - tile * nblk;  // blockIndex = blk.x + blk.y * blockSqrtCount
-  const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
+  const int tile = logical / ngrp;
+  const int bi0 = (logical - tile * ngrp) * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
   const int ty = tile / P.tiles_x, tx = tile - ty * P.tiles_x;
   const int cx0 = tx * TX, cy0 = ty * THY;
   const int cx = cx0 + (int)(threadIdx.x % TX);
@@ -156,11 +157,11 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   if (!TOP) {
 #pragma unroll
     for (int q = 0; q < PT; ++q) {
-      // unconditional (clamped) loads keep st[] in registers
+      // unconditional (clamped) loads keep the staging arrays in registers
       const int k = min((int)threadIdx.x + q * NT, NSTAGE - 1);
-      const int r = k / (RH * RW), rem = k - r * (RH * RW);
+      const int r = k / (RH * RW), rem = k - r * (RH * RW);  // r indexes the 4*PD directions
       const int yy = rem / RW, xx = rem - yy * RW;
-      const int a = bi * 4 + r;
+      const int a = bi0 * 4 + r;
       int gx = (a & umask) * ubx + (cx0 >> 1) - 1 + xx;
       int gy = (a >> ushift) * uby + (cy0 >> 1) - 1 + yy;
       gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
@@ -185,11 +186,11 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   }
   const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
 
-  // ---- SampleRadianceSDF (RadianceCascades.fs:60-92), 4*PY rays in lockstep
-  float rdx[4], rdy[4];
+  // ---- SampleRadianceSDF (RadianceCascades.fs:60-92), NR rays in lockstep; ray k = p*ND + r
+  float rdx[ND], rdy[ND];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float2 d = dirs[bi * 4 + r];
+  for (int r = 0; r < ND; ++r) {
+    const float2 d = dirs[bi0 * 4 + r];
     rdx[r] = d.x;
     rdy[r] = d.y;
   }
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   for (int k = 0; k < NR; ++k) {
     t[k] = P.t0;
     hit_idx[k] = -1;
-    act[k] = pok[k >> 2];
+    act[k] = pok[k / ND];
   }
 #ifndef RC2DGI_DIAG_MAX_ITERS
 #define RC2DGI_DIAG_MAX_ITERS 32  // RadianceCascades.fs:64 (diagnostic builds may cap it; never shipped)
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
     bool any_live = false;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
-      const int r = k & 3, p = k >> 2;
+      const int r = k % ND, p = k / ND;
       const float px = ox + (t[k] * rdx[r]) * P.aspy;
       const float py = oy[p] + (t[k] * rdy[r]) * P.aspx;
       live[k] = act[k] && !(t[k] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
@@ -223,7 +224,14 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
     if (!any_live) break;  // every ray left its interval or the screen: no more samples
     unsigned q[NR];
 #pragma unroll
-    for (int k = 0; k < NR; ++k) q[k] = dist[idx[k]];
+    for (int k = 0; k < NR; ++k) {
+      if (MASKED) {
+        q[k] = 0xFFFFu;  // dead rays issue no load (exec-masked lanes generate no requests)
+        if (live[k]) q[k] = dist[idx[k]];
+      } else {
+        q[k] = dist[idx[k]];  // dead rays re-read texel 0 (one cached line)
+      }
+    }
     bool any = false;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {  // branch-free: selects, no exec-mask juggling
@@ -258,8 +266,8 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
     px = fminf(fmaxf(px, 0.5f), P.bdxf * 0.5f - 0.5f);
     py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
     // Power-of-two cascade resolution: every quantity below is an exact multiple of 1/4, so
-    // x = samplePos * CW - 0.5 = px - 0.5 + offset*blockDim/2 exactly: the four rays share
-    // the bilinear weights and (relative to their staged footprints) the tap coordinates.
+    // x = samplePos * CW - 0.5 = px - 0.5 + offset*blockDim/2 exactly: all rays share the
+    // bilinear weights and (relative to their staged footprints) the tap coordinates.
     int lx0 = 0, ly0 = 0;
     float wx = 0.0f, wy = 0.0f;
     if (!TOP && pow2c) {
@@ -269,81 +277,87 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       lx0 = (int)fx - ((cx0 >> 1) - 1);
       ly0 = (int)fy - ((cy0 >> 1) - 1);
     }
-    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = p * 4 + r;
-      float4 rad = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-      if (hit_idx[k] >= 0) {
-        const float4 e = emis[hit_idx[k]];
-        if (sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f) {
-          rad = make_float4(e.x, e.y, e.z, 1.0f);
-        } else {
-          const float4 c = color[hit_idx[k]];
-          rad = make_float4(c.x, c.y, c.z, P.reflectivity);
-        }
-      }
-      const int ai = bi * 4 + r;  // angleIndex
-      if (rad.w != 0.0f) {
-        if (!TOP) {
-          float4 t00, t10, t01, t11;
-          float ux = wx, uy = wy;
-          if (pow2c) {
-            const float4 *sr = s_up + r * RH * RW;
-            t00 = sr[ly0 * RW + lx0];
-            t10 = sr[ly0 * RW + lx0 + 1];
-            t01 = sr[(ly0 + 1) * RW + lx0];
-            t11 = sr[(ly0 + 1) * RW + lx0 + 1];
+    for (int dblk = 0; dblk < PD; ++dblk) {
+      const int bi = bi0 + dblk;
+      float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int r = dblk * 4 + r4;  // index into the 4*PD directions
+        const int k = p * ND + r;
+        float4 rad = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+        if (hit_idx[k] >= 0) {
+          const float4 e = emis[hit_idx[k]];
+          if (sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f) {
+            rad = make_float4(e.x, e.y, e.z, 1.0f);
           } else {
-            // general GL path (mod(float(angleIndex), 2b), floor(float(angleIndex)/2b) are exact integers)
-            const float offx = (float)(ai & umask), offy = (float)(ai >> ushift);
-            const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
-            const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
-            int x0, x1, y0, y1;
-            wrap_linear(sx, Axis{P.c.CW, 0}, x0, x1, ux);
-            wrap_linear(sy, Axis{P.c.CH, 0}, y0, y1, uy);
-            const int rx0 = (ai & umask) * ubx + (cx0 >> 1) - 1, ry0 = (ai >> ushift) * uby + (cy0 >> 1) - 1;
-            auto rel = [](int g, int o, int n) {
-              int l = g - o;
-              return l < 0 ? l + n : (l >= n ? l - n : l);
-            };
-            const int a0 = rel(x0, rx0, P.c.CW), a1 = rel(x1, rx0, P.c.CW);
-            const int b0 = rel(y0, ry0, P.c.CH), b1 = rel(y1, ry0, P.c.CH);
-            if ((unsigned)a0 < (unsigned)RW && (unsigned)a1 < (unsigned)RW && (unsigned)b0 < (unsigned)RH &&
-                (unsigned)b1 < (unsigned)RH) {
-              const float4 *sr = s_up + r * RH * RW;
-              t00 = sr[b0 * RW + a0];
-              t10 = sr[b0 * RW + a1];
-              t01 = sr[b1 * RW + a0];
-              t11 = sr[b1 * RW + a1];
-            } else {
-              // rounding stepped outside the staged footprint: read HBM.  Non-temporal loads
-              // keep the compiler from fusing this path with the LDS path into flat loads.
-              t00 = ntload4(&upper[(size_t)y0 * P.c.pitch + x0]);
-              t10 = ntload4(&upper[(size_t)y0 * P.c.pitch + x1]);
-              t01 = ntload4(&upper[(size_t)y1 * P.c.pitch + x0]);
-              t11 = ntload4(&upper[(size_t)y1 * P.c.pitch + x1]);
-            }
+            const float4 c = color[hit_idx[k]];
+            rad = make_float4(c.x, c.y, c.z, P.reflectivity);
           }
-          const float4 up = lerp_gl(lerp_gl(t00, t10, ux), lerp_gl(t01, t11, ux), uy);
-          rad.x = rad.x + up.x * rad.w;
-          rad.y = rad.y + up.y * rad.w;
-          rad.z = rad.z + up.z * rad.w;
-          rad.w = rad.w * up.w;
-        } else {
-          const float4 sk = sky[ai];  // top cascade: analytic sky, tabulated per angleIndex
-          rad.x = rad.x + sk.x;
-          rad.y = rad.y + sk.y;
-          rad.z = rad.z + sk.z;
         }
+        const int ai = bi * 4 + r4;  // angleIndex
+        if (rad.w != 0.0f) {
+          if (!TOP) {
+            float4 t00, t10, t01, t11;
+            float ux = wx, uy = wy;
+            if (pow2c) {
+              const float4 *sr = s_up + r * RH * RW;
+              t00 = sr[ly0 * RW + lx0];
+              t10 = sr[ly0 * RW + lx0 + 1];
+              t01 = sr[(ly0 + 1) * RW + lx0];
+              t11 = sr[(ly0 + 1) * RW + lx0 + 1];
+            } else {
+              // general GL path (mod(float(angleIndex), 2b), floor(float(angleIndex)/2b) are exact integers)
+              const float offx = (float)(ai & umask), offy = (float)(ai >> ushift);
+              const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
+              const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
+              int x0, x1, y0, y1;
+              wrap_linear(sx, Axis{P.c.CW, 0}, x0, x1, ux);
+              wrap_linear(sy, Axis{P.c.CH, 0}, y0, y1, uy);
+              const int rx0 = (ai & umask) * ubx + (cx0 >> 1) - 1, ry0 = (ai >> ushift) * uby + (cy0 >> 1) - 1;
+              auto rel = [](int g, int o, int n) {
+                int l = g - o;
+                return l < 0 ? l + n : (l >= n ? l - n : l);
+              };
+              const int a0 = rel(x0, rx0, P.c.CW), a1 = rel(x1, rx0, P.c.CW);
+              const int b0 = rel(y0, ry0, P.c.CH), b1 = rel(y1, ry0, P.c.CH);
+              if ((unsigned)a0 < (unsigned)RW && (unsigned)a1 < (unsigned)RW && (unsigned)b0 < (unsigned)RH &&
+                  (unsigned)b1 < (unsigned)RH) {
+                const float4 *sr = s_up + r * RH * RW;
+                t00 = sr[b0 * RW + a0];
+                t10 = sr[b0 * RW + a1];
+                t01 = sr[b1 * RW + a0];
+                t11 = sr[b1 * RW + a1];
+              } else {
+                // rounding stepped outside the staged footprint: read HBM.  Non-temporal loads
+                // keep the compiler from fusing this path with the LDS path into flat loads.
+                t00 = ntload4(&upper[(size_t)y0 * P.c.pitch + x0]);
+                t10 = ntload4(&upper[(size_t)y0 * P.c.pitch + x1]);
+                t01 = ntload4(&upper[(size_t)y1 * P.c.pitch + x0]);
+                t11 = ntload4(&upper[(size_t)y1 * P.c.pitch + x1]);
+              }
+            }
+            const float4 up = lerp_gl(lerp_gl(t00, t10, ux), lerp_gl(t01, t11, ux), uy);
+            rad.x = rad.x + up.x * rad.w;
+            rad.y = rad.y + up.y * rad.w;
+            rad.z = rad.z + up.z * rad.w;
+            rad.w = rad.w * up.w;
+          } else {
+            const float4 sk = sky[ai];  // top cascade: analytic sky, tabulated per angleIndex
+            rad.x = rad.x + sk.x;
+            rad.y = rad.y + sk.y;
+            rad.z = rad.z + sk.z;
+          }
+        }
+        acc.x = acc.x + rad.x * 0.25f;
+        acc.y = acc.y + rad.y * 0.25f;
+        acc.z = acc.z + rad.z * 0.25f;
+        acc.w = acc.w + rad.w * 0.25f;
       }
-      acc.x = acc.x + rad.x * 0.25f;
-      acc.y = acc.y + rad.y * 0.25f;
-      acc.z = acc.z + rad.z * 0.25f;
-      acc.w = acc.w + rad.w * 0.25f;
+      const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
+      const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
+      out[(size_t)j * P.c.pitch + i] = blend_over_black(acc);
     }
-    const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
-    out[(size_t)j * P.c.pitch + i] = blend_over_black(acc);
   }
 }
 
@@ -434,22 +448,24 @@ hipError_t launch_jfa_step(const float2 *src, float2 *dst, unsigned short *dist,
   return hipGetLastError();
 }
 
-template <int TX, int TY, int PY>
+template <int TX, int TY, int PY, int PD = 1, bool MASKED = false>
 static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
   P.tiles_per_block = P.tiles_x * ceil_div(P.bdy, TY * PY);
-  const int nwg = P.tiles_per_block * P.bsc * P.bsc;
+  const int nwg = P.tiles_per_block * P.bsc * P.bsc / PD;
   if (a.level == a.N - 1)
-    hipLaunchKernelGGL((k_rc_level<TX, TY, PY, true>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out, a.dist,
-                       a.color, a.emissive, a.dirs, a.sky);
+    hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, true, MASKED>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper,
+                       a.out, a.dist, a.color, a.emissive, a.dirs, a.sky);
   else
-    hipLaunchKernelGGL((k_rc_level<TX, TY, PY, false>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out,
-                       a.dist, a.color, a.emissive, a.dirs, a.sky);
+    hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, false, MASKED>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper,
+                       a.out, a.dist, a.color, a.emissive, a.dirs, a.sky);
 }
 
-// RC tile variants (tuning knob "rc_variant"): probes per workgroup = TX x (TY*PY)
-static const char *kRcVariantNames[] = {"16x16x1", "16x8x2", "16x16x2", "32x8x1", "64x4x1", "8x8x1", "32x8x2",
-                                        "16x4x4", "64x4x2"};
+// RC tile variants (tuning knob "rc_variant"): TXxTYxPY probes per workgroup, "dD" = D direction
+// blocks per workgroup (needs 4^level >= D; falls back to d1 below that)
+static const char *kRcVariantNames[] = {"16x16x1", "16x8x2",   "16x16x2",  "32x8x1",   "64x4x1",
+                                        "8x8x1",   "32x8x2",   "16x16x1d2", "16x16x1d4", "16x8x1d2",
+                                        "32x8x1d2", "16x8x1d4", "8x8x1d4"};
 int rc_variant_count() { return (int)(sizeof(kRcVariantNames) / sizeof(kRcVariantNames[0])); }
 const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
@@ -478,6 +494,7 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.t0 = ((float)start / (float)maxValue) * a.ray_range;
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
+  const int nblk = P.bsc * P.bsc;
   switch (a.variant) {
     case 1: launch_rc_tiles<16, 8, 2>(a, P, st); break;
     case 2: launch_rc_tiles<16, 16, 2>(a, P, st); break;
@@ -485,8 +502,12 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
     case 4: launch_rc_tiles<64, 4, 1>(a, P, st); break;
     case 5: launch_rc_tiles<8, 8, 1>(a, P, st); break;
     case 6: launch_rc_tiles<32, 8, 2>(a, P, st); break;
-    case 7: launch_rc_tiles<16, 4, 4>(a, P, st); break;
-    case 8: launch_rc_tiles<64, 4, 2>(a, P, st); break;
+    case 7: nblk >= 2 ? launch_rc_tiles<16, 16, 1, 2>(a, P, st) : launch_rc_tiles<16, 16, 1>(a, P, st); break;
+    case 8: nblk >= 4 ? launch_rc_tiles<16, 16, 1, 4>(a, P, st) : launch_rc_tiles<16, 16, 1>(a, P, st); break;
+    case 9: nblk >= 2 ? launch_rc_tiles<16, 8, 1, 2>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
+    case 10: nblk >= 2 ? launch_rc_tiles<32, 8, 1, 2>(a, P, st) : launch_rc_tiles<32, 8, 1>(a, P, st); break;
+    case 11: nblk >= 4 ? launch_rc_tiles<16, 8, 1, 4>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
+    case 12: nblk >= 4 ? launch_rc_tiles<8, 8, 1, 4>(a, P, st) : launch_rc_tiles<8, 8, 1>(a, P, st); break;
     default: launch_rc_tiles<16, 16, 1>(a, P, st); break;
   }
   return hipGetLastError();
