@@ -60,8 +60,6 @@ struct rc2dgi_ctx {
   hipEvent_t ev[P_COUNT + 1] = {};
   std::vector<hipEvent_t> ev_level;  // N + 1
   std::vector<int> rc_variant;  // per level tile shape (tuning)
-  std::vector<unsigned short *> poly;  // per level polyphase distance copies (nullptr = off)
-  int poly_min_level = 3;              // tuning: first level using a polyphase copy
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
   std::string err;
@@ -112,15 +110,8 @@ void free_level_bufs(rc2dgi_ctx *c) {
   c->level_bufs.clear();
 }
 
-void free_poly(rc2dgi_ctx *c) {
-  for (unsigned short *p : c->poly)
-    if (p) (void)hipFree(p);
-  c->poly.clear();
-}
-
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
-  free_poly(c);
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky};
   for (void *p : bufs)
@@ -176,12 +167,6 @@ int allocate(rc2dgi_ctx *c) {
   c->have_frame = c->frame_done = false;
   c->ev_level.resize(c->N + 1);
   c->rc_variant.resize(c->N, default_rc_variant(c->N - 1));
-  {  // polyphase copies where the probe lattice is sparse (b >= 8) and the screen tiles evenly
-    c->poly.assign(c->N, nullptr);
-    for (int L = c->poly_min_level; L < c->N; ++L)
-      if (L >= 1 && (c->W % (1 << L)) == 0 && (c->H % (1 << L)) == 0)
-        HIPCHK(c, alloc(&c->poly[L], (size_t)c->W * c->H * sizeof(unsigned short)));
-  }
   for (int L = 0; L < c->N; ++L) c->rc_variant[L] = default_rc_variant(L);
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
@@ -482,9 +467,6 @@ int rc2dgi_do(rc2dgi_ctx *c) {
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[2], st));
 
-  for (int L = 0; L < c->N; ++L)
-    if (c->poly[L]) HIPCHK(c, launch_polyphase(c->dist, c->sd.pitch, c->W, c->H, L, c->poly[L], st));
-
   // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362)
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
@@ -504,7 +486,6 @@ int rc2dgi_do(rc2dgi_ctx *c) {
     a.ray_range = c->ray_range;
     a.reflectivity = c->reflectivity;
     a.variant = c->rc_variant[L];
-    a.poly = c->poly[L];
     HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
     if (c->keep_levels)
       HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], dstGI, (size_t)c->cd.pitch * c->CH * sizeof(float4),
@@ -613,18 +594,6 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     const int L = std::atoi(k.c_str() + 12);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
     c->rc_variant[L] = value;
-    return RC2DGI_OK;
-  }
-  if (k == "poly_min_level") {
-    if (value < 1 || value > 16) return fail(c, RC2DGI_E_ARG, "poly_min_level must be in 1..16");
-    c->poly_min_level = value;
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    free_poly(c);
-    c->poly.assign(c->N, nullptr);
-    for (int L = c->poly_min_level; L < c->N; ++L)
-      if ((c->W % (1 << L)) == 0 && (c->H % (1 << L)) == 0)
-        HIPCHK(c, alloc(&c->poly[L], (size_t)c->W * c->H * sizeof(unsigned short)));
     return RC2DGI_OK;
   }
   return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);

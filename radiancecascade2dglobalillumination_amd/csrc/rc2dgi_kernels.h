@@ -36,12 +36,7 @@ struct RcLevelArgs {
   int level, N;
   float ray_range, reflectivity;
   int variant;           // tile shape (rc_variant_name)
-  const unsigned short *poly;  // polyphase copy of dist with factor 2^level, or nullptr
 };
-
-// polyphase copy of the 16-bit distance field with phase factor 2^k (W, H multiples of 2^k)
-hipError_t launch_polyphase(const unsigned short *dist, int pitch, int W, int H, int k, unsigned short *out,
-                            hipStream_t st);
 
 int rc_variant_count();
 const char *rc_variant_name(int v);

@@ -86,17 +86,7 @@ struct RcParams {
   int level, bsc, bdx, bdy, tiles_x, tiles_per_block;
   float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
   float aspx, aspy, t0, t1, reflectivity;
-  // polyphase copy of the distance field for the first march step (nullptr = not used):
-  // texel (X, Y) lives at ((Y & m) * b + (X & m)) * sub_w * sub_h + (Y >> k) * sub_w + (X >> k)
-  const unsigned short *poly;
-  int poly_k, poly_sub_w, poly_sub_h;
 };
-
-// Polyphase index of screen texel (X, Y) for phase factor b = 2^k
-__device__ __forceinline__ int poly_index(int X, int Y, int k, int sub_w, int sub_h) {
-  const int m = (1 << k) - 1;
-  return (((Y & m) << k) + (X & m)) * (sub_w * sub_h) + (Y >> k) * sub_w + (X >> k);
-}
 
 // q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
 // multiply and one fma residual correction reproduce the correctly rounded quotient for every
@@ -218,7 +208,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
 #endif
 #pragma unroll 1
   for (int it = 0; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
-    int idx[NR], pidx[NR];
+    int idx[NR];
     bool live[NR];
     bool any_live = false;
 #pragma unroll
@@ -229,26 +219,17 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       live[k] = act[k] && !(t[k] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
       act[k] = live[k];
       any_live |= live[k];
-      const int X = wrap_nearest(px, sax), Y = wrap_nearest(py, say);
-      idx[k] = live[k] ? Y * P.s.pitch + X : 0;
-      // first step: every lane of the wave samples the probe lattice (spacing 2^level) shifted by
-      // t0*dir -- contiguous in the polyphase copy (same texel, same value)
-      pidx[k] = live[k] ? poly_index(X, Y, P.poly_k, P.poly_sub_w, P.poly_sub_h) : 0;
+      idx[k] = live[k] ? wrap_nearest(py, say) * P.s.pitch + wrap_nearest(px, sax) : 0;
     }
     if (!any_live) break;  // every ray left its interval or the screen: no more samples
     unsigned q[NR];
-    if (it == 0 && P.poly) {
 #pragma unroll
-      for (int k = 0; k < NR; ++k) q[k] = P.poly[pidx[k]];
-    } else {
-#pragma unroll
-      for (int k = 0; k < NR; ++k) {
-        if (MASKED) {
-          q[k] = 0xFFFFu;  // dead rays issue no load (exec-masked lanes generate no requests)
-          if (live[k]) q[k] = dist[idx[k]];
-        } else {
-          q[k] = dist[idx[k]];  // dead rays re-read texel 0 (one cached line)
-        }
+    for (int k = 0; k < NR; ++k) {
+      if (MASKED) {
+        q[k] = 0xFFFFu;  // dead rays issue no load (exec-masked lanes generate no requests)
+        if (live[k]) q[k] = dist[idx[k]];
+      } else {
+        q[k] = dist[idx[k]];  // dead rays re-read texel 0 (one cached line)
       }
     }
     bool any = false;
@@ -378,27 +359,6 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       out[(size_t)j * P.c.pitch + i] = blend_over_black(acc);
     }
   }
-}
-
-// ---------------------------------------------------------------- polyphase distance field
-// out[poly_index(X, Y)] = dist[Y][X] for phase factor 2^k (W, H multiples of 2^k).  One thread
-// per output texel: coalesced writes, strided reads.
-__global__ __launch_bounds__(256) void k_polyphase(const unsigned short *__restrict__ dist, int pitch, int W, int H,
-                                                   int k, unsigned short *__restrict__ out) {
-  const int o = blockIdx.x * 256 + threadIdx.x;
-  if (o >= W * H) return;
-  const int sub_w = W >> k, sub_h = H >> k, per = sub_w * sub_h;
-  const int phase = o / per, rem = o - phase * per;
-  const int sy = rem / sub_w, sx = rem - sy * sub_w;
-  const int m = (1 << k) - 1;
-  const int X = (sx << k) + (phase & m), Y = (sy << k) + (phase >> k);
-  out[o] = dist[(size_t)Y * pitch + X];
-}
-
-hipError_t launch_polyphase(const unsigned short *dist, int pitch, int W, int H, int k, unsigned short *out,
-                            hipStream_t st) {
-  hipLaunchKernelGGL(k_polyphase, dim3(ceil_div(W * H, 256)), dim3(256), 0, st, dist, pitch, W, H, k, out);
-  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- Blur + copy-back
@@ -534,10 +494,6 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.t0 = ((float)start / (float)maxValue) * a.ray_range;
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
-  P.poly = a.poly;
-  P.poly_k = a.level;
-  P.poly_sub_w = s.W >> a.level;
-  P.poly_sub_h = s.H >> a.level;
   const int nblk = P.bsc * P.bsc;
   switch (a.variant) {
     case 1: launch_rc_tiles<16, 8, 2>(a, P, st); break;

@@ -342,20 +342,3 @@ def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene):
             g = ctx.download_level(L)
             assert np.array_equal(g, fr.gi_levels[L]), f"variant {v} level {L}: {np.count_nonzero(g != fr.gi_levels[L])}"
     ctx.close()
-
-
-@pytest.mark.parametrize("poly_min", [1, 2, 3, 16])
-def test_polyphase_first_step_is_bit_identical(RC2DGI, poly_min):
-    """The polyphase copy of the distance field (first march step) is a re-indexing only."""
-    W, H, N, rr = 256, 256, 6, 2.0
-    color, emis = make_scene("demo", W, H)
-    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr), color, emis, keep_levels=True)
-    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
-    ctx.set_tuning("poly_min_level", poly_min)
-    ctx.set_keep_levels(True)
-    ctx.frame(color, emis)
-    ctx.sync()
-    for L in range(N):
-        assert np.array_equal(ctx.download_level(L), fr.gi_levels[L]), f"level {L}"
-    assert np.array_equal(ctx.download("color"), fr.color_out)
-    ctx.close()
