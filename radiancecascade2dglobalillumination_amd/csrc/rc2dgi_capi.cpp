@@ -44,7 +44,9 @@ struct rc2dgi_ctx {
   CascadeDims cd{};
   // device buffers (the reference's render textures)
   float4 *color_in = nullptr, *emissive = nullptr, *temp = nullptr, *color_out = nullptr;
-  float2 *jump1 = nullptr, *jump2 = nullptr;
+  unsigned *jump1 = nullptr, *jump2 = nullptr;  // packed seeds
+  unsigned *occ = nullptr;                      // ScreenUV occupancy mask
+  int mpitch = 0;                               // mask row pitch (words)
   unsigned short *dist = nullptr;  // packUNorm16 q
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float2 *dirs = nullptr;  // concatenated per level
@@ -112,12 +114,13 @@ void free_level_bufs(rc2dgi_ctx *c) {
 
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
-  void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist,
+  void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   c->color_in = c->emissive = c->temp = c->color_out = nullptr;
   c->jump1 = c->jump2 = nullptr;
+  c->occ = nullptr;
   c->dist = nullptr;
   c->gi1 = c->gi2 = c->blur = nullptr;
   c->dirs = nullptr;
@@ -147,8 +150,10 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->emissive, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->temp, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->color_out, ns * sizeof(float4)));
-  HIPCHK(c, alloc(&c->jump1, ns * sizeof(float2)));
-  HIPCHK(c, alloc(&c->jump2, ns * sizeof(float2)));
+  HIPCHK(c, alloc(&c->jump1, ns * sizeof(unsigned)));
+  HIPCHK(c, alloc(&c->jump2, ns * sizeof(unsigned)));
+  c->mpitch = ((c->W + 63) / 64) * 2;
+  HIPCHK(c, alloc(&c->occ, (size_t)c->mpitch * c->H * sizeof(unsigned)));
   HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->gi1, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->gi2, nc * sizeof(float4)));
@@ -445,8 +450,10 @@ int rc2dgi_do(rc2dgi_ctx *c) {
   const int mx = c->W > c->H ? c->W : c->H;
   const float aspx = (float)c->W / (float)mx, aspy = (float)c->H / (float)mx;
 
-  // 1. ScreenUV -> jumpRT1 (RC2DGI.cs:276-285)
-  HIPCHK(c, launch_screen_uv(c->color_in, c->jump1, c->sd, st));
+  // 1. ScreenUV (RC2DGI.cs:276-285): occupancy mask; J0 itself is only materialised when a
+  //    single JFA step leaves it visible in jumpRT1
+  HIPCHK(c, launch_occupancy(c->color_in, c->occ, c->mpitch, c->sd, st));
+  if (c->S == 1) HIPCHK(c, launch_seeds_from_mask(c->occ, c->mpitch, c->jump1, c->sd, st));
   if (T) HIPCHK(c, hipEventRecord(c->ev[1], st));
 
   // 2. JumpFlood ping-pong (RC2DGI.cs:287-326); 3. DistanceField fused into the last step
@@ -460,9 +467,10 @@ int rc2dgi_do(rc2dgi_ctx *c) {
       oy[k] = ((float)(k - 1) * aspx) * stepSize;
     }
     const bool last = i == c->S - 1;
-    const float2 *src = j1final ? c->jump1 : c->jump2;
-    float2 *dst = j1final ? c->jump2 : c->jump1;
-    HIPCHK(c, launch_jfa_step(src, dst, last ? c->dist : nullptr, c->sd, ox, oy, st));
+    const unsigned *src = i == 0 ? c->occ : (j1final ? c->jump1 : c->jump2);
+    unsigned *dst = j1final ? c->jump2 : c->jump1;
+    HIPCHK(c, launch_jfa_step(i == 0, src, i == 0 ? c->mpitch : c->sd.pitch, dst, last ? c->dist : nullptr, c->sd,
+                              ox, oy, st));
     j1final = !j1final;
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[2], st));
@@ -678,11 +686,18 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
       }
       break;
     case RC2DGI_RT_JUMP1:
-    case RC2DGI_RT_JUMP2: {
-      std::vector<float2> s((size_t)w * h);
-      HIPCHK(c, hipMemcpy2D(s.data(), (size_t)w * 8, which == RC2DGI_RT_JUMP1 ? c->jump1 : c->jump2,
-                            (size_t)pitch * 8, (size_t)w * 8, h, hipMemcpyDeviceToHost));
-      for (size_t k = 0; k < s.size(); ++k) img[k] = make_float4(s[k].x, s[k].y, 0.0f, 1.0f);
+    case RC2DGI_RT_JUMP2: {  // packed seed -> the reference's (u, v, 0, 1), (0,0,0,1) = no seed
+      std::vector<unsigned> s((size_t)w * h);
+      HIPCHK(c, hipMemcpy2D(s.data(), (size_t)w * 4, which == RC2DGI_RT_JUMP1 ? c->jump1 : c->jump2,
+                            (size_t)pitch * 4, (size_t)w * 4, h, hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < s.size(); ++k) {
+        if (s[k] == 0xFFFFFFFFu) {
+          img[k] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+        } else {
+          const int si = (int)(s[k] & 0xFFFFu), sj = (int)(s[k] >> 16);
+          img[k] = make_float4(((float)si + 0.5f) / (float)w, ((float)sj + 0.5f) / (float)h, 0.0f, 1.0f);
+        }
+      }
       break;
     }
     case RC2DGI_RT_DIST: {

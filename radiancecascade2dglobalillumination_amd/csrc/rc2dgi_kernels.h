@@ -16,14 +16,17 @@ struct CascadeDims {
   int powW, powH;
 };
 
-// ScreenUV (shaders/ScreenUV.fs) -> seeds (u, v); (0,0) = no seed
-hipError_t launch_screen_uv(const float4 *color, float2 *seeds, ScreenDims s, hipStream_t st);
+// ScreenUV (shaders/ScreenUV.fs) as a 1-bit occupancy mask (row pitch mpitch 32-bit words)
+hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, ScreenDims s, hipStream_t st);
+// the ScreenUV seed texture J0 (packed seeds) from the mask
+hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *seeds, ScreenDims s, hipStream_t st);
 
-// one JumpFlood step (shaders/JumpFlood.fs).  off_x/off_y = vec2(k,k)*_Aspect.yx*_StepSize for
-// k = -1,0,1 (host-computed).  dist != nullptr fuses DistanceField.fs into the step: the stored
-// value is the 16-bit q of packUNorm16 (the RC pass reads q/65535).
-hipError_t launch_jfa_step(const float2 *src, float2 *dst, unsigned short *dist, ScreenDims s, const float off_x[3],
-                           const float off_y[3], hipStream_t st);
+// one JumpFlood step (shaders/JumpFlood.fs) over packed seeds (sj<<16 | si, 0xFFFFFFFF = none).
+// first: src is the occupancy mask (pitch in words), else packed seeds (pitch in texels).
+// off_x/off_y = vec2(k,k)*_Aspect.yx*_StepSize for k = -1,0,1 (host-computed).
+// dist != nullptr fuses DistanceField.fs: stores the 16-bit q of packUNorm16.
+hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
+                           ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st);
 
 struct RcLevelArgs {
   const float4 *upper;   // G_{L+1} (nullptr at the top level)

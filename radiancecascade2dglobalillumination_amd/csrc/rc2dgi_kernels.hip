@@ -1,7 +1,7 @@
 // rc2dgi_kernels.hip -- CDNA4 (gfx950) kernels for the DoRC2DGI() pass chain.
 //
 // Pass  <-  reference
-//   k_screen_uv     shaders/ScreenUV.fs:10-28          (RC2DGI.cs:278-285)
+//   k_occupancy     shaders/ScreenUV.fs:10-28          (RC2DGI.cs:278-285), as a 1-bit mask
 //   k_jfa_step      shaders/JumpFlood.fs:11-38         (RC2DGI.cs:296-326)
 //                   + shaders/DistanceField.fs:12-34 fused into the last step (RC2DGI.cs:328-340)
 //   k_rc_level      shaders/RadianceCascades.fs:30-161 (RC2DGI.cs:342-362, 408-433)
@@ -11,7 +11,9 @@
 //
 // Storage in HBM (pitch-linear, GL row order, row 0 = bottom):
 //   colorRT/emissiveRT/tempRT/colorRT_out  float4  (the reference's RGBA, f32 mode)
-//   jumpRT1/2                              float2  (u, v); the reference's B=0, A=1 are implicit
+//   jumpRT1/2                              uint32  packed seed texel (sj<<16 | si); the reference's
+//                                                  (u, v) = ((si+0.5)/W, (sj+0.5)/H), B=0, A=1
+//   ScreenUV seeds (J0)                    1 bit   occupancy mask read by the first JFA step
 //   distRT                                 uint16  q = packUNorm16(d) (DistanceField.fs:12-19);
 //                                                  RadianceCascades.fs:30-33 reads q / 65535
 //   giRT1/2, cascadeBlurRT                 float4
@@ -25,16 +27,40 @@ namespace rc2dgi {
 static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
 // ---------------------------------------------------------------- ScreenUV
-__global__ __launch_bounds__(256) void k_screen_uv(const float4 *__restrict__ color, float2 *__restrict__ seeds,
-                                                   ScreenDims s) {
+// jumpRT texels hold a packed seed: (sj << 16) | si for the seed texel (si, sj), whose value in the
+// reference is its fragTexCoord ((si+0.5)/W, (sj+0.5)/H); kNoSeed is the reference's (0,0).
+constexpr unsigned kNoSeed = 0xFFFFFFFFu;
+
+__device__ __forceinline__ unsigned pack_seed(int si, int sj) { return ((unsigned)sj << 16) | (unsigned)si; }
+
+// ScreenUV.fs:19 `any(greaterThan(color.rgb, 0))` as a 1-bit occupancy mask (one 64-texel ballot
+// per wave; mask row pitch s.mpitch words).  The seed texture J0 itself is never observable when
+// the JFA runs >= 2 steps (step 1 overwrites jumpRT1), so step 0 reads the mask instead.
+__global__ __launch_bounds__(256) void k_occupancy(const float4 *__restrict__ color, unsigned *__restrict__ mask,
+                                                   ScreenDims s, int mpitch) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  bool occ = false;
+  if (i < s.W && j < s.H) {
+    const float4 c = color[(size_t)j * s.pitch + i];
+    occ = c.x > 0.0f || c.y > 0.0f || c.z > 0.0f;
+  }
+  const unsigned long long b = __ballot(occ);
+  if ((threadIdx.x & 63) == 0 && j < s.H) {
+    unsigned *row = mask + (size_t)j * mpitch + (blockIdx.x * 2);
+    row[0] = (unsigned)b;
+    row[1] = (unsigned)(b >> 32);
+  }
+}
+
+// J0 materialised from the mask (only needed when the JFA has a single step)
+__global__ __launch_bounds__(256) void k_seeds_from_mask(const unsigned *__restrict__ mask, int mpitch,
+                                                         unsigned *__restrict__ seeds, ScreenDims s) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= s.H) return;
-  const float u = texcoord(i, Axis{s.W, s.powW}), v = texcoord(j, Axis{s.H, s.powH});
-  // fragTexCoord samples its own texel (identity mapping)
-  const float4 c = color[(size_t)j * s.pitch + i];
-  const bool occ = c.x > 0.0f || c.y > 0.0f || c.z > 0.0f;
-  seeds[(size_t)j * s.pitch + i] = occ ? make_float2(u, v) : make_float2(0.0f, 0.0f);
+  const bool occ = (mask[(size_t)j * mpitch + (i >> 5)] >> (i & 31)) & 1u;
+  seeds[(size_t)j * s.pitch + i] = occ ? pack_seed(i, j) : kNoSeed;
 }
 
 // ---------------------------------------------------------------- JumpFlood (+ DistanceField)
@@ -42,33 +68,46 @@ struct JfaOffsets {
   float ox[3], oy[3];
 };
 
-__global__ __launch_bounds__(256) void k_jfa_step(const float2 *__restrict__ src, float2 *__restrict__ dst,
-                                                  unsigned short *__restrict__ dist, ScreenDims s, JfaOffsets o) {
+// One JumpFlood.fs step.  FIRST: taps read the occupancy mask (the ScreenUV seeds); otherwise the
+// packed seeds of the previous step.  dist != nullptr fuses DistanceField.fs.
+template <bool FIRST>
+__global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ src, int src_pitch,
+                                                  unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
+                                                  ScreenDims s, JfaOffsets o) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= s.H) return;
   const Axis ax{s.W, s.powW}, ay{s.H, s.powH};
   const float u = texcoord(i, ax), v = texcoord(j, ay);
   float minDist = 1.0f, bx = 0.0f, by = 0.0f;
+  unsigned best = kNoSeed;
 #pragma unroll
   for (int y = 0; y < 3; ++y) {
     const int tj = wrap_nearest(v + o.oy[y], ay);
 #pragma unroll
     for (int x = 0; x < 3; ++x) {
       const int ti = wrap_nearest(u + o.ox[x], ax);
-      const float2 p = src[(size_t)tj * s.pitch + ti];
-      if (p.x != 0.0f && p.y != 0.0f) {
-        const float dx = p.x - u, dy = p.y - v;
+      unsigned seed;
+      if (FIRST) {
+        const bool occ = (src[(size_t)tj * src_pitch + (ti >> 5)] >> (ti & 31)) & 1u;
+        seed = occ ? pack_seed(ti, tj) : kNoSeed;
+      } else {
+        seed = src[(size_t)tj * src_pitch + ti];
+      }
+      if (seed != kNoSeed) {  // peek.x != 0 && peek.y != 0 (a seed's uv is never 0)
+        const float px = texcoord((int)(seed & 0xFFFFu), ax), py = texcoord((int)(seed >> 16), ay);
+        const float dx = px - u, dy = py - v;
         const float d = dx * dx + dy * dy;
         if (d < minDist) {
           minDist = d;
-          bx = p.x;
-          by = p.y;
+          bx = px;
+          by = py;
+          best = seed;
         }
       }
     }
   }
-  dst[(size_t)j * s.pitch + i] = make_float2(bx, by);
+  dst[(size_t)j * s.pitch + i] = best;
   if (dist) {
     // DistanceField.fs: distance(fragTexCoord, seed) -> packUNorm16: store the 16-bit q
     // (RadianceCascades.fs unpackUNorm16 recovers exactly q / 65535)
@@ -432,19 +471,27 @@ __global__ __launch_bounds__(256) void k_unorm8_to_f32(const unsigned char *__re
 // ---------------------------------------------------------------- launchers
 static dim3 grid2d(int w, int h) { return dim3(ceil_div(w, 64), ceil_div(h, 4)); }
 
-hipError_t launch_screen_uv(const float4 *color, float2 *seeds, ScreenDims s, hipStream_t st) {
-  hipLaunchKernelGGL(k_screen_uv, grid2d(s.W, s.H), dim3(256), 0, st, color, seeds, s);
+hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, ScreenDims s, hipStream_t st) {
+  hipLaunchKernelGGL(k_occupancy, grid2d(s.W, s.H), dim3(256), 0, st, color, mask, s, mpitch);
   return hipGetLastError();
 }
 
-hipError_t launch_jfa_step(const float2 *src, float2 *dst, unsigned short *dist, ScreenDims s, const float off_x[3],
-                           const float off_y[3], hipStream_t st) {
+hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *seeds, ScreenDims s, hipStream_t st) {
+  hipLaunchKernelGGL(k_seeds_from_mask, grid2d(s.W, s.H), dim3(256), 0, st, mask, mpitch, seeds, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
+                           ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st) {
   JfaOffsets o;
   for (int k = 0; k < 3; ++k) {
     o.ox[k] = off_x[k];
     o.oy[k] = off_y[k];
   }
-  hipLaunchKernelGGL(k_jfa_step, grid2d(s.W, s.H), dim3(256), 0, st, src, dst, dist, s, o);
+  if (first)
+    hipLaunchKernelGGL(k_jfa_step<true>, grid2d(s.W, s.H), dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
+  else
+    hipLaunchKernelGGL(k_jfa_step<false>, grid2d(s.W, s.H), dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
   return hipGetLastError();
 }
 
