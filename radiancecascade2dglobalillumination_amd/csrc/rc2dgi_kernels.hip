@@ -38,18 +38,25 @@ __device__ __forceinline__ unsigned pack_seed(int si, int sj) { return ((unsigne
 // the JFA runs >= 2 steps (step 1 overwrites jumpRT1), so step 0 reads the mask instead.
 __global__ __launch_bounds__(256) void k_occupancy(const float4 *__restrict__ color, unsigned *__restrict__ mask,
                                                    ScreenDims s, int mpitch) {
+  // 4 rows per wave (loads issued together), one 64-texel ballot per row
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-  bool occ = false;
-  if (i < s.W && j < s.H) {
-    const float4 c = color[(size_t)j * s.pitch + i];
-    occ = c.x > 0.0f || c.y > 0.0f || c.z > 0.0f;
+  const int j0 = blockIdx.y * 16 + (threadIdx.x >> 6);
+  float4 c[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = j0 + 4 * t;
+    c[t] = (i < s.W && j < s.H) ? color[(size_t)j * s.pitch + i] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  const unsigned long long b = __ballot(occ);
-  if ((threadIdx.x & 63) == 0 && j < s.H) {
-    unsigned *row = mask + (size_t)j * mpitch + (blockIdx.x * 2);
-    row[0] = (unsigned)b;
-    row[1] = (unsigned)(b >> 32);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = j0 + 4 * t;
+    const bool occ = c[t].x > 0.0f || c[t].y > 0.0f || c[t].z > 0.0f;
+    const unsigned long long b = __ballot(occ);
+    if ((threadIdx.x & 63) == 0 && j < s.H) {
+      unsigned *row = mask + (size_t)j * mpitch + (blockIdx.x * 2);
+      row[0] = (unsigned)b;
+      row[1] = (unsigned)(b >> 32);
+    }
   }
 }
 
@@ -70,51 +77,71 @@ struct JfaOffsets {
 
 // One JumpFlood.fs step.  FIRST: taps read the occupancy mask (the ScreenUV seeds); otherwise the
 // packed seeds of the previous step.  dist != nullptr fuses DistanceField.fs.
+// A 256-thread workgroup covers 64 x (4*JT) texels; each lane owns JT texels 4 rows apart and issues all 9*JT tap loads before the first compare (latency-bound gathers).
+constexpr int JT = 4;
+
 template <bool FIRST>
 __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ src, int src_pitch,
                                                   unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                   ScreenDims s, JfaOffsets o) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (i >= s.W || j >= s.H) return;
+  const int j0 = blockIdx.y * (4 * JT) + (threadIdx.x >> 6);
+  if (i >= s.W) return;
   const Axis ax{s.W, s.powW}, ay{s.H, s.powH};
-  const float u = texcoord(i, ax), v = texcoord(j, ay);
-  float minDist = 1.0f, bx = 0.0f, by = 0.0f;
-  unsigned best = kNoSeed;
+  const float u = texcoord(i, ax);
+  int ti[3];
 #pragma unroll
-  for (int y = 0; y < 3; ++y) {
-    const int tj = wrap_nearest(v + o.oy[y], ay);
+  for (int x = 0; x < 3; ++x) ti[x] = wrap_nearest(u + o.ox[x], ax);
+  unsigned seed[JT][9];
 #pragma unroll
-    for (int x = 0; x < 3; ++x) {
-      const int ti = wrap_nearest(u + o.ox[x], ax);
-      unsigned seed;
-      if (FIRST) {
-        const bool occ = (src[(size_t)tj * src_pitch + (ti >> 5)] >> (ti & 31)) & 1u;
-        seed = occ ? pack_seed(ti, tj) : kNoSeed;
-      } else {
-        seed = src[(size_t)tj * src_pitch + ti];
+  for (int t = 0; t < JT; ++t) {
+    const int j = min(j0 + 4 * t, s.H - 1);  // clamped rows are computed but not stored
+    const float v = texcoord(j, ay);
+#pragma unroll
+    for (int y = 0; y < 3; ++y) {
+      const int tj = wrap_nearest(v + o.oy[y], ay);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        if (FIRST) {
+          const bool occ = (src[(size_t)tj * src_pitch + (ti[x] >> 5)] >> (ti[x] & 31)) & 1u;
+          seed[t][y * 3 + x] = occ ? pack_seed(ti[x], tj) : kNoSeed;
+        } else {
+          seed[t][y * 3 + x] = src[(size_t)tj * src_pitch + ti[x]];
+        }
       }
-      if (seed != kNoSeed) {  // peek.x != 0 && peek.y != 0 (a seed's uv is never 0)
-        const float px = texcoord((int)(seed & 0xFFFFu), ax), py = texcoord((int)(seed >> 16), ay);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < JT; ++t) {
+    const int j = j0 + 4 * t;
+    if (j >= s.H) break;
+    const float v = texcoord(j, ay);
+    float minDist = 1.0f, bx = 0.0f, by = 0.0f;
+    unsigned best = kNoSeed;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
+      const unsigned sd = seed[t][k];
+      if (sd != kNoSeed) {  // peek.x != 0 && peek.y != 0 (a seed's uv is never 0)
+        const float px = texcoord((int)(sd & 0xFFFFu), ax), py = texcoord((int)(sd >> 16), ay);
         const float dx = px - u, dy = py - v;
         const float d = dx * dx + dy * dy;
         if (d < minDist) {
           minDist = d;
           bx = px;
           by = py;
-          best = seed;
+          best = sd;
         }
       }
     }
-  }
-  dst[(size_t)j * s.pitch + i] = best;
-  if (dist) {
-    // DistanceField.fs: distance(fragTexCoord, seed) -> packUNorm16: store the 16-bit q
-    // (RadianceCascades.fs unpackUNorm16 recovers exactly q / 65535)
-    const float dx = u - bx, dy = v - by;
-    const float d = sqrtf(dx * dx + dy * dy);
-    const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
-    dist[(size_t)j * s.pitch + i] = (unsigned short)(unsigned)(cl * 65535.0f + 0.5f);
+    dst[(size_t)j * s.pitch + i] = best;
+    if (dist) {
+      // DistanceField.fs: distance(fragTexCoord, seed) -> packUNorm16: store the 16-bit q
+      // (RadianceCascades.fs unpackUNorm16 recovers exactly q / 65535)
+      const float dx = u - bx, dy = v - by;
+      const float d = sqrtf(dx * dx + dy * dy);
+      const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
+      dist[(size_t)j * s.pitch + i] = (unsigned short)(unsigned)(cl * 65535.0f + 0.5f);
+    }
   }
 }
 
@@ -472,7 +499,8 @@ __global__ __launch_bounds__(256) void k_unorm8_to_f32(const unsigned char *__re
 static dim3 grid2d(int w, int h) { return dim3(ceil_div(w, 64), ceil_div(h, 4)); }
 
 hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, ScreenDims s, hipStream_t st) {
-  hipLaunchKernelGGL(k_occupancy, grid2d(s.W, s.H), dim3(256), 0, st, color, mask, s, mpitch);
+  hipLaunchKernelGGL(k_occupancy, dim3(ceil_div(s.W, 64), ceil_div(s.H, 16)), dim3(256), 0, st, color, mask, s,
+                     mpitch);
   return hipGetLastError();
 }
 
@@ -488,10 +516,11 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     o.ox[k] = off_x[k];
     o.oy[k] = off_y[k];
   }
+  const dim3 grid(ceil_div(s.W, 64), ceil_div(s.H, 4 * JT));
   if (first)
-    hipLaunchKernelGGL(k_jfa_step<true>, grid2d(s.W, s.H), dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
+    hipLaunchKernelGGL(k_jfa_step<true>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
   else
-    hipLaunchKernelGGL(k_jfa_step<false>, grid2d(s.W, s.H), dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
+    hipLaunchKernelGGL(k_jfa_step<false>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
   return hipGetLastError();
 }
 
