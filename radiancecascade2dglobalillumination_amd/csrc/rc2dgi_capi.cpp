@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -49,6 +50,7 @@ struct rc2dgi_ctx {
   int mpitch = 0;                               // mask row pitch (words)
   unsigned short *dist = nullptr;  // packUNorm16 q
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
+  float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
   float4 *sky = nullptr;
   // state
@@ -115,14 +117,14 @@ void free_level_bufs(rc2dgi_ctx *c) {
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
-                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky};
+                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   c->color_in = c->emissive = c->temp = c->color_out = nullptr;
   c->jump1 = c->jump2 = nullptr;
   c->occ = nullptr;
   c->dist = nullptr;
-  c->gi1 = c->gi2 = c->blur = nullptr;
+  c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
   c->sky = nullptr;
 }
@@ -158,6 +160,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->gi1, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->gi2, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
+  HIPCHK(c, alloc(&c->gi_spare, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->dirs, dir_table_len(c->N) * sizeof(float2)));
   HIPCHK(c, alloc(&c->sky, ((size_t)4 << (2 * (c->N - 1))) * sizeof(float4)));
   // initial contents: ClearAllRTs (RC2DGI.cs:109) -> (0,0,0,1) is implied by the frame
@@ -502,13 +505,19 @@ int rc2dgi_do(rc2dgi_ctx *c) {
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev_level[0], st));
   if (T) HIPCHK(c, hipEventRecord(c->ev[3], st));
-  float4 *finalGI = gi1final ? c->gi1 : c->gi2;  // RC2DGI.cs:365
+  float4 *&finalGI = gi1final ? c->gi1 : c->gi2;  // RC2DGI.cs:365
   c->final_gi = gi1final ? 1 : 2;
 
-  // 5. blur + blended copy-back (RC2DGI.cs:367-387)
+  // 5. blur + blended copy-back (RC2DGI.cs:367-387): one fused pass into the spare texture, which
+  //    then becomes finalGI (buffer swap, same contents as blending in place)
   if (c->blur_radius > 0.0f) {
-    HIPCHK(c, launch_blur(finalGI, c->blur, c->cd, c->blur_radius, st));
-    HIPCHK(c, launch_blur_copyback(c->blur, finalGI, c->cd, st));
+    if (launch_blur_fused(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, st)) {
+      HIPCHK(c, hipGetLastError());
+      std::swap(finalGI, c->gi_spare);
+    } else {
+      HIPCHK(c, launch_blur(finalGI, c->blur, c->cd, c->blur_radius, st));
+      HIPCHK(c, launch_blur_copyback(c->blur, finalGI, c->cd, st));
+    }
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[4], st));
 

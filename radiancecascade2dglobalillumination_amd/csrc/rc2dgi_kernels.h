@@ -50,6 +50,10 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
 // Blur.fs into blur_out, then the default-shader blended copy-back into gi (RC2DGI.cs:367-387)
 hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st);
 hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st);
+// both in one pass (power-of-two cascade sizes, radius <= 6); gi_out may not alias gi_in.
+// Returns false (nothing launched) when the shape is not supported.
+bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
+                       hipStream_t st);
 
 // merge.fs into temp, then tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
 hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,

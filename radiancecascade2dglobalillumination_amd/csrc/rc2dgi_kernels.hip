@@ -457,6 +457,65 @@ __global__ __launch_bounds__(256) void k_blur(const float4 *__restrict__ gi, flo
   blur_out[(size_t)j * c.pitch + i] = blend_over_black(res);
 }
 
+// Blur.fs + its blended copy-back in one pass, for power-of-two cascade sizes.  There the
+// copy-back's LINEAR sample of cascadeBlurRT at fragTexCoord lands exactly on the texel
+// (x = (i+0.5)/n*n - 0.5 = i, weight 0: fma(0, b - a, a) = a), so each texel needs only its
+// own blur value.  G_0 is staged in LDS: a 64 x 16 core plus an H-texel halo covers every
+// bilinear tap of radius <= H - 2 (taps that ever fall outside are read from HBM).
+template <int H>
+__global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ gi_in, float4 *__restrict__ blur_out,
+                                                    float4 *__restrict__ gi_out, CascadeDims c, float radius) {
+  constexpr int TW = 64 + 2 * H, TH = 16 + 2 * H;
+  __shared__ float4 tile[TH * TW];
+  const int x0 = blockIdx.x * 64 - H, y0 = blockIdx.y * 16 - H;
+  for (int k = threadIdx.x; k < TW * TH; k += 256) {
+    const int ty = k / TW, tx = k - ty * TW;
+    const int gx = (x0 + tx) & (c.CW - 1), gy = (y0 + ty) & (c.CH - 1);
+    tile[k] = gi_in[(size_t)gy * c.pitch + gx];
+  }
+  __syncthreads();
+  const Axis ax{c.CW, 1}, ay{c.CH, 1};
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float u = texcoord(i, ax);
+  const float tsx = 1.0f / (float)c.CW, tsy = 1.0f / (float)c.CH;
+  const float kx[8] = {-1.f, 1.f, -1.f, 1.f, 0.f, 0.f, -1.f, 1.f};
+  const float ky[8] = {-1.f, -1.f, 1.f, 1.f, -1.f, 1.f, 0.f, 0.f};
+  auto fetch = [&](int gx, int gy) -> float4 {
+    const int lx = (gx - x0) & (c.CW - 1), ly = (gy - y0) & (c.CH - 1);
+    if (lx < TW && ly < TH) return tile[ly * TW + lx];
+    return ntload4(&gi_in[(size_t)gy * c.pitch + gx]);
+  };
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = blockIdx.y * 16 + (threadIdx.x >> 6) + 4 * t;
+    if (i >= c.CW || j >= c.CH) continue;
+    const float v = texcoord(j, ay);
+    float4 res = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {  // Blur.fs:22-34 order: 4 corners, 4 edges, centre
+      float su = u, sv = v, w = 0.250f;
+      if (k < 8) {
+        su = u + (kx[k] * tsx) * radius;
+        sv = v + (ky[k] * tsy) * radius;
+        w = k < 4 ? 0.0625f : 0.125f;
+      }
+      int a0, a1, b0, b1;
+      float wx, wy;
+      wrap_linear(su, ax, a0, a1, wx);
+      wrap_linear(sv, ay, b0, b1, wy);
+      const float4 tp = lerp_gl(lerp_gl(fetch(a0, b0), fetch(a1, b0), wx), lerp_gl(fetch(a0, b1), fetch(a1, b1), wx), wy);
+      res.x = res.x + tp.x * w;
+      res.y = res.y + tp.y * w;
+      res.z = res.z + tp.z * w;
+      res.w = res.w + tp.w * w;
+    }
+    const float4 b = blend_over_black(res);  // cascadeBlurRT cleared to (0,0,0,1)
+    const size_t o = (size_t)j * c.pitch + i;
+    blur_out[o] = b;
+    gi_out[o] = blend(b, tile[(j - y0) * TW + (i - x0)]);  // copy-back onto finalGI, blended
+  }
+}
+
 __global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict__ blur, float4 *__restrict__ gi,
                                                        CascadeDims c) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -592,6 +651,19 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
 hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st) {
   hipLaunchKernelGGL(k_blur, grid2d(c.CW, c.CH), dim3(256), 0, st, gi, blur_out, c, radius);
   return hipGetLastError();
+}
+
+bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
+                       hipStream_t st) {
+  if (!(c.powW && c.powH) || c.CW < 64 || c.CH < 16) return false;
+  const dim3 grid(ceil_div(c.CW, 64), ceil_div(c.CH, 16));
+  if (radius <= 2.0f)
+    hipLaunchKernelGGL(k_blur_fused<4>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius);
+  else if (radius <= 6.0f)
+    hipLaunchKernelGGL(k_blur_fused<8>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius);
+  else
+    return false;
+  return true;
 }
 
 hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st) {
