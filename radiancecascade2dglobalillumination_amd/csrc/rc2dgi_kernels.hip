@@ -272,7 +272,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
 #ifndef RC2DGI_DIAG_MAX_ITERS
 #define RC2DGI_DIAG_MAX_ITERS 32  // RadianceCascades.fs:64 (diagnostic builds may cap it; never shipped)
 #endif
-#pragma unroll 1
+#pragma unroll
   for (int it = 0; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
     int idx[NR];
     bool live[NR];
@@ -478,32 +478,59 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ g
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const float u = texcoord(i, ax);
   const float tsx = 1.0f / (float)c.CW, tsy = 1.0f / (float)c.CH;
-  const float kx[8] = {-1.f, 1.f, -1.f, 1.f, 0.f, 0.f, -1.f, 1.f};
-  const float ky[8] = {-1.f, -1.f, 1.f, 1.f, -1.f, 1.f, 0.f, 0.f};
-  auto fetch = [&](int gx, int gy) -> float4 {
-    const int lx = (gx - x0) & (c.CW - 1), ly = (gy - y0) & (c.CH - 1);
-    if (lx < TW && ly < TH) return tile[ly * TW + lx];
-    return ntload4(&gi_in[(size_t)gy * c.pitch + gx]);
-  };
+  // Blur.fs taps use only three distinct x coordinates (offset -1, 0, +1 texels * radius) and three
+  // y coordinates; resolve each to (tap0, tap1, weight) once.  fragTexCoord + vec2(k, .) * texelSize *
+  // _BlurRadius evaluates x as u + (k * tsx) * radius, the same float for every tap with that k.
+  int xa[3], xb[3];
+  float xw[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const float su = q == 1 ? u : u + ((float)(q - 1) * tsx) * radius;
+    wrap_linear(su, ax, xa[q], xb[q], xw[q]);
+    xa[q] = (xa[q] - x0) & (c.CW - 1);  // tile-local columns
+    xb[q] = (xb[q] - x0) & (c.CW - 1);
+  }
+  const bool xin = xa[0] < TW && xb[0] < TW && xa[2] < TW && xb[2] < TW && xa[1] < TW && xb[1] < TW;
+  // Blur.fs:22-34 order: (-1,-1) (1,-1) (-1,1) (1,1) (0,-1) (0,1) (-1,0) (1,0) (0,0); index 0..2 = -1,0,+1
+  constexpr int KX[9] = {0, 2, 0, 2, 1, 1, 0, 2, 1};
+  constexpr int KY[9] = {0, 0, 2, 2, 0, 2, 1, 1, 1};
+  constexpr float KW[9] = {0.0625f, 0.0625f, 0.0625f, 0.0625f, 0.125f, 0.125f, 0.125f, 0.125f, 0.250f};
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int j = blockIdx.y * 16 + (threadIdx.x >> 6) + 4 * t;
     if (i >= c.CW || j >= c.CH) continue;
     const float v = texcoord(j, ay);
+    int ya[3], yb[3];
+    float yw[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const float sv = q == 1 ? v : v + ((float)(q - 1) * tsy) * radius;
+      wrap_linear(sv, ay, ya[q], yb[q], yw[q]);
+      ya[q] = (ya[q] - y0) & (c.CH - 1);
+      yb[q] = (yb[q] - y0) & (c.CH - 1);
+    }
+    const bool inside = xin && ya[0] < TH && yb[0] < TH && ya[1] < TH && yb[1] < TH && ya[2] < TH && yb[2] < TH;
     float4 res = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {  // Blur.fs:22-34 order: 4 corners, 4 edges, centre
-      float su = u, sv = v, w = 0.250f;
-      if (k < 8) {
-        su = u + (kx[k] * tsx) * radius;
-        sv = v + (ky[k] * tsy) * radius;
-        w = k < 4 ? 0.0625f : 0.125f;
+    for (int k = 0; k < 9; ++k) {
+      const int qx = KX[k], qy = KY[k];
+      float4 t00, t10, t01, t11;
+      if (inside) {
+        t00 = tile[ya[qy] * TW + xa[qx]];
+        t10 = tile[ya[qy] * TW + xb[qx]];
+        t01 = tile[yb[qy] * TW + xa[qx]];
+        t11 = tile[yb[qy] * TW + xb[qx]];
+      } else {  // a tap beyond the staged halo: global coordinates are tile-local + origin
+        auto g = [&](int ly, int lx) {
+          return ntload4(&gi_in[(size_t)((ly + y0) & (c.CH - 1)) * c.pitch + ((lx + x0) & (c.CW - 1))]);
+        };
+        t00 = g(ya[qy], xa[qx]);
+        t10 = g(ya[qy], xb[qx]);
+        t01 = g(yb[qy], xa[qx]);
+        t11 = g(yb[qy], xb[qx]);
       }
-      int a0, a1, b0, b1;
-      float wx, wy;
-      wrap_linear(su, ax, a0, a1, wx);
-      wrap_linear(sv, ay, b0, b1, wy);
-      const float4 tp = lerp_gl(lerp_gl(fetch(a0, b0), fetch(a1, b0), wx), lerp_gl(fetch(a0, b1), fetch(a1, b1), wx), wy);
+      const float4 tp = lerp_gl(lerp_gl(t00, t10, xw[qx]), lerp_gl(t01, t11, xw[qx]), yw[qy]);
+      const float w = KW[k];
       res.x = res.x + tp.x * w;
       res.y = res.y + tp.y * w;
       res.z = res.z + tp.z * w;
