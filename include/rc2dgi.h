@@ -139,6 +139,9 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
 /* ---- tuning knobs (performance only; results are identical for every value).
  *   "rc_variant"      RC workgroup tile shape for every level (0 .. rc_variant_count-1)
  *   "rc_variant_L<n>" the same for level n only
+ *   "blur_path"       blur / copy-back / merge kernels: 0 auto (fixed-tap blur with merge fused
+ *                     where the sizes allow), 1 LDS-tiled blur + copy-back, then merge,
+ *                     2 separate blur, copy-back and merge passes
  * rc2dgi_get_tuning also answers "rc_variant_count". */
 int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
 int rc2dgi_get_tuning(rc2dgi_ctx *ctx, const char *key, int *value);

@@ -64,6 +64,7 @@ struct rc2dgi_ctx {
   hipEvent_t ev[P_COUNT + 1] = {};
   std::vector<hipEvent_t> ev_level;  // N + 1
   std::vector<int> rc_variant;  // per level tile shape (tuning)
+  int blur_path = 0;             // tuning "blur_path"
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
   std::string err;
@@ -508,10 +509,21 @@ int rc2dgi_do(rc2dgi_ctx *c) {
   float4 *&finalGI = gi1final ? c->gi1 : c->gi2;  // RC2DGI.cs:365
   c->final_gi = gi1final ? 1 : 2;
 
-  // 5. blur + blended copy-back (RC2DGI.cs:367-387): one fused pass into the spare texture, which
-  //    then becomes finalGI (buffer swap, same contents as blending in place)
+  // 5. blur + blended copy-back (RC2DGI.cs:367-387) into the spare texture, which then becomes
+  //    finalGI (buffer swap, same contents as blending in place); 6. merge + copy-back
+  //    (RC2DGI.cs:389-404), fused into the blur pass when the fixed-tap kernel applies and the
+  //    cascade matches the screen (its pass time is then reported under blur).
+  bool merged = false;
   if (c->blur_radius > 0.0f) {
-    if (launch_blur_fused(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, st)) {
+    bool fused = false;
+    if (c->blur_path == 0) {
+      const bool mrg = c->sd.W == c->CW && c->sd.H == c->CH;
+      fused = launch_blur_rows(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, c->color_in, c->temp,
+                               c->color_out, c->sd, mrg, st);
+      merged = fused && mrg;
+    }
+    if (!fused && c->blur_path <= 1) fused = launch_blur_fused(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, st);
+    if (fused) {
       HIPCHK(c, hipGetLastError());
       std::swap(finalGI, c->gi_spare);
     } else {
@@ -520,9 +532,7 @@ int rc2dgi_do(rc2dgi_ctx *c) {
     }
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[4], st));
-
-  // 6. merge + copy-back (RC2DGI.cs:389-404)
-  HIPCHK(c, launch_merge(c->color_in, finalGI, c->temp, c->color_out, c->sd, c->cd, st));
+  if (!merged) HIPCHK(c, launch_merge(c->color_in, finalGI, c->temp, c->color_out, c->sd, c->cd, st));
   if (T) HIPCHK(c, hipEventRecord(c->ev[5], st));
   c->frame_done = true;
   c->have_frame = true;
@@ -613,6 +623,11 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_variant[L] = value;
     return RC2DGI_OK;
   }
+  if (k == "blur_path") {
+    if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "blur_path out of range");
+    c->blur_path = value;
+    return RC2DGI_OK;
+  }
   return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);
 }
 
@@ -627,6 +642,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
     const int L = std::atoi(k.c_str() + 12);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
     *value = c->rc_variant[L];
+    return RC2DGI_OK;
+  }
+  if (k == "blur_path") {
+    *value = c->blur_path;
     return RC2DGI_OK;
   }
   return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);

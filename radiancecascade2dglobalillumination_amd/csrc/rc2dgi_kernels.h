@@ -10,6 +10,12 @@ struct ScreenDims {
   int powW, powH;  // power-of-two flags (GL wrap arithmetic differs)
 };
 
+// fixed bilinear taps of Blur.fs for a dyadic radius (see k_blur_rows)
+struct BlurTaps {
+  int a0;         // column / row offset of the "-radius" tap pair
+  float w0, w2;   // weights of the "-radius" and "+radius" tap pairs
+};
+
 struct CascadeDims {
   int CW, CH;
   int pitch;
@@ -54,6 +60,13 @@ hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, h
 // Returns false (nothing launched) when the shape is not supported.
 bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
                        hipStream_t st);
+
+// Blur + copy-back (+ merge and its copy-back when `merge`) with fixed taps; false when the
+// radius / sizes do not allow it (see k_blur_rows).  blur_rows_plan: F = floor(radius) or -1.
+int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt);
+bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
+                      const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
+                      hipStream_t st);
 
 // merge.fs into temp, then tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
 hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,

@@ -543,6 +543,91 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ g
   }
 }
 
+// Blur.fs + blended copy-back (+ merge.fs and its copy-back when MERGE) for power-of-two cascades
+// and a dyadic radius (radius * 256 integral, radius < F + 1, sizes <= 2^14).  Then every
+// fragTexCoord + k * texelSize * radius is exact (a multiple of 2^-8 texels below 2^15 texels), so
+// the LINEAR taps of texel i sit at the fixed columns i + a0, i + a0 + 1 (weight w0), i, i + 1
+// (weight 0) and i + F, i + F + 1 (weight w2) -- the same for every texel, the same values the
+// general path computes.  Rows follow the same pattern.  Each thread owns a column of 8
+// consecutive rows: it lerps every input row horizontally once (3 samples per row) and reuses those
+// along the column for the vertical lerps of all 8 outputs.  Weight-0 lerps are identities for
+// finite values (fma(0, b - a, a) = a) and are skipped.  With MERGE (screen == cascade size) the
+// merge's LINEAR sample of finalGI lands exactly on the texel as well (same argument), so
+// merge.fs runs on the blended GI value held in registers.
+template <int F, bool MERGE>
+__global__ __launch_bounds__(256) void k_blur_rows(const float4 *__restrict__ gi_in, float4 *__restrict__ blur_out,
+                                                   float4 *__restrict__ gi_out, CascadeDims c, BlurTaps bt,
+                                                   const float4 *__restrict__ color_in, float4 *__restrict__ temp,
+                                                   float4 *__restrict__ color_out, int spitch) {
+  constexpr int HALO = F + 1, TW = 64 + 2 * HALO, TH = 32 + 2 * HALO, NR = 8 + 2 * HALO;
+  __shared__ float4 tile[TH * TW];
+  const int x0 = blockIdx.x * 64 - HALO, y0 = blockIdx.y * 32 - HALO;
+  for (int k = threadIdx.x; k < TW * TH; k += 256) {
+    const int ty = k / TW, tx = k - ty * TW;
+    const int gx = (x0 + tx) & (c.CW - 1), gy = (y0 + ty) & (c.CH - 1);
+    tile[k] = gi_in[(size_t)gy * c.pitch + gx];
+  }
+  __syncthreads();
+  const int lx = (threadIdx.x & 63) + HALO;  // tile column of this thread's texel
+  const int r0 = (threadIdx.x >> 6) * 8;     // first input row (tile-local) = first output row - HALO
+  const bool lo = bt.a0 == -F - 1;           // a0 is -F-1 (fractional radius) or -F (integral radius)
+  const float w0 = bt.w0, w2 = bt.w2;
+  // h[k][q]: input row r0 + k lerped horizontally at column offset q (0: a0, 1: 0, 2: F)
+  float4 h[NR][3];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const float4 *row = tile + (r0 + k) * TW + lx;
+    const float4 a = row[bt.a0], b = row[bt.a0 + 1];
+    h[k][0] = lerp_gl(a, b, w0);
+    h[k][1] = row[0];
+    h[k][2] = lerp_gl(row[F], row[F + 1], w2);
+  }
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int m = t + HALO;  // this output's own row in h
+    // row pairs of the y offsets: -1 -> (m + a0, m + a0 + 1) w0; 0 -> m (weight 0); +1 -> (m + F, m + F + 1) w2
+    float4 s[3][3];  // s[qy][qx]
+#pragma unroll
+    for (int qx = 0; qx < 3; ++qx) {
+      const float4 ra = lo ? h[m - F - 1][qx] : h[m - F][qx];
+      const float4 rb = lo ? h[m - F][qx] : h[m - F + 1][qx];
+      s[0][qx] = lerp_gl(ra, rb, w0);
+      s[1][qx] = h[m][qx];
+      s[2][qx] = lerp_gl(h[m + F][qx], h[m + F + 1][qx], w2);
+    }
+    // Blur.fs:22-34 order: (-1,-1) (1,-1) (-1,1) (1,1) (0,-1) (0,1) (-1,0) (1,0) (0,0)
+    constexpr int KX[9] = {0, 2, 0, 2, 1, 1, 0, 2, 1};
+    constexpr int KY[9] = {0, 0, 2, 2, 0, 2, 1, 1, 1};
+    constexpr float KW[9] = {0.0625f, 0.0625f, 0.0625f, 0.0625f, 0.125f, 0.125f, 0.125f, 0.125f, 0.250f};
+    float4 res = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float4 tp = s[KY[k]][KX[k]];
+      const float w = KW[k];
+      res.x = res.x + tp.x * w;
+      res.y = res.y + tp.y * w;
+      res.z = res.z + tp.z * w;
+      res.w = res.w + tp.w * w;
+    }
+    const float4 b = blend_over_black(res);  // cascadeBlurRT cleared to (0,0,0,1)
+    const float4 g = blend(b, h[m][1]);      // copy-back onto finalGI, blended
+    const int j = blockIdx.y * 32 + r0 + t;
+    const size_t o = (size_t)j * c.pitch + i;
+    blur_out[o] = b;
+    gi_out[o] = g;
+    if constexpr (MERGE) {  // merge.fs:10-15 + tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
+      const size_t so = (size_t)j * spitch + i;
+      const float4 col = color_in[so];
+      const float4 src =
+          make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
+      const float4 tt = blend_over_black(src);
+      temp[so] = tt;
+      color_out[so] = blend(tt, col);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict__ blur, float4 *__restrict__ gi,
                                                        CascadeDims c) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -690,6 +775,37 @@ bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Ca
     hipLaunchKernelGGL(k_blur_fused<8>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius);
   else
     return false;
+  return true;
+}
+
+int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt) {
+  if (!(c.powW && c.powH) || c.CW < 64 || c.CH < 32 || c.CW > 16384 || c.CH > 16384) return -1;
+  if (!(radius > 0.0f) || !(radius < 3.0f) || radius * 256.0f != floorf(radius * 256.0f)) return -1;
+  // x = i - radius and i + radius are exact: floor / fraction do not depend on i
+  const float lo = -radius, hi = radius;
+  bt->a0 = (int)floorf(lo);
+  bt->w0 = lo - floorf(lo);
+  bt->w2 = hi - floorf(hi);
+  return (int)floorf(hi);  // F
+}
+
+bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
+                      const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
+                      hipStream_t st) {
+  BlurTaps bt;
+  const int F = blur_rows_plan(c, radius, &bt);
+  if (F < 0) return false;
+  if (merge && !(s.W == c.CW && s.H == c.CH)) return false;
+  const dim3 grid(c.CW / 64, c.CH / 32);
+#define RC2DGI_BLUR_ROWS(FV, MV)                                                                               \
+  hipLaunchKernelGGL((k_blur_rows<FV, MV>), grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, bt, color_in, \
+                     temp, color_out, s.pitch)
+  if (merge) {
+    if (F == 0) RC2DGI_BLUR_ROWS(0, true); else if (F == 1) RC2DGI_BLUR_ROWS(1, true); else RC2DGI_BLUR_ROWS(2, true);
+  } else {
+    if (F == 0) RC2DGI_BLUR_ROWS(0, false); else if (F == 1) RC2DGI_BLUR_ROWS(1, false); else RC2DGI_BLUR_ROWS(2, false);
+  }
+#undef RC2DGI_BLUR_ROWS
   return true;
 }
 

@@ -342,3 +342,33 @@ def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene):
             g = ctx.download_level(L)
             assert np.array_equal(g, fr.gi_levels[L]), f"variant {v} level {L}: {np.count_nonzero(g != fr.gi_levels[L])}"
     ctx.close()
+
+
+@pytest.mark.parametrize("W,H,rs,radius", [
+    (128, 128, 1.0, 1.5),    # fixed taps (F=1), merge fused
+    (256, 128, 1.0, 2.5),    # F=2
+    (128, 64, 1.0, 1.0),     # integral radius: a0 = -F
+    (64, 64, 1.0, 0.5),      # F=0
+    (512, 64, 1.0, 2.99609375),  # largest dyadic radius below 3
+    (128, 128, 1.0, 1.37),   # not dyadic: LDS-tiled general kernel
+    (128, 128, 1.0, 3.0),    # F=3: beyond the fixed-tap kernels
+    (256, 256, 0.5, 1.5),    # cascade 128^2 != screen: fixed taps, separate merge
+    (200, 120, 1.0, 1.5),    # non-power-of-two: separate passes only
+])
+def test_every_blur_path_matches_oracle(RC2DGI, W, H, rs, radius):
+    """blur_path 0 (fixed taps + fused merge), 1 (LDS tile), 2 (separate passes): same bits."""
+    p = oracle.Params(W=W, H=H, N=3, ray_range=4.0, render_scale=rs, blur_radius=radius)
+    color, emis = make_scene("rand:51", W, H)
+    fr = oracle_dict(oracle.frame(p, color, emis))
+    ctx = RC2DGI(W, H, cascade_count=3, render_scale=rs, ray_range=4.0)
+    set_uniforms(ctx, p)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    for path in (0, 1, 2):
+        ctx.set_tuning("blur_path", path)
+        assert ctx.get_tuning("blur_path") == path
+        ctx.do_rc2dgi()
+        ctx.sync()
+        got = {k: ctx.download(k) for k in ("color", "temp", "gi1", "gi2", "blur", "final_gi")}
+        assert_parity(got, fr, list(got), exact=True, what=f"blur_path {path}")
+    ctx.close()
