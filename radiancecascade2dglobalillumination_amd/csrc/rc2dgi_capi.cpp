@@ -719,7 +719,7 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
       HIPCHK(c, hipMemcpy2D(s.data(), (size_t)w * 4, which == RC2DGI_RT_JUMP1 ? c->jump1 : c->jump2,
                             (size_t)pitch * 4, (size_t)w * 4, h, hipMemcpyDeviceToHost));
       for (size_t k = 0; k < s.size(); ++k) {
-        if (s[k] == 0xFFFFFFFFu) {
+        if (s[k] == 0x80008000u) {  // kNoSeed
           img[k] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
         } else {
           const int si = (int)(s[k] & 0xFFFFu), sj = (int)(s[k] >> 16);

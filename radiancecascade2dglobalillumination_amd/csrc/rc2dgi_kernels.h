@@ -27,7 +27,7 @@ hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, Scr
 // the ScreenUV seed texture J0 (packed seeds) from the mask
 hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *seeds, ScreenDims s, hipStream_t st);
 
-// one JumpFlood step (shaders/JumpFlood.fs) over packed seeds (sj<<16 | si, 0xFFFFFFFF = none).
+// one JumpFlood step (shaders/JumpFlood.fs) over packed seeds (sj<<16 | si, 0x80008000 = none).
 // first: src is the occupancy mask (pitch in words), else packed seeds (pitch in texels).
 // off_x/off_y = vec2(k,k)*_Aspect.yx*_StepSize for k = -1,0,1 (host-computed).
 // dist != nullptr fuses DistanceField.fs: stores the 16-bit q of packUNorm16.

@@ -29,7 +29,7 @@ static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 // ---------------------------------------------------------------- ScreenUV
 // jumpRT texels hold a packed seed: (sj << 16) | si for the seed texel (si, sj), whose value in the
 // reference is its fragTexCoord ((si+0.5)/W, (sj+0.5)/H); kNoSeed is the reference's (0,0).
-constexpr unsigned kNoSeed = 0xFFFFFFFFu;
+constexpr unsigned kNoSeed = 0x80008000u;  // si = sj = 32768: never a texel (W, H <= 32768)
 
 __device__ __forceinline__ unsigned pack_seed(int si, int sj) { return ((unsigned)sj << 16) | (unsigned)si; }
 
@@ -73,6 +73,12 @@ __global__ __launch_bounds__(256) void k_seeds_from_mask(const unsigned *__restr
 // ---------------------------------------------------------------- JumpFlood (+ DistanceField)
 struct JfaOffsets {
   float ox[3], oy[3];
+};
+
+// power-of-two screens: integer tap offsets and the distance-key scaling (see k_jfa_p2)
+struct JfaTaps {
+  int dx[3], dy[3];
+  float scx, scy, dinit;
 };
 
 // One JumpFlood.fs step.  FIRST: taps read the occupancy mask (the ScreenUV seeds); otherwise the
@@ -138,6 +144,87 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
       // DistanceField.fs: distance(fragTexCoord, seed) -> packUNorm16: store the 16-bit q
       // (RadianceCascades.fs unpackUNorm16 recovers exactly q / 65535)
       const float dx = u - bx, dy = v - by;
+      const float d = sqrtf(dx * dx + dy * dy);
+      const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
+      dist[(size_t)j * s.pitch + i] = (unsigned short)(unsigned)(cl * 65535.0f + 0.5f);
+    }
+  }
+}
+
+// JumpFlood.fs step for power-of-two W and H.  There every fragTexCoord + offset is exact, so a
+// tap's NEAREST texel is (i + dx, j + dy) & (size - 1) with integer dx, dy fixed per step (host:
+// floor(0.5 + offset * size)); tap rows are wave-uniform (scalar row addresses).
+// Seed distance: fragTexCoord differences are exact as well, dx = (si - i) / W, and a power-of-two
+// scaling commutes with rounding, so the shader's `dx*dx + dy*dy < minDist` is the same comparison
+// on ((si - i) * scx)^2 + ((sj - j) * scy)^2 < max(W,H)^2.
+//   IKEY (W == H <= 4096): (si - i)^2 and (sj - j)^2 are integers below 2^24 (exact in fp32), so
+//     the shader's rounded sum is the integer sum converted with round-to-nearest-even: one packed
+//     16-bit subtract and one clamped 16-bit dot product per tap.
+//   otherwise the fp32 form.
+// The no-seed value 0x80008000 is at least max(W,H) away from every texel (and below overflow),
+// so it never beats the initial minDist and needs no test of its own.
+template <bool FIRST, bool IKEY>
+__global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src, int src_pitch,
+                                                unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
+                                                ScreenDims s, JfaTaps o) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j0 = blockIdx.y * (4 * JT) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (i >= s.W) return;
+  unsigned ti[3];  // unsigned: scalar row base + 32-bit lane offset addressing
+#pragma unroll
+  for (int x = 0; x < 3; ++x) ti[x] = (unsigned)(i + o.dx[x]) & (unsigned)(s.W - 1);
+  unsigned seed[JT][9];
+#pragma unroll
+  for (int t = 0; t < JT; ++t) {
+    const int j = min(j0 + 4 * t, s.H - 1);  // clamped rows are computed but not stored
+#pragma unroll
+    for (int y = 0; y < 3; ++y) {
+      const unsigned tj = (unsigned)(j + o.dy[y]) & (unsigned)(s.H - 1);
+      const unsigned *row = src + (size_t)tj * src_pitch;
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        if (FIRST) {
+          const bool occ = (row[ti[x] >> 5] >> (ti[x] & 31)) & 1u;
+          seed[t][y * 3 + x] = occ ? ((tj << 16) | ti[x]) : kNoSeed;
+        } else {
+          seed[t][y * 3 + x] = *reinterpret_cast<const unsigned *>(reinterpret_cast<const char *>(row) + (ti[x] << 2));
+        }
+      }
+    }
+  }
+  typedef short v2s __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int t = 0; t < JT; ++t) {
+    const int j = j0 + 4 * t;
+    if (j >= s.H) break;
+    float minKey = o.dinit;
+    unsigned best = kNoSeed;
+    const unsigned here = pack_seed(i, j);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
+      const unsigned sd = seed[t][k];
+      float key;
+      if constexpr (IKEY) {
+        const v2s d = __builtin_bit_cast(v2s, sd) - __builtin_bit_cast(v2s, here);
+        key = (float)__builtin_amdgcn_sdot2(d, d, 0, true);
+      } else {
+        const float dx = (float)((int)(sd & 0xFFFFu) - i) * o.scx, dy = (float)((int)(sd >> 16) - j) * o.scy;
+        key = dx * dx + dy * dy;
+      }
+      if (key < minKey) {
+        minKey = key;
+        best = sd;
+      }
+    }
+    dst[(size_t)j * s.pitch + i] = best;
+    if (dist) {  // DistanceField.fs, as in k_jfa_step
+      const Axis ax{s.W, 1}, ay{s.H, 1};
+      float bx = 0.0f, by = 0.0f;
+      if (best != kNoSeed) {
+        bx = texcoord((int)(best & 0xFFFFu), ax);
+        by = texcoord((int)(best >> 16), ay);
+      }
+      const float dx = texcoord(i, ax) - bx, dy = texcoord(j, ay) - by;
       const float d = sqrtf(dx * dx + dy * dy);
       const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
       dist[(size_t)j * s.pitch + i] = (unsigned short)(unsigned)(cl * 65535.0f + 0.5f);
@@ -680,6 +767,34 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
   return hipGetLastError();
 }
 
+// Integer taps for k_jfa_p2: power-of-two W, H <= 16384 (the no-seed value must stay at least
+// max(W,H) away), and every fragTexCoord + offset exactly representable: (i + 0.5) / n has its
+// lowest bit at 2^-(log2 n + 1) and a nonzero offset is a power of two 2^-m (aspect ratio and step
+// size are powers of two), so the sum, below 2 in magnitude, is exact when both exponents are
+// within 23 bits.
+bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp) {
+  if (!(s.powW && s.powH) || s.W > 16384 || s.H > 16384) return false;
+  auto axis = [](int n, const float off[3], int out[3]) {
+    const int q = __builtin_ctz((unsigned)n);
+    if (q + 1 > 23) return false;
+    for (int k = 0; k < 3; ++k) {
+      if (off[k] != 0.0f) {
+        int e;
+        const float m = frexpf(fabsf(off[k]), &e);  // |off| = m * 2^e
+        if (m != 0.5f || 1 - e > 23) return false;
+      }
+      out[k] = (int)floorf(0.5f + off[k] * (float)n);  // exact: off * n is a power of two or 0
+    }
+    return true;
+  };
+  if (!axis(s.W, off_x, tp->dx) || !axis(s.H, off_y, tp->dy)) return false;
+  const int mx = s.W > s.H ? s.W : s.H;
+  tp->scx = (float)(mx / s.W);
+  tp->scy = (float)(mx / s.H);
+  tp->dinit = (float)mx * (float)mx;
+  return true;
+}
+
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st) {
   JfaOffsets o;
@@ -688,10 +803,22 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     o.oy[k] = off_y[k];
   }
   const dim3 grid(ceil_div(s.W, 64), ceil_div(s.H, 4 * JT));
-  if (first)
+  JfaTaps tp;
+  if (jfa_p2_taps(s, off_x, off_y, &tp)) {
+    const bool ikey = s.W == s.H && s.W <= 4096;
+#define RC2DGI_JFA(F, K) \
+  hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp)
+    if (first) {
+      if (ikey) RC2DGI_JFA(true, true); else RC2DGI_JFA(true, false);
+    } else {
+      if (ikey) RC2DGI_JFA(false, true); else RC2DGI_JFA(false, false);
+    }
+#undef RC2DGI_JFA
+  } else if (first) {
     hipLaunchKernelGGL(k_jfa_step<true>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
-  else
+  } else {
     hipLaunchKernelGGL(k_jfa_step<false>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
+  }
   return hipGetLastError();
 }
 

@@ -51,3 +51,46 @@ def test_pow2_division_is_reciprocal_multiply():
     for n in (1, 2, 64, 1024, 4096, 8192, 16384):
         nf = np.float32(n)
         assert np.array_equal(a / nf, a * (np.float32(1) / nf))
+
+
+def _jfa_shader_key(si, sj, i, j, W, H):
+    """JumpFlood.fs distance in fp32: texcoord differences, squared, summed (no contraction)."""
+    f = np.float32
+    u, v = (f(i) + f(0.5)) / f(W), (f(j) + f(0.5)) / f(H)
+    px, py = (si.astype(f) + f(0.5)) / f(W), (sj.astype(f) + f(0.5)) / f(H)
+    dx, dy = px - u, py - v
+    return dx * dx + dy * dy
+
+
+def test_jfa_integer_key_matches_shader_distance():
+    """k_jfa_p2 IKEY (W == H <= 4096): float(dx^2 + dy^2) over integer texel differences, scaled by
+    W^-2, equals the shader's fp32 distance for every seed offset, so comparisons agree."""
+    W = H = 4096
+    rng = np.random.default_rng(7)
+    i, j = 1234, 3001
+    si = np.concatenate([rng.integers(0, W, 200000), np.arange(W)]).astype(np.int64)
+    sj = np.concatenate([rng.integers(0, H, 200000), np.full(W, 4095)]).astype(np.int64)
+    want = _jfa_shader_key(si, sj, i, j, W, H)
+    n = (si - i) ** 2 + (sj - j) ** 2
+    got = n.astype(np.float32) * np.float32(2.0 ** -24)
+    assert np.array_equal(got, want)
+    # the no-seed value (32768, 32768) keys above the initial minDist (W^2) for every texel
+    for ii, jj in ((0, 0), (4095, 4095), (0, 4095)):
+        d = np.int64(32768 - ii) ** 2 + np.int64(32768 - jj) ** 2
+        assert min(d, 2 ** 31 - 1) >= W * W  # v_dot2_i32_i16 with clamp
+
+
+def test_jfa_scaled_float_key_matches_shader_distance():
+    """k_jfa_p2 fp32 key (power-of-two, non-square or > 4096): ((si-i)*scx)^2 + ((sj-j)*scy)^2
+    equals the shader distance times max(W,H)^2 exactly."""
+    rng = np.random.default_rng(8)
+    for W, H in ((128, 64), (64, 128), (8192, 8192), (16384, 256)):
+        mx = max(W, H)
+        i, j = W // 3, H // 5
+        si, sj = rng.integers(0, W, 100000), rng.integers(0, H, 100000)
+        want = _jfa_shader_key(si, sj, i, j, W, H)
+        f = np.float32
+        dx = (si - i).astype(f) * f(mx // W)
+        dy = (sj - j).astype(f) * f(mx // H)
+        got = (dx * dx + dy * dy) * f(1.0 / mx) * f(1.0 / mx)
+        assert np.array_equal(got, want), (W, H)
