@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define RC2DGI_ABI_VERSION 1
+#define RC2DGI_ABI_VERSION 2  /* 2: row-strip sharding entry points */
 
 typedef struct rc2dgi_ctx rc2dgi_ctx;
 
@@ -142,6 +142,8 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *   "blur_path"       blur / copy-back / merge kernels: 0 auto (fixed-tap blur with merge fused
  *                     where the sizes allow), 1 LDS-tiled blur + copy-back, then merge,
  *                     2 separate blur, copy-back and merge passes
+ *   "poison"          debug: fill the intermediate render textures with 0xFF bytes before each
+ *                     frame (rows a sharded frame never computes then read as NaN)
  * rc2dgi_get_tuning also answers "rc_variant_count". */
 int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
 int rc2dgi_get_tuning(rc2dgi_ctx *ctx, const char *key, int *value);
@@ -150,6 +152,42 @@ int rc2dgi_get_tuning(rc2dgi_ctx *ctx, const char *key, int *value);
  * as stored by its pass (costs N extra cascade textures and one copy per level). */
 int rc2dgi_set_keep_levels(rc2dgi_ctx *ctx, int enable);
 int rc2dgi_download_level(rc2dgi_ctx *ctx, int level, void *host, int pitch_bytes, int format);
+
+/* ---- row-strip sharding of one frame over `world` ranks.
+ * rc2dgi_set_shard: the context computes screen rows [rank*H/world, (rank+1)*H/world) of the
+ * merged colorRT / tempRT and exactly what they depend on (world = 1: the whole frame again).
+ * Other rows of its render textures are not meaningful.  Color / emissive inputs are uploaded
+ * whole to every rank.  The one exchange is distRT: after phase 1 (ScreenUV, JumpFlood,
+ * DistanceField) every rank's distRT strip goes to every other rank, then phase 2 (cascades,
+ * blur, merge) runs.  Three ways to run a sharded frame:
+ *   - rc2dgi_shard_connect: an RCCL communicator owned by the context (one process per GPU,
+ *     ranks = shards); rc2dgi_do then runs the frame with the exchange (ncclBroadcast of each
+ *     strip, grouped) on the context stream.  rc2dgi_shard_unique_id makes the id on rank 0;
+ *     the host passes it to the other ranks.
+ *   - rc2dgi_do_group: n contexts of one process, context k = shard k of n (any devices):
+ *     phase 1 on each, strips exchanged by device copies, phase 2 on each.
+ *   - rc2dgi_do_phase(ctx, 1); the host's own exchange (rc2dgi_device_buffer gives the
+ *     device pointer and pitch of distRT); rc2dgi_do_phase(ctx, 2).
+ * rc2dgi_do on a sharded context without a communicator returns RC2DGI_E_STATE. */
+#define RC2DGI_UNIQUE_ID_BYTES 128
+int rc2dgi_set_shard(rc2dgi_ctx *ctx, int rank, int world);
+int rc2dgi_shard_rows(rc2dgi_ctx *ctx, int *y0, int *y1);
+int rc2dgi_shard_unique_id(void *id, int nbytes);
+int rc2dgi_shard_connect(rc2dgi_ctx *ctx, const void *id, int nbytes);
+int rc2dgi_do_phase(rc2dgi_ctx *ctx, int phase);
+int rc2dgi_do_group(rc2dgi_ctx **ctxs, int n);
+/* raw device storage of a render texture: float4 texels (COLOR = merged output after a frame,
+ * else the input; GI1/GI2/BLUR/TEMP/EMISSIVE), uint16 q (DIST), uint32 packed seeds (JUMP1/2) */
+int rc2dgi_device_buffer(rc2dgi_ctx *ctx, int which, void **dev, int *pitch_bytes);
+
+/* host-only planner (no device needed): the rows a shard computes for one pass.
+ *   pass = RC2DGI_PLAN_JFA + step (screen rows; the last step also writes distRT)
+ *        | RC2DGI_PLAN_LEVEL + level (probe rows of every direction block)
+ *        | RC2DGI_PLAN_BLUR (cascade rows) | RC2DGI_PLAN_MERGE (screen rows)
+ * writes up to max_intervals [begin, end) pairs into `intervals`; returns the count. */
+enum { RC2DGI_PLAN_JFA = 0, RC2DGI_PLAN_LEVEL = 1000, RC2DGI_PLAN_BLUR = 2000, RC2DGI_PLAN_MERGE = 2001 };
+int rc2dgi_plan_rows(const rc2dgi_config *cfg, float blur_radius, int rank, int world, int pass, int *intervals,
+                     int max_intervals);
 
 #ifdef __cplusplus
 }

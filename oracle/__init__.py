@@ -81,6 +81,7 @@ def lib():
         L.orc_blur_copyback.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
         L.orc_merge.argtypes = [_f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 _f32p]
+        L.orc_set_rows.argtypes = [ctypes.c_int, ctypes.c_int]
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_set_num_threads.argtypes = [ctypes.c_int]
         _lib = L

@@ -173,6 +173,16 @@ int orc_sky_table(const orc_cfg *c, float *rgb) {
 
 /* ------------------------------------------------------------ passes */
 /* shaders/ScreenUV.fs:10-28 over a target cleared to (0,0,0,1) (RC2DGI.cs:278-285) */
+/* test-only row window (row-strip sharding tests): the JFA, DF, blur, copy-back and merge
+ * passes write only rows [g_row0, g_row1) when set; the default is every row */
+static int g_row0 = 0, g_row1 = 1 << 30;
+void orc_set_rows(int row0, int row1) {
+  g_row0 = row0 < 0 ? 0 : row0;
+  g_row1 = row1 < 0 ? (1 << 30) : row1;
+}
+static int row_lo(void) { return g_row0; }
+static int row_hi(int n) { return g_row1 < n ? g_row1 : n; }
+
 void orc_screen_uv(const float *color, float *jump, int W, int H, const float *tc) {
 #pragma omp parallel for schedule(static)
   for (int j = 0; j < H; ++j)
@@ -197,7 +207,7 @@ void orc_screen_uv(const float *color, float *jump, int W, int H, const float *t
 void orc_jfa_step(const float *src, float *dst, int W, int H, float step, float aspx, float aspy,
                   const float *tc) {
 #pragma omp parallel for schedule(static)
-  for (int j = 0; j < H; ++j)
+  for (int j = row_lo(); j < row_hi(H); ++j)
     for (int i = 0; i < W; ++i) {
       float u, v;
       tc_at(tc, i, j, W, H, &u, &v);
@@ -226,7 +236,7 @@ void orc_jfa_step(const float *src, float *dst, int W, int H, float step, float 
 /* shaders/DistanceField.fs:12-34 (packUNorm16 :12-19), RC2DGI.cs:328-340 */
 void orc_distance_field(const float *jump, float *dist, int W, int H, const float *tc) {
 #pragma omp parallel for schedule(static)
-  for (int j = 0; j < H; ++j)
+  for (int j = row_lo(); j < row_hi(H); ++j)
     for (int i = 0; i < W; ++i) {
       float u, v;
       tc_at(tc, i, j, W, H, &u, &v);
@@ -355,7 +365,7 @@ void orc_blur(const float *gi, float *blur, int CW, int CH, float radius, const 
                                0.125f,  0.125f,  0.125f,  0.250f};
   float tsx = 1.0f / (float)CW, tsy = 1.0f / (float)CH; /* texelSize = 1/_Resolution */
 #pragma omp parallel for schedule(static)
-  for (int j = 0; j < CH; ++j)
+  for (int j = row_lo(); j < row_hi(CH); ++j)
     for (int i = 0; i < CW; ++i) {
       float u, v;
       tc_at(tc, i, j, CW, CH, &u, &v);
@@ -380,7 +390,7 @@ void orc_blur(const float *gi, float *blur, int CW, int CH, float radius, const 
  * shader (texture*colDiffuse*fragColor, all white) -- blended, no clear. */
 void orc_blur_copyback(const float *blur, float *gi, int CW, int CH, const float *tc) {
 #pragma omp parallel for schedule(static)
-  for (int j = 0; j < CH; ++j)
+  for (int j = row_lo(); j < row_hi(CH); ++j)
     for (int i = 0; i < CW; ++i) {
       float u, v;
       tc_at(tc, i, j, CW, CH, &u, &v);
@@ -395,7 +405,7 @@ void orc_blur_copyback(const float *blur, float *gi, int CW, int CH, const float
 void orc_merge(const float *color, const float *gi, float *temp, float *color_out, int W, int H,
                int CW, int CH, const float *tc) {
 #pragma omp parallel for schedule(static)
-  for (int j = 0; j < H; ++j)
+  for (int j = row_lo(); j < row_hi(H); ++j)
     for (int i = 0; i < W; ++i) {
       float u, v;
       tc_at(tc, i, j, W, H, &u, &v);

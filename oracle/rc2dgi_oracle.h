@@ -82,6 +82,10 @@ void orc_merge(const float *color, const float *gi, float *temp, float *color_ou
 int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,
               const orc_overrides *ov, orc_frame_out *out);
 
+/* test-only: restrict the JFA / DF / blur / copy-back / merge passes to rows [row0, row1)
+ * (row1 < 0: all rows) -- row-strip sharding tests */
+void orc_set_rows(int row0, int row1);
+
 /* threads the restatement uses (OpenMP) */
 int orc_num_threads(void);
 void orc_set_num_threads(int n);

@@ -3,7 +3,9 @@
 // ping-pong identities) and :408-433 (uniform binding).
 #include "../../include/rc2dgi.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -15,6 +17,7 @@
 #include <vector>
 
 #include "rc2dgi_kernels.h"
+#include "rc2dgi_shard.h"
 
 using namespace rc2dgi;
 
@@ -26,6 +29,39 @@ enum Pass { P_SCREENUV = 0, P_JFA, P_RC, P_BLUR, P_MERGE, P_TOTAL, P_COUNT };
 
 inline bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// RCCL, resolved at first use (the single-GPU path never loads it).  In a process that already
+// loaded RCCL (e.g. through torch.distributed) dlopen returns that same library.
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclBroadcast) broadcast = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  bool ok = false;
+};
+
+const Rccl &rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return x;
+    x.get_unique_id = reinterpret_cast<decltype(x.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+    x.comm_init_rank = reinterpret_cast<decltype(x.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+    x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.group_start = reinterpret_cast<decltype(x.group_start)>(dlsym(h, "ncclGroupStart"));
+    x.group_end = reinterpret_cast<decltype(x.group_end)>(dlsym(h, "ncclGroupEnd"));
+    x.broadcast = reinterpret_cast<decltype(x.broadcast)>(dlsym(h, "ncclBroadcast"));
+    x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
+    x.ok = x.get_unique_id && x.comm_init_rank && x.comm_destroy && x.group_start && x.group_end && x.broadcast &&
+           x.error_string;
+    return x;
+  }();
+  return r;
+}
 
 }  // namespace
 
@@ -65,8 +101,15 @@ struct rc2dgi_ctx {
   std::vector<hipEvent_t> ev_level;  // N + 1
   std::vector<int> rc_variant;  // per level tile shape (tuning)
   int blur_path = 0;             // tuning "blur_path"
+  bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
+  // row-strip sharding
+  int rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
+  hipEvent_t ev_phase1 = nullptr;   // end of phase 1 (group exchange)
+  hipEvent_t ev_frame = nullptr;    // end of the last group frame (peers copy from our distRT)
+  bool gi1final = false;            // phase 1 -> phase 2 state
   std::string err;
 };
 
@@ -242,6 +285,10 @@ int upload_tables(rc2dgi_ctx *c) {
   return RC2DGI_OK;
 }
 
+FramePlan make_plan(const rc2dgi_ctx *c) {
+  return plan_frame(PlanInputs{c->W, c->H, c->CW, c->CH, c->S, c->N, c->blur_radius, c->rank, c->world});
+}
+
 bool screen_rt(int which) {
   return which == RC2DGI_RT_COLOR || which == RC2DGI_RT_EMISSIVE || which == RC2DGI_RT_JUMP1 ||
          which == RC2DGI_RT_JUMP2 || which == RC2DGI_RT_DIST || which == RC2DGI_RT_TEMP;
@@ -288,6 +335,8 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
   }
   c->stream = c->own_stream;
   for (auto &ev : c->ev) (void)hipEventCreate(&ev);
+  (void)hipEventCreateWithFlags(&c->ev_phase1, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&c->ev_frame, hipEventDisableTiming);
   rc = allocate(c);
   if (rc != RC2DGI_OK) {
     fprintf(stderr, "rc2dgi_create: %s\n", c->err.c_str());
@@ -303,6 +352,9 @@ int rc2dgi_destroy(rc2dgi_ctx *c) {
   if (!c) return RC2DGI_E_ARG;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
+  if (c->ev_phase1) (void)hipEventDestroy(c->ev_phase1);
+  if (c->ev_frame) (void)hipEventDestroy(c->ev_frame);
   free_buffers(c);
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -441,18 +493,25 @@ int rc2dgi_upload_device(rc2dgi_ctx *c, int which, const void *dev, int pitch_by
 }
 
 // ------------------------------------------------------------------ DoRC2DGI()
-int rc2dgi_do(rc2dgi_ctx *c) {
-  if (!c) return RC2DGI_E_ARG;
+namespace {
+
+// phase 1: ScreenUV, JumpFlood, DistanceField (RC2DGI.cs:276-340)
+int do_phase1(rc2dgi_ctx *c, const FramePlan &plan) {
   HIPCHK(c, hipSetDevice(c->device));
   int rc = upload_tables(c);
   if (rc != RC2DGI_OK) return rc;
   hipStream_t st = c->stream;
   const bool T = c->timing;
+  if (c->poison) {  // debug: rows a (sharded) frame never writes read as NaN / far seeds / far distance
+    const size_t ns = (size_t)c->sd.pitch * c->H, nc = (size_t)c->cd.pitch * c->CH;
+    HIPCHK(c, hipMemsetAsync(c->jump1, 0xFF, ns * 4, st));
+    HIPCHK(c, hipMemsetAsync(c->jump2, 0xFF, ns * 4, st));
+    HIPCHK(c, hipMemsetAsync(c->dist, 0xFF, ns * 2, st));
+    HIPCHK(c, hipMemsetAsync(c->temp, 0xFF, ns * 16, st));
+    HIPCHK(c, hipMemsetAsync(c->color_out, 0xFF, ns * 16, st));
+    for (float4 *b : {c->gi1, c->gi2, c->blur, c->gi_spare}) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * 16, st));
+  }
   if (T) HIPCHK(c, hipEventRecord(c->ev[0], st));
-
-  // aspect = (W, H) / max(W, H)  (RC2DGI.cs:273)
-  const int mx = c->W > c->H ? c->W : c->H;
-  const float aspx = (float)c->W / (float)mx, aspy = (float)c->H / (float)mx;
 
   // 1. ScreenUV (RC2DGI.cs:276-285): occupancy mask; J0 itself is only materialised when a
   //    single JFA step leaves it visible in jumpRT1
@@ -462,23 +521,26 @@ int rc2dgi_do(rc2dgi_ctx *c) {
 
   // 2. JumpFlood ping-pong (RC2DGI.cs:287-326); 3. DistanceField fused into the last step
   bool j1final = true;
-  float stepSize = 1.0f;
   for (int i = 0; i < c->S; ++i) {
-    stepSize *= 0.5f;
     float ox[3], oy[3];
-    for (int k = 0; k < 3; ++k) {  // vec2(x, y) * _Aspect.yx * _StepSize
-      ox[k] = ((float)(k - 1) * aspy) * stepSize;
-      oy[k] = ((float)(k - 1) * aspx) * stepSize;
-    }
+    jfa_offsets(c->W, c->H, i, ox, oy);  // vec2(x, y) * _Aspect.yx * _StepSize
     const bool last = i == c->S - 1;
     const unsigned *src = i == 0 ? c->occ : (j1final ? c->jump1 : c->jump2);
     unsigned *dst = j1final ? c->jump2 : c->jump1;
-    HIPCHK(c, launch_jfa_step(i == 0, src, i == 0 ? c->mpitch : c->sd.pitch, dst, last ? c->dist : nullptr, c->sd,
-                              ox, oy, st));
+    for (auto &r : plan.jfa[i].iv)
+      HIPCHK(c, launch_jfa_step(i == 0, src, i == 0 ? c->mpitch : c->sd.pitch, dst, last ? c->dist : nullptr,
+                                c->sd, ox, oy, st, r.first, r.second));
     j1final = !j1final;
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[2], st));
+  return RC2DGI_OK;
+}
 
+// phase 2: cascades, blur, merge (RC2DGI.cs:342-404)
+int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  const bool T = c->timing;
   // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362)
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
@@ -498,7 +560,11 @@ int rc2dgi_do(rc2dgi_ctx *c) {
     a.ray_range = c->ray_range;
     a.reflectivity = c->reflectivity;
     a.variant = c->rc_variant[L];
-    HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
+    for (auto &r : plan.level[L].iv) {
+      a.p0 = r.first;
+      a.p1 = r.second;
+      HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
+    }
     if (c->keep_levels)
       HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], dstGI, (size_t)c->cd.pitch * c->CH * sizeof(float4),
                                hipMemcpyDeviceToDevice, st));
@@ -516,27 +582,210 @@ int rc2dgi_do(rc2dgi_ctx *c) {
   bool merged = false;
   if (c->blur_radius > 0.0f) {
     bool fused = false;
-    if (c->blur_path == 0) {
-      const bool mrg = c->sd.W == c->CW && c->sd.H == c->CH;
-      fused = launch_blur_rows(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, c->color_in, c->temp,
-                               c->color_out, c->sd, mrg, st);
-      merged = fused && mrg;
+    BlurTaps bt;
+    const bool mrg = c->sd.W == c->CW && c->sd.H == c->CH;
+    if (c->blur_path == 0 && blur_rows_plan(c->cd, c->blur_radius, &bt) >= 0) {
+      for (auto &r : plan.blur.iv)
+        launch_blur_rows(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, c->color_in, c->temp, c->color_out,
+                         c->sd, mrg, st, r.first, r.second);
+      fused = true;
+      merged = mrg;
+    } else if (c->blur_path <= 1 && blur_fused_ok(c->cd, c->blur_radius)) {
+      for (auto &r : plan.blur.iv)
+        launch_blur_fused(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, st, r.first, r.second);
+      fused = true;
     }
-    if (!fused && c->blur_path <= 1) fused = launch_blur_fused(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, st);
     if (fused) {
       HIPCHK(c, hipGetLastError());
       std::swap(finalGI, c->gi_spare);
     } else {
-      HIPCHK(c, launch_blur(finalGI, c->blur, c->cd, c->blur_radius, st));
-      HIPCHK(c, launch_blur_copyback(c->blur, finalGI, c->cd, st));
+      for (auto &r : plan.blur.iv) HIPCHK(c, launch_blur(finalGI, c->blur, c->cd, c->blur_radius, st, r.first, r.second));
+      for (auto &r : plan.blur.iv) HIPCHK(c, launch_blur_copyback(c->blur, finalGI, c->cd, st, r.first, r.second));
     }
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[4], st));
-  if (!merged) HIPCHK(c, launch_merge(c->color_in, finalGI, c->temp, c->color_out, c->sd, c->cd, st));
+  if (!merged)
+    for (auto &r : plan.merge.iv)
+      HIPCHK(c, launch_merge(c->color_in, finalGI, c->temp, c->color_out, c->sd, c->cd, st, r.first, r.second));
   if (T) HIPCHK(c, hipEventRecord(c->ev[5], st));
   c->frame_done = true;
   c->have_frame = true;
   return RC2DGI_OK;
+}
+
+// distRT strip of shard q: device pointer and byte count (rows are contiguous, pitch-linear)
+void dist_strip(const rc2dgi_ctx *c, int q, unsigned short **p, size_t *bytes) {
+  int y0, y1;
+  strip_rows(c->H, q, c->world, y0, y1);
+  *p = c->dist + (size_t)y0 * c->sd.pitch;
+  *bytes = (size_t)(y1 - y0) * c->sd.pitch * sizeof(unsigned short);
+}
+
+}  // namespace
+
+int rc2dgi_do(rc2dgi_ctx *c) {
+  if (!c) return RC2DGI_E_ARG;
+  if (c->world > 1 && !c->comm)
+    return fail(c, RC2DGI_E_STATE, "sharded context: use rc2dgi_shard_connect, rc2dgi_do_group or rc2dgi_do_phase");
+  const FramePlan plan = make_plan(c);
+  int rc = do_phase1(c, plan);
+  if (rc != RC2DGI_OK) return rc;
+  if (c->comm) {  // every strip of distRT to every rank: one in-place broadcast per root
+    const Rccl &R = rccl();
+    ncclResult_t e = R.group_start();
+    for (int q = 0; q < c->world && e == ncclSuccess; ++q) {
+      unsigned short *p;
+      size_t n;
+      dist_strip(c, q, &p, &n);
+      e = R.broadcast(p, p, n, ncclUint8, q, c->comm, c->stream);
+    }
+    const ncclResult_t e2 = R.group_end();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess) return fail(c, RC2DGI_E_HIP, std::string("ncclBroadcast: ") + R.error_string(e));
+  }
+  return do_phase2(c, plan);
+}
+
+int rc2dgi_do_phase(rc2dgi_ctx *c, int phase) {
+  if (!c) return RC2DGI_E_ARG;
+  if (phase != 1 && phase != 2) return fail(c, RC2DGI_E_ARG, "phase is 1 or 2");
+  const FramePlan plan = make_plan(c);
+  return phase == 1 ? do_phase1(c, plan) : do_phase2(c, plan);
+}
+
+int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
+  if (!cs || n < 1) return RC2DGI_E_ARG;
+  for (int k = 0; k < n; ++k) {
+    if (!cs[k]) return RC2DGI_E_ARG;
+    const rc2dgi_ctx *c = cs[k];
+    if (c->rank != k || c->world != n || c->W != cs[0]->W || c->H != cs[0]->H || c->N != cs[0]->N ||
+        c->CW != cs[0]->CW || c->CH != cs[0]->CH)
+      return fail(cs[k], RC2DGI_E_ARG, "rc2dgi_do_group: context k must be shard k of n of one configuration");
+  }
+  // a peer may still be copying our previous distRT strip: wait for every peer's last frame
+  for (int k = 0; k < n; ++k) {
+    HIPCHK(cs[k], hipSetDevice(cs[k]->device));
+    for (int q = 0; q < n; ++q)
+      if (q != k) HIPCHK(cs[k], hipStreamWaitEvent(cs[k]->stream, cs[q]->ev_frame, 0));
+  }
+  for (int k = 0; k < n; ++k) {
+    int rc = do_phase1(cs[k], make_plan(cs[k]));
+    if (rc != RC2DGI_OK) return rc;
+    HIPCHK(cs[k], hipEventRecord(cs[k]->ev_phase1, cs[k]->stream));
+  }
+  for (int k = 0; k < n; ++k) {
+    rc2dgi_ctx *c = cs[k];
+    HIPCHK(c, hipSetDevice(c->device));
+    for (int q = 0; q < n; ++q) {
+      if (q == k) continue;
+      HIPCHK(c, hipStreamWaitEvent(c->stream, cs[q]->ev_phase1, 0));
+      unsigned short *src, *dst;
+      size_t bytes;
+      dist_strip(cs[q], q, &src, &bytes);
+      dist_strip(c, q, &dst, &bytes);
+      HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    }
+  }
+  // phase 2 of a context overwrites nothing a peer still copies from (only distRT is read)
+  for (int k = 0; k < n; ++k) {
+    int rc = do_phase2(cs[k], make_plan(cs[k]));
+    if (rc != RC2DGI_OK) return rc;
+    HIPCHK(cs[k], hipEventRecord(cs[k]->ev_frame, cs[k]->stream));
+  }
+  return RC2DGI_OK;
+}
+
+int rc2dgi_set_shard(rc2dgi_ctx *c, int rank, int world) {
+  if (!c) return RC2DGI_E_ARG;
+  if (world < 1 || rank < 0 || rank >= world || world > c->H)
+    return fail(c, RC2DGI_E_ARG, "rank must be in [0, world), world in [1, H]");
+  if ((world != c->world || rank != c->rank) && c->comm) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)rccl().comm_destroy(c->comm);
+    c->comm = nullptr;
+  }
+  c->rank = rank;
+  c->world = world;
+  c->frame_done = c->have_frame = false;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_shard_rows(rc2dgi_ctx *c, int *y0, int *y1) {
+  if (!c || !y0 || !y1) return RC2DGI_E_ARG;
+  strip_rows(c->H, c->rank, c->world, *y0, *y1);
+  return RC2DGI_OK;
+}
+
+int rc2dgi_shard_unique_id(void *id, int nbytes) {
+  if (!id || nbytes < (int)sizeof(ncclUniqueId)) return RC2DGI_E_ARG;
+  const Rccl &R = rccl();
+  if (!R.ok) return RC2DGI_E_UNSUPPORTED;
+  ncclUniqueId u;
+  if (R.get_unique_id(&u) != ncclSuccess) return RC2DGI_E_HIP;
+  std::memcpy(id, &u, sizeof(u));
+  return RC2DGI_OK;
+}
+
+int rc2dgi_shard_connect(rc2dgi_ctx *c, const void *id, int nbytes) {
+  if (!c || !id || nbytes < (int)sizeof(ncclUniqueId)) return fail(c, RC2DGI_E_ARG, "bad unique id");
+  const Rccl &R = rccl();
+  if (!R.ok) return fail(c, RC2DGI_E_UNSUPPORTED, "librccl not found");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->comm) {
+    (void)R.comm_destroy(c->comm);
+    c->comm = nullptr;
+  }
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  const ncclResult_t e = R.comm_init_rank(&c->comm, c->world, u, c->rank);
+  if (e != ncclSuccess) {
+    c->comm = nullptr;
+    return fail(c, RC2DGI_E_HIP, std::string("ncclCommInitRank: ") + R.error_string(e));
+  }
+  return RC2DGI_OK;
+}
+
+int rc2dgi_device_buffer(rc2dgi_ctx *c, int which, void **dev, int *pitch_bytes) {
+  if (!c || !dev || !pitch_bytes) return RC2DGI_E_ARG;
+  if (which == RC2DGI_RT_FINAL_GI) which = c->final_gi == 2 ? RC2DGI_RT_GI2 : RC2DGI_RT_GI1;
+  const int sp = c->sd.pitch, cp = c->cd.pitch;
+  switch (which) {
+    case RC2DGI_RT_COLOR: *dev = c->frame_done ? c->color_out : c->color_in; *pitch_bytes = sp * 16; break;
+    case RC2DGI_RT_EMISSIVE: *dev = c->emissive; *pitch_bytes = sp * 16; break;
+    case RC2DGI_RT_TEMP: *dev = c->temp; *pitch_bytes = sp * 16; break;
+    case RC2DGI_RT_JUMP1: *dev = c->jump1; *pitch_bytes = sp * 4; break;
+    case RC2DGI_RT_JUMP2: *dev = c->jump2; *pitch_bytes = sp * 4; break;
+    case RC2DGI_RT_DIST: *dev = c->dist; *pitch_bytes = sp * 2; break;
+    case RC2DGI_RT_GI1: *dev = c->gi1; *pitch_bytes = cp * 16; break;
+    case RC2DGI_RT_GI2: *dev = c->gi2; *pitch_bytes = cp * 16; break;
+    case RC2DGI_RT_BLUR: *dev = c->blur; *pitch_bytes = cp * 16; break;
+    default: return fail(c, RC2DGI_E_ARG, "bad render texture id");
+  }
+  return RC2DGI_OK;
+}
+
+int rc2dgi_plan_rows(const rc2dgi_config *cfg, float blur_radius, int rank, int world, int pass, int *intervals,
+                     int max_intervals) {
+  if (!cfg || cfg->screen_width <= 0 || cfg->screen_height <= 0 || cfg->cascade_count < 1 ||
+      cfg->cascade_count > 15 || !(cfg->render_scale > 0.0f) || world < 1 || rank < 0 || rank >= world ||
+      world > cfg->screen_height)
+    return RC2DGI_E_ARG;
+  int CW, CH, S;
+  derive_sizes(cfg->screen_width, cfg->screen_height, cfg->cascade_count, cfg->render_scale, CW, CH, S);
+  const FramePlan p =
+      plan_frame(PlanInputs{cfg->screen_width, cfg->screen_height, CW, CH, S, cfg->cascade_count, blur_radius, rank, world});
+  const RowSet *rs = nullptr;
+  if (pass >= RC2DGI_PLAN_JFA && pass < RC2DGI_PLAN_JFA + S) rs = &p.jfa[pass - RC2DGI_PLAN_JFA];
+  else if (pass >= RC2DGI_PLAN_LEVEL && pass < RC2DGI_PLAN_LEVEL + cfg->cascade_count) rs = &p.level[pass - RC2DGI_PLAN_LEVEL];
+  else if (pass == RC2DGI_PLAN_BLUR) rs = &p.blur;
+  else if (pass == RC2DGI_PLAN_MERGE) rs = &p.merge;
+  else return RC2DGI_E_ARG;
+  const int n = (int)rs->iv.size();
+  for (int k = 0; k < n && k < max_intervals && intervals; ++k) {
+    intervals[2 * k] = rs->iv[k].first;
+    intervals[2 * k + 1] = rs->iv[k].second;
+  }
+  return n;
 }
 
 int rc2dgi_sync(rc2dgi_ctx *c) {
@@ -628,6 +877,10 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->blur_path = value;
     return RC2DGI_OK;
   }
+  if (k == "poison") {
+    c->poison = value != 0;
+    return RC2DGI_OK;
+  }
   return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);
 }
 
@@ -646,6 +899,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "blur_path") {
     *value = c->blur_path;
+    return RC2DGI_OK;
+  }
+  if (k == "poison") {
+    *value = c->poison ? 1 : 0;
     return RC2DGI_OK;
   }
   return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);

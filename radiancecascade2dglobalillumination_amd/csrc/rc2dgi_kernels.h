@@ -16,6 +16,12 @@ struct BlurTaps {
   float w0, w2;   // weights of the "-radius" and "+radius" tap pairs
 };
 
+// power-of-two JFA: integer tap offsets and the distance-key scaling (see k_jfa_p2)
+struct JfaTaps {
+  int dx[3], dy[3];
+  float scx, scy, dinit;
+};
+
 struct CascadeDims {
   int CW, CH;
   int pitch;
@@ -32,7 +38,11 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
 // off_x/off_y = vec2(k,k)*_Aspect.yx*_StepSize for k = -1,0,1 (host-computed).
 // dist != nullptr fuses DistanceField.fs: stores the 16-bit q of packUNorm16.
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
-                           ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st);
+                           ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0 = 0,
+                           int row1 = -1);  // output rows [row0, row1) (-1 = H)
+// integer taps of the power-of-two JFA kernel (false: the float path runs); also used by the
+// row-strip planner
+bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp);
 
 struct RcLevelArgs {
   const float4 *upper;   // G_{L+1} (nullptr at the top level)
@@ -45,6 +55,7 @@ struct RcLevelArgs {
   int level, N;
   float ray_range, reflectivity;
   int variant;           // tile shape (rc_variant_name)
+  int p0 = 0, p1 = -1;   // probe rows [p0, p1) of every direction block (-1 = all)
 };
 
 int rc_variant_count();
@@ -54,23 +65,27 @@ const char *rc_variant_name(int v);
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);
 
 // Blur.fs into blur_out, then the default-shader blended copy-back into gi (RC2DGI.cs:367-387)
-hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st);
-hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st);
+hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st,
+                       int row0 = 0, int row1 = -1);
+hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st, int row0 = 0,
+                                int row1 = -1);
 // both in one pass (power-of-two cascade sizes, radius <= 6); gi_out may not alias gi_in.
 // Returns false (nothing launched) when the shape is not supported.
+bool blur_fused_ok(CascadeDims c, float radius);  // power-of-two sizes, radius <= 6
 bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
-                       hipStream_t st);
+                       hipStream_t st, int row0 = 0, int row1 = -1);
 
 // Blur + copy-back (+ merge and its copy-back when `merge`) with fixed taps; false when the
 // radius / sizes do not allow it (see k_blur_rows).  blur_rows_plan: F = floor(radius) or -1.
 int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt);
 bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
                       const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
-                      hipStream_t st);
+                      hipStream_t st, int row0 = 0, int row1 = -1);
 
 // merge.fs into temp, then tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
 hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,
-                        CascadeDims c, hipStream_t st);
+                        CascadeDims c, hipStream_t st, int row0 = 0,
+                        int row1 = -1);
 
 // format conversion for uploads from device memory: RGBA8 unorm -> float4 (k/255)
 hipError_t launch_unorm8_to_f32(const unsigned char *src, int src_pitch_bytes, float4 *dst, int dst_pitch, int W,

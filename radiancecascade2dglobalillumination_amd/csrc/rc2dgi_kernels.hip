@@ -75,11 +75,6 @@ struct JfaOffsets {
   float ox[3], oy[3];
 };
 
-// power-of-two screens: integer tap offsets and the distance-key scaling (see k_jfa_p2)
-struct JfaTaps {
-  int dx[3], dy[3];
-  float scx, scy, dinit;
-};
 
 // One JumpFlood.fs step.  FIRST: taps read the occupancy mask (the ScreenUV seeds); otherwise the
 // packed seeds of the previous step.  dist != nullptr fuses DistanceField.fs.
@@ -89,9 +84,9 @@ constexpr int JT = 4;
 template <bool FIRST>
 __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ src, int src_pitch,
                                                   unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
-                                                  ScreenDims s, JfaOffsets o) {
+                                                  ScreenDims s, JfaOffsets o, int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j0 = blockIdx.y * (4 * JT) + (threadIdx.x >> 6);
+  const int j0 = row0 + blockIdx.y * (4 * JT) + (threadIdx.x >> 6);
   if (i >= s.W) return;
   const Axis ax{s.W, s.powW}, ay{s.H, s.powH};
   const float u = texcoord(i, ax);
@@ -101,7 +96,7 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
   unsigned seed[JT][9];
 #pragma unroll
   for (int t = 0; t < JT; ++t) {
-    const int j = min(j0 + 4 * t, s.H - 1);  // clamped rows are computed but not stored
+    const int j = min(j0 + 4 * t, row1 - 1);  // clamped rows are computed but not stored
     const float v = texcoord(j, ay);
 #pragma unroll
     for (int y = 0; y < 3; ++y) {
@@ -120,7 +115,7 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
 #pragma unroll
   for (int t = 0; t < JT; ++t) {
     const int j = j0 + 4 * t;
-    if (j >= s.H) break;
+    if (j >= row1) break;
     const float v = texcoord(j, ay);
     float minDist = 1.0f, bx = 0.0f, by = 0.0f;
     unsigned best = kNoSeed;
@@ -166,9 +161,9 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
 template <bool FIRST, bool IKEY>
 __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src, int src_pitch,
                                                 unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
-                                                ScreenDims s, JfaTaps o) {
+                                                ScreenDims s, JfaTaps o, int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j0 = blockIdx.y * (4 * JT) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j0 = row0 + blockIdx.y * (4 * JT) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (i >= s.W) return;
   unsigned ti[3];  // unsigned: scalar row base + 32-bit lane offset addressing
 #pragma unroll
@@ -176,7 +171,7 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
   unsigned seed[JT][9];
 #pragma unroll
   for (int t = 0; t < JT; ++t) {
-    const int j = min(j0 + 4 * t, s.H - 1);  // clamped rows are computed but not stored
+    const int j = min(j0 + 4 * t, row1 - 1);  // clamped rows are computed but not stored
 #pragma unroll
     for (int y = 0; y < 3; ++y) {
       const unsigned tj = (unsigned)(j + o.dy[y]) & (unsigned)(s.H - 1);
@@ -196,7 +191,7 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
 #pragma unroll
   for (int t = 0; t < JT; ++t) {
     const int j = j0 + 4 * t;
-    if (j >= s.H) break;
+    if (j >= row1) break;
     float minKey = o.dinit;
     unsigned best = kNoSeed;
     const unsigned here = pack_seed(i, j);
@@ -237,6 +232,7 @@ struct RcParams {
   ScreenDims s;
   CascadeDims c;
   int level, bsc, bdx, bdy, tiles_x, tiles_per_block;
+  int p0, p1;  // probe rows [p0, p1) of every direction block (row-strip shards; 0, bdy otherwise)
   float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
   float aspx, aspy, t0, t1, reflectivity;
 };
@@ -297,7 +293,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   const int tile = logical / ngrp;
   const int bi0 = (logical - tile * ngrp) * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
   const int ty = tile / P.tiles_x, tx = tile - ty * P.tiles_x;
-  const int cx0 = tx * TX, cy0 = ty * THY;
+  const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
   const int cx = cx0 + (int)(threadIdx.x % TX);
   const int cyb = cy0 + (int)(threadIdx.x / TX);
   const bool xok = cx < P.bdx;
@@ -334,7 +330,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
 #pragma unroll
   for (int p = 0; p < PY; ++p) {
     const int cy = cyb + p * TY;
-    pok[p] = xok && cy < P.bdy;
+    pok[p] = xok && cy < P.p1;
     oy[p] = div_res(((float)cy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P.c.powH);
   }
   const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
@@ -516,10 +512,10 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
 
 // ---------------------------------------------------------------- Blur + copy-back
 __global__ __launch_bounds__(256) void k_blur(const float4 *__restrict__ gi, float4 *__restrict__ blur_out,
-                                              CascadeDims c, float radius) {
+                                              CascadeDims c, float radius, int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (i >= c.CW || j >= c.CH) return;
+  const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= c.CW || j >= row1) return;
   const Axis ax{c.CW, c.powW}, ay{c.CH, c.powH};
   const float u = texcoord(i, ax), v = texcoord(j, ay);
   const float tsx = 1.0f / (float)c.CW, tsy = 1.0f / (float)c.CH;
@@ -551,10 +547,12 @@ __global__ __launch_bounds__(256) void k_blur(const float4 *__restrict__ gi, flo
 // bilinear tap of radius <= H - 2 (taps that ever fall outside are read from HBM).
 template <int H>
 __global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ gi_in, float4 *__restrict__ blur_out,
-                                                    float4 *__restrict__ gi_out, CascadeDims c, float radius) {
+                                                    float4 *__restrict__ gi_out, CascadeDims c, float radius,
+                                                    int tile0) {
   constexpr int TW = 64 + 2 * H, TH = 16 + 2 * H;
   __shared__ float4 tile[TH * TW];
-  const int x0 = blockIdx.x * 64 - H, y0 = blockIdx.y * 16 - H;
+  const int by = (int)blockIdx.y + tile0;  // 16-row tile
+  const int x0 = blockIdx.x * 64 - H, y0 = by * 16 - H;
   for (int k = threadIdx.x; k < TW * TH; k += 256) {
     const int ty = k / TW, tx = k - ty * TW;
     const int gx = (x0 + tx) & (c.CW - 1), gy = (y0 + ty) & (c.CH - 1);
@@ -584,7 +582,7 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ g
   constexpr float KW[9] = {0.0625f, 0.0625f, 0.0625f, 0.0625f, 0.125f, 0.125f, 0.125f, 0.125f, 0.250f};
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int j = blockIdx.y * 16 + (threadIdx.x >> 6) + 4 * t;
+    const int j = by * 16 + (threadIdx.x >> 6) + 4 * t;
     if (i >= c.CW || j >= c.CH) continue;
     const float v = texcoord(j, ay);
     int ya[3], yb[3];
@@ -645,10 +643,11 @@ template <int F, bool MERGE>
 __global__ __launch_bounds__(256) void k_blur_rows(const float4 *__restrict__ gi_in, float4 *__restrict__ blur_out,
                                                    float4 *__restrict__ gi_out, CascadeDims c, BlurTaps bt,
                                                    const float4 *__restrict__ color_in, float4 *__restrict__ temp,
-                                                   float4 *__restrict__ color_out, int spitch) {
+                                                   float4 *__restrict__ color_out, int spitch, int tile0) {
   constexpr int HALO = F + 1, TW = 64 + 2 * HALO, TH = 32 + 2 * HALO, NR = 8 + 2 * HALO;
   __shared__ float4 tile[TH * TW];
-  const int x0 = blockIdx.x * 64 - HALO, y0 = blockIdx.y * 32 - HALO;
+  const int by = (int)blockIdx.y + tile0;  // 32-row tile
+  const int x0 = blockIdx.x * 64 - HALO, y0 = by * 32 - HALO;
   for (int k = threadIdx.x; k < TW * TH; k += 256) {
     const int ty = k / TW, tx = k - ty * TW;
     const int gx = (x0 + tx) & (c.CW - 1), gy = (y0 + ty) & (c.CH - 1);
@@ -699,7 +698,7 @@ __global__ __launch_bounds__(256) void k_blur_rows(const float4 *__restrict__ gi
     }
     const float4 b = blend_over_black(res);  // cascadeBlurRT cleared to (0,0,0,1)
     const float4 g = blend(b, h[m][1]);      // copy-back onto finalGI, blended
-    const int j = blockIdx.y * 32 + r0 + t;
+    const int j = by * 32 + r0 + t;
     const size_t o = (size_t)j * c.pitch + i;
     blur_out[o] = b;
     gi_out[o] = g;
@@ -716,10 +715,10 @@ __global__ __launch_bounds__(256) void k_blur_rows(const float4 *__restrict__ gi
 }
 
 __global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict__ blur, float4 *__restrict__ gi,
-                                                       CascadeDims c) {
+                                                       CascadeDims c, int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (i >= c.CW || j >= c.CH) return;
+  const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= c.CW || j >= row1) return;
   const float u = texcoord(i, Axis{c.CW, c.powW}), v = texcoord(j, Axis{c.CH, c.powH});
   const float4 s = sample_bilinear(blur, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
   const size_t o = (size_t)j * c.pitch + i;
@@ -729,10 +728,10 @@ __global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict_
 // ---------------------------------------------------------------- Merge + copy-back
 __global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_in, const float4 *__restrict__ gi,
                                                float4 *__restrict__ temp, float4 *__restrict__ color_out,
-                                               ScreenDims s, CascadeDims c) {
+                                               ScreenDims s, CascadeDims c, int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (i >= s.W || j >= s.H) return;
+  const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= s.W || j >= row1) return;
   const float u = texcoord(i, Axis{s.W, s.powW}), v = texcoord(j, Axis{s.H, s.powH});
   const size_t o = (size_t)j * s.pitch + i;
   const float4 col = color_in[o];
@@ -796,18 +795,22 @@ bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTa
 }
 
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
-                           ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st) {
+                           ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0,
+                           int row1) {
+  if (row1 < 0 || row1 > s.H) row1 = s.H;
+  if (row0 < 0) row0 = 0;
+  if (row0 >= row1) return hipSuccess;
   JfaOffsets o;
   for (int k = 0; k < 3; ++k) {
     o.ox[k] = off_x[k];
     o.oy[k] = off_y[k];
   }
-  const dim3 grid(ceil_div(s.W, 64), ceil_div(s.H, 4 * JT));
+  const dim3 grid(ceil_div(s.W, 64), ceil_div(row1 - row0, 4 * JT));
   JfaTaps tp;
   if (jfa_p2_taps(s, off_x, off_y, &tp)) {
     const bool ikey = s.W == s.H && s.W <= 4096;
 #define RC2DGI_JFA(F, K) \
-  hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp)
+  hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1)
     if (first) {
       if (ikey) RC2DGI_JFA(true, true); else RC2DGI_JFA(true, false);
     } else {
@@ -815,9 +818,9 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     }
 #undef RC2DGI_JFA
   } else if (first) {
-    hipLaunchKernelGGL(k_jfa_step<true>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
+    hipLaunchKernelGGL(k_jfa_step<true>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
   } else {
-    hipLaunchKernelGGL(k_jfa_step<false>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o);
+    hipLaunchKernelGGL(k_jfa_step<false>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
   }
   return hipGetLastError();
 }
@@ -825,7 +828,7 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
 template <int TX, int TY, int PY, int PD = 1, bool MASKED = false>
 static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
-  P.tiles_per_block = P.tiles_x * ceil_div(P.bdy, TY * PY);
+  P.tiles_per_block = P.tiles_x * ceil_div(P.p1 - P.p0, TY * PY);
   const int nwg = P.tiles_per_block * P.bsc * P.bsc / PD;
   if (a.level == a.N - 1)
     hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, true, MASKED>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper,
@@ -851,6 +854,8 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.bsc = 1 << a.level;
   P.bdx = c.CW >> a.level;
   P.bdy = c.CH >> a.level;
+  P.p0 = a.p0 < 0 ? 0 : a.p0;
+  P.p1 = (a.p1 < 0 || a.p1 > P.bdy) ? P.bdy : a.p1;
   P.CRx = (float)c.CW;
   P.CRy = (float)c.CH;
   P.invCRx = 1.0f / P.CRx;  // used only when CW / CH are powers of two (then exact)
@@ -887,19 +892,34 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   return hipGetLastError();
 }
 
-hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st) {
-  hipLaunchKernelGGL(k_blur, grid2d(c.CW, c.CH), dim3(256), 0, st, gi, blur_out, c, radius);
+static void clamp_rows(int n, int &row0, int &row1) {
+  if (row1 < 0 || row1 > n) row1 = n;
+  if (row0 < 0) row0 = 0;
+}
+
+hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st, int row0,
+                       int row1) {
+  clamp_rows(c.CH, row0, row1);
+  if (row0 >= row1) return hipSuccess;
+  hipLaunchKernelGGL(k_blur, grid2d(c.CW, row1 - row0), dim3(256), 0, st, gi, blur_out, c, radius, row0, row1);
   return hipGetLastError();
 }
 
+bool blur_fused_ok(CascadeDims c, float radius) {
+  return c.powW && c.powH && c.CW >= 64 && c.CH >= 16 && radius <= 6.0f;
+}
+
 bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
-                       hipStream_t st) {
-  if (!(c.powW && c.powH) || c.CW < 64 || c.CH < 16) return false;
-  const dim3 grid(ceil_div(c.CW, 64), ceil_div(c.CH, 16));
+                       hipStream_t st, int row0, int row1) {
+  if (!blur_fused_ok(c, radius)) return false;
+  clamp_rows(c.CH, row0, row1);
+  if (row0 >= row1) return true;
+  const int t0 = row0 / 16, t1 = ceil_div(row1, 16);  // whole 16-row tiles
+  const dim3 grid(ceil_div(c.CW, 64), t1 - t0);
   if (radius <= 2.0f)
-    hipLaunchKernelGGL(k_blur_fused<4>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius);
+    hipLaunchKernelGGL(k_blur_fused<4>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius, t0);
   else if (radius <= 6.0f)
-    hipLaunchKernelGGL(k_blur_fused<8>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius);
+    hipLaunchKernelGGL(k_blur_fused<8>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius, t0);
   else
     return false;
   return true;
@@ -918,15 +938,18 @@ int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt) {
 
 bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
                       const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
-                      hipStream_t st) {
+                      hipStream_t st, int row0, int row1) {
   BlurTaps bt;
   const int F = blur_rows_plan(c, radius, &bt);
   if (F < 0) return false;
   if (merge && !(s.W == c.CW && s.H == c.CH)) return false;
-  const dim3 grid(c.CW / 64, c.CH / 32);
+  clamp_rows(c.CH, row0, row1);
+  if (row0 >= row1) return true;
+  const int t0 = row0 / 32, t1 = ceil_div(row1, 32);  // whole 32-row tiles
+  const dim3 grid(c.CW / 64, t1 - t0);
 #define RC2DGI_BLUR_ROWS(FV, MV)                                                                               \
   hipLaunchKernelGGL((k_blur_rows<FV, MV>), grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, bt, color_in, \
-                     temp, color_out, s.pitch)
+                     temp, color_out, s.pitch, t0)
   if (merge) {
     if (F == 0) RC2DGI_BLUR_ROWS(0, true); else if (F == 1) RC2DGI_BLUR_ROWS(1, true); else RC2DGI_BLUR_ROWS(2, true);
   } else {
@@ -936,14 +959,19 @@ bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Cas
   return true;
 }
 
-hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st) {
-  hipLaunchKernelGGL(k_blur_copyback, grid2d(c.CW, c.CH), dim3(256), 0, st, blur, gi, c);
+hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st, int row0, int row1) {
+  clamp_rows(c.CH, row0, row1);
+  if (row0 >= row1) return hipSuccess;
+  hipLaunchKernelGGL(k_blur_copyback, grid2d(c.CW, row1 - row0), dim3(256), 0, st, blur, gi, c, row0, row1);
   return hipGetLastError();
 }
 
 hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,
-                        CascadeDims c, hipStream_t st) {
-  hipLaunchKernelGGL(k_merge, grid2d(s.W, s.H), dim3(256), 0, st, color_in, gi, temp, color_out, s, c);
+                        CascadeDims c, hipStream_t st, int row0, int row1) {
+  clamp_rows(s.H, row0, row1);
+  if (row0 >= row1) return hipSuccess;
+  hipLaunchKernelGGL(k_merge, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in, gi, temp, color_out, s, c,
+                     row0, row1);
   return hipGetLastError();
 }
 

@@ -90,6 +90,15 @@ def load_library(path: Optional[str] = None):
         "rc2dgi_set_tuning": ([vp, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
         "rc2dgi_get_tuning": ([vp, ctypes.c_char_p, ip], ctypes.c_int),
         "rc2dgi_download_level": ([vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_set_shard": ([vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_shard_rows": ([vp, ip, ip], ctypes.c_int),
+        "rc2dgi_shard_unique_id": ([vp, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_shard_connect": ([vp, vp, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_do_phase": ([vp, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_do_group": ([ctypes.POINTER(vp), ctypes.c_int], ctypes.c_int),
+        "rc2dgi_device_buffer": ([vp, ctypes.c_int, ctypes.POINTER(vp), ip], ctypes.c_int),
+        "rc2dgi_plan_rows": ([ctypes.POINTER(_Config), ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip,
+                              ctypes.c_int], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -305,6 +314,34 @@ class RC2DGI:
             d["levels"] = [float(x) for x in lv[:levels]]
         return d
 
+    # ---------------------------------------------------------------- row-strip sharding
+    def set_shard(self, rank: int, world: int) -> None:
+        """Compute screen rows [rank*H/world, (rank+1)*H/world) of the merged colorRT (and what
+        they depend on).  world = 1: the whole frame."""
+        self._check(self._L.rc2dgi_set_shard(self._h, int(rank), int(world)), "set_shard")
+
+    def shard_rows(self):
+        y0, y1 = ctypes.c_int(), ctypes.c_int()
+        self._check(self._L.rc2dgi_shard_rows(self._h, ctypes.byref(y0), ctypes.byref(y1)), "shard_rows")
+        return y0.value, y1.value
+
+    def connect(self, unique_id: bytes) -> None:
+        """RCCL communicator over the shards (one process per GPU); then do_rc2dgi() runs the
+        distRT exchange itself."""
+        buf = ctypes.create_string_buffer(bytes(unique_id), UNIQUE_ID_BYTES)
+        self._check(self._L.rc2dgi_shard_connect(self._h, buf, UNIQUE_ID_BYTES), "shard_connect")
+
+    def do_phase(self, phase: int) -> None:
+        """1: ScreenUV + JumpFlood + DistanceField; 2: cascades, blur, merge (exchange distRT between)."""
+        self._check(self._L.rc2dgi_do_phase(self._h, int(phase)), f"do_phase {phase}")
+
+    def device_buffer(self, which: str):
+        """(device pointer, pitch in bytes) of a render texture's raw storage."""
+        p, pitch = ctypes.c_void_p(), ctypes.c_int()
+        self._check(self._L.rc2dgi_device_buffer(self._h, RT[which], ctypes.byref(p), ctypes.byref(pitch)),
+                    f"device_buffer {which}")
+        return p.value, pitch.value
+
     def frame(self, color, emissive) -> None:
         """Upload the painted scene and run one DoRC2DGI() (the reference's per-frame order,
         RC2DGI.cs:122-132)."""
@@ -317,4 +354,45 @@ def abi_version() -> int:
     return load_library().rc2dgi_abi_version()
 
 
-__all__ = ["RC2DGI", "RC2DGIError", "load_library", "abi_version", "RT", "PASS_NAMES"]
+UNIQUE_ID_BYTES = 128
+PLAN_JFA, PLAN_LEVEL, PLAN_BLUR, PLAN_MERGE = 0, 1000, 2000, 2001
+
+
+def shard_unique_id() -> bytes:
+    """RCCL unique id for rc2dgi_shard_connect (create on rank 0, send to the other ranks)."""
+    L = load_library()
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    rc = L.rc2dgi_shard_unique_id(buf, UNIQUE_ID_BYTES)
+    if rc != 0:
+        raise RC2DGIError(rc, "rc2dgi_shard_unique_id")
+    return buf.raw
+
+
+def do_group(ctxs: Sequence["RC2DGI"]) -> None:
+    """One sharded frame over in-process contexts (context k = shard k of len(ctxs))."""
+    L = load_library()
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    rc = L.rc2dgi_do_group(arr, len(ctxs))
+    if rc != 0:
+        msgs = [c._L.rc2dgi_last_error(c._h) for c in ctxs]
+        raise RC2DGIError(rc, "rc2dgi_do_group: " + "; ".join(m.decode() for m in msgs if m))
+
+
+def plan_rows(W: int, H: int, N: int, blur_radius: float, rank: int, world: int, pass_id: int,
+              render_scale: float = 1.0):
+    """Host-only planner: [(begin, end), ...] rows shard `rank` of `world` computes for a pass
+    (PLAN_JFA + step, PLAN_LEVEL + level, PLAN_BLUR, PLAN_MERGE)."""
+    L = load_library()
+    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, (ctypes.c_int * 5)())
+    buf = (ctypes.c_int * 64)()
+    n = L.rc2dgi_plan_rows(ctypes.byref(cfg), float(blur_radius), rank, world, pass_id, buf, 32)
+    if n < 0:
+        raise RC2DGIError(n, "rc2dgi_plan_rows")
+    if n > 32:
+        buf = (ctypes.c_int * (2 * n))()
+        n = L.rc2dgi_plan_rows(ctypes.byref(cfg), float(blur_radius), rank, world, pass_id, buf, n)
+    return [(buf[2 * k], buf[2 * k + 1]) for k in range(n)]
+
+
+__all__ = ["RC2DGI", "RC2DGIError", "load_library", "abi_version", "RT", "PASS_NAMES", "shard_unique_id", "do_group",
+           "plan_rows", "PLAN_JFA", "PLAN_LEVEL", "PLAN_BLUR", "PLAN_MERGE"]

@@ -1,0 +1,125 @@
+"""GPU: row-strip sharding through the C ABI, bit-exact against the unsharded frame.
+
+In-process shards (``rc2dgi_do_group``: context k = shard k of n, distRT strips exchanged by
+device copies) on one GPU, with every intermediate render texture poisoned before the frame;
+each shard's colorRT / tempRT strip must equal the whole-frame result bit for bit.  The RCCL
+transport is exercised at world size 1 (communicator, grouped in-place broadcast); more ranks
+need more GPUs than a test box has.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_err  # noqa: F401  (shared helpers live there)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def R():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from radiancecascade2dglobalillumination_amd import rc2dgi
+
+    return rc2dgi
+
+
+def _scene(spec, W, H):
+    from radiancecascade2dglobalillumination_amd import scenes
+
+    if spec == "demo":
+        return scenes.demo(W, H)
+    return scenes.random_scene(W, H, int(spec.split(":")[1]))
+
+
+def _full(R, W, H, N, rr, rs, blur, color, emis):
+    ctx = R.RC2DGI(W, H, cascade_count=N, render_scale=rs, ray_range=rr)
+    ctx.set_shader_value("_BlurRadius", blur)
+    ctx.frame(color, emis)
+    ctx.sync()
+    out = {k: ctx.download(k) for k in ("color", "temp")}
+    ctx.close()
+    return out
+
+
+CASES = [
+    # W, H, N, rayRange, renderScale, blur, world, scene
+    (256, 256, 5, 3.0, 1.0, 1.5, 2, "demo"),      # fixed-tap blur + fused merge, integer JFA key
+    (512, 256, 4, 2.0, 1.0, 1.5, 3, "rand:21"),   # non-square power of two: float JFA key
+    (200, 120, 3, 2.0, 1.0, 2.5, 4, "rand:22"),   # non-power-of-two: float JFA taps, separate passes
+    (320, 256, 4, 8.0, 0.5, 1.37, 3, "rand:23"),  # cascades coarser than the screen
+    (128, 128, 3, 4.0, 1.0, 0.0, 5, "rand:24"),   # blur off
+    (1024, 1024, 6, 2.0, 1.0, 1.5, 8, "demo"),
+    (1200, 900, 6, 2.0, 1.0, 1.5, 8, "demo"),     # C1 size
+]
+
+
+@pytest.mark.parametrize("W,H,N,rr,rs,blur,world,scene", CASES)
+def test_group_shards_match_whole_frame(R, W, H, N, rr, rs, blur, world, scene):
+    color, emis = _scene(scene, W, H)
+    want = _full(R, W, H, N, rr, rs, blur, color, emis)
+    ctxs = []
+    for k in range(world):
+        c = R.RC2DGI(W, H, cascade_count=N, render_scale=rs, ray_range=rr)
+        c.set_shader_value("_BlurRadius", blur)
+        c.set_shard(k, world)
+        c.set_tuning("poison", 1)
+        c.upload("color", color)
+        c.upload("emissive", emis)
+        ctxs.append(c)
+    for _ in range(2):  # the second frame checks the cross-frame ordering of the exchange
+        R.do_group(ctxs)
+        for c in ctxs:
+            c.sync()
+        for c in ctxs:
+            y0, y1 = c.shard_rows()
+            for k in ("color", "temp"):
+                got = c.download(k)[y0:y1]
+                mism = np.count_nonzero(got != want[k][y0:y1])
+                assert mism == 0, f"shard {c.shard_rows()} {k}: {mism} values differ"
+    for c in ctxs:
+        c.close()
+
+
+def test_sharded_context_needs_an_exchange(R):
+    c = R.RC2DGI(64, 64, cascade_count=2)
+    c.set_shard(1, 2)
+    assert c.shard_rows() == (32, 64)
+    with pytest.raises(R.RC2DGIError) as e:
+        c.do_rc2dgi()
+    assert e.value.code == -6
+    with pytest.raises(R.RC2DGIError):
+        c.set_shard(2, 2)
+    c.close()
+
+
+def test_rccl_transport_single_rank(R):
+    """shard_connect + do_rc2dgi with a real RCCL communicator (world 1: the grouped in-place
+    broadcast runs on the context stream) -- same bits as a plain context."""
+    W = H = 256
+    color, emis = _scene("demo", W, H)
+    want = _full(R, W, H, 4, 2.0, 1.0, 1.5, color, emis)
+    c = R.RC2DGI(W, H, cascade_count=4, ray_range=2.0)
+    c.set_shard(0, 1)
+    c.connect(R.shard_unique_id())
+    c.frame(color, emis)
+    c.sync()
+    assert np.array_equal(c.download("color"), want["color"])
+    c.close()
+
+
+def test_phase_api_matches_do(R):
+    """do_phase(1) + do_phase(2) on an unsharded context is one DoRC2DGI()."""
+    W, H = 192, 128
+    color, emis = _scene("rand:25", W, H)
+    want = _full(R, W, H, 4, 2.0, 1.0, 1.5, color, emis)
+    c = R.RC2DGI(W, H, cascade_count=4, ray_range=2.0)
+    c.upload("color", color)
+    c.upload("emissive", emis)
+    c.do_phase(1)
+    ptr, pitch = c.device_buffer("dist")
+    assert ptr and pitch >= W * 2
+    c.do_phase(2)
+    c.sync()
+    assert np.array_equal(c.download("color"), want["color"])
+    c.close()
