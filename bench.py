@@ -164,6 +164,74 @@ def bench_batch(a, rank, local, world):
         g.close()
 
 
+def bench_strips(a, rank, local, world):
+    """SURVEY §8e / BASELINE configs[3]: ONE frame split into row strips, one shard per rank
+    (strong scaling).  Ranks exchange their distRT strips over RCCL inside librc2dgi
+    (rc2dgi_shard_connect).  With one process and --shards P > 1 the P shards run as
+    in-process contexts on the one GPU (rc2dgi_do_group): the rehearsal of the decomposition,
+    whose time is the sum of the shards' work (redundant halo rows included)."""
+    import numpy as np
+    import torch
+
+    from radiancecascade2dglobalillumination_amd import RC2DGI, scenes
+    from radiancecascade2dglobalillumination_amd import dist as rdist
+    from radiancecascade2dglobalillumination_amd import rc2dgi as R
+
+    W, H, N = a.size, a.height or a.size, a.cascades
+    color, emis = scenes.demo(W, H)  # the same scene on every rank: one frame
+    virtual = world == 1 and a.shards > 1
+    nsh = a.shards if virtual else world
+
+    def make(k):
+        g = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local)
+        g.set_shard(k, nsh)
+        g.upload("color", color)
+        g.upload("emissive", emis)
+        return g
+
+    if virtual:
+        ctxs = [make(k) for k in range(nsh)]
+        run = lambda: R.do_group(ctxs)  # noqa: E731
+    else:
+        g = make(rank)
+        uid = [R.shard_unique_id() if rank == 0 else None]
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.broadcast_object_list(uid, src=0)
+        g.connect(uid[0])
+        ctxs = [g]
+        run = g.do_rc2dgi
+    CW, CH = ctxs[0].cascade_resolution
+    for _ in range(a.warmup):
+        run()
+    for g in ctxs:
+        g.sync()
+    rdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        run()
+    for g in ctxs:
+        g.sync()
+    torch.cuda.synchronize()
+    rdist.barrier()
+    wall = rdist.max_over_ranks([time.perf_counter() - t0], device="cuda")[0]
+    units = CW * CH * N * a.steps  # one frame per step, whatever the shard count
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"Mpixel*cascades/s (whole DoRC2DGI frame, row strips) at {W}x{H}, cascadeCount={N}",
+            "value": round(units / wall / 1e6, 1), "unit": "Mpixel*cascades/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall * 1e3 / a.steps, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
+            "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}, row strips",
+                       "shards": nsh, "parallelism": f"strips{nsh}" + ("-in-process" if virtual else "-rccl")},
+            "frames_per_s": round(a.steps / wall, 2)}), flush=True)
+    for g in ctxs:
+        g.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -180,6 +248,10 @@ def main():
     ap.add_argument("--scene", default="demo", help="demo | random:<seed>")
     ap.add_argument("--batch", type=int, default=0,
                     help="scenes per GPU, one context + stream each (BASELINE configs[4] batch mode)")
+    ap.add_argument("--mode", default="replicas", choices=("replicas", "strips"),
+                    help="strips: one frame split into row strips over the ranks (BASELINE configs[3])")
+    ap.add_argument("--shards", type=int, default=1,
+                    help="strips on one process: run this many shards as in-process contexts")
     a = ap.parse_args()
 
     import numpy as np
@@ -191,6 +263,8 @@ def main():
     rank, local, world = rdist.init("nccl")
     if a.batch:
         return bench_batch(a, rank, local, world)
+    if a.mode == "strips":
+        return bench_strips(a, rank, local, world)
 
     W = a.size
     H = a.height or a.size
@@ -240,7 +314,8 @@ def main():
         if rec.get("config") == f"{W}x{H}_N{N}":
             traffic = rec.get("hbm_bytes_per_launch")
     line = {
-        "metric": "Mpixel*cascades/s (RC pass) at 4096^2, cascadeCount=6",
+        "metric": (f"Mpixel*cascades/s (RC pass) at {W}^2, cascadeCount={N}" if W == H else
+                   f"Mpixel*cascades/s (RC pass) at {W}x{H}, cascadeCount={N}"),
         "value": round(value, 1),
         "unit": "Mpixel*cascades/s",
         "n_gpus": world,
@@ -251,7 +326,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (reference demo scene painted at 4096^2, resident in HBM)",
+        "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
         "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}", "screen": [W, H],
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
                    "parallelism": f"replicas{world}"},
