@@ -184,9 +184,11 @@ def bench_strips(a, rank, local, world):
 
     def make(k):
         g = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local)
-        g.set_shard(k, nsh)
         g.upload("color", color)
         g.upload("emissive", emis)
+        if not a.no_autotune:
+            g.autotune(1)  # on the whole frame; the orders carry over to the shard
+        g.set_shard(k, nsh)
         return g
 
     if virtual:
@@ -250,6 +252,8 @@ def main():
                     help="scenes per GPU, one context + stream each (BASELINE configs[4] batch mode)")
     ap.add_argument("--mode", default="replicas", choices=("replicas", "strips"),
                     help="strips: one frame split into row strips over the ranks (BASELINE configs[3])")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="keep the default RC workgroup order (setup otherwise times the candidates per level)")
     ap.add_argument("--shards", type=int, default=1,
                     help="strips on one process: run this many shards as in-process contexts")
     a = ap.parse_args()
@@ -278,6 +282,7 @@ def main():
     # inputs resident in HBM before the timed region
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
+    orders = None if a.no_autotune else ctx.autotune(2)  # setup: schedule choice, results identical
     ctx.set_timing(True)
     if a.sweep_rc:
         sweep_rc(ctx, N, a.steps, rounds=3)
@@ -329,7 +334,8 @@ def main():
         "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
         "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}", "screen": [W, H],
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
-                   "parallelism": f"replicas{world}"},
+                   "parallelism": f"replicas{world}",
+                   "rc_order": orders or "default"},
         "rc_ms_per_frame": round(t_rc / a.steps, 4),
         "rc_level_ms": [round(x / a.steps, 4) for x in lvl_ms.tolist()],
         "full_pipeline_ms": round(t_tot / a.steps, 4),

@@ -142,10 +142,16 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *   "blur_path"       blur / copy-back / merge kernels: 0 auto (fixed-tap blur with merge fused
  *                     where the sizes allow), 1 LDS-tiled blur + copy-back, then merge,
  *                     2 separate blur, copy-back and merge passes
+ *   "rc_order_L<n>"   workgroup order of level n: px | py << 8 | dg << 16 = patches of px x py
+ *                     probe tiles x groups of dg direction blocks (0: tile-major, the default)
  *   "poison"          debug: fill the intermediate render textures with 0xFF bytes before each
  *                     frame (rows a sharded frame never computes then read as NaN)
  * rc2dgi_get_tuning also answers "rc_variant_count". */
 int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
+/* time `frames` frames per candidate workgroup order on the uploaded scene and keep the fastest
+ * per level (like a convolution library's benchmark mode; results are identical for every
+ * order).  Runs whole frames on the context stream; synchronous. */
+int rc2dgi_autotune(rc2dgi_ctx *ctx, int frames);
 int rc2dgi_get_tuning(rc2dgi_ctx *ctx, const char *key, int *value);
 
 /* ---- debug views beyond the reference's thumbnails: keep a copy of every cascade level G_L

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <utility>
 #include <string>
@@ -100,6 +101,7 @@ struct rc2dgi_ctx {
   hipEvent_t ev[P_COUNT + 1] = {};
   std::vector<hipEvent_t> ev_level;  // N + 1
   std::vector<int> rc_variant;  // per level tile shape (tuning)
+  std::vector<int> rc_order;    // per level workgroup order px | py << 8 | dg << 16 (tuning, 0 = tile-major)
   int blur_path = 0;             // tuning "blur_path"
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
@@ -184,6 +186,19 @@ int default_rc_variant(int level) {
   return 0;
 }
 
+inline int order_code(int px, int py, int dg) { return px | (py << 8) | (dg << 16); }
+
+// default workgroup order per level (scripts/sweep_rc_order.py, profiles/r01/rc_order_*.json):
+// from level 3 up, patches of 2 x 2 tiles x 8 direction blocks keep the distance-field
+// footprint of an XCD's resident workgroups closer to its L2; below, tile-major
+int default_rc_order(int level) { return level >= 3 ? order_code(2, 2, 8) : 0; }
+
+// rc2dgi_autotune candidates (px, py, dg); the library falls back to tile-major per level where
+// a candidate does not tile the grid
+const int kOrderCandidates[][3] = {{0, 0, 0},  {2, 2, 8},  {4, 4, 4},  {2, 4, 4},  {2, 8, 8},  {2, 16, 16},
+                                   {1, 16, 16}, {1, 16, 32}, {1, 32, 16}, {1, 4, 64}, {2, 8, 16}, {4, 8, 4},
+                                   {1, 8, 8},  {2, 2, 16}, {4, 2, 32}, {1, 4, 16}};
+
 // (re)allocate every render texture for the current W, H, N (RC2DGI.cs:79-98)
 int allocate(rc2dgi_ctx *c) {
   free_buffers(c);
@@ -220,6 +235,8 @@ int allocate(rc2dgi_ctx *c) {
   c->ev_level.resize(c->N + 1);
   c->rc_variant.resize(c->N, default_rc_variant(c->N - 1));
   for (int L = 0; L < c->N; ++L) c->rc_variant[L] = default_rc_variant(L);
+  c->rc_order.resize(c->N);
+  for (int L = 0; L < c->N; ++L) c->rc_order[L] = default_rc_order(L);
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
     for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, nc * sizeof(float4)));
@@ -560,6 +577,9 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.ray_range = c->ray_range;
     a.reflectivity = c->reflectivity;
     a.variant = c->rc_variant[L];
+    a.order_px = c->rc_order[L] & 0xFF;
+    a.order_py = (c->rc_order[L] >> 8) & 0xFF;
+    a.order_dg = c->rc_order[L] >> 16;
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
       a.p1 = r.second;
@@ -651,6 +671,41 @@ int rc2dgi_do_phase(rc2dgi_ctx *c, int phase) {
   if (phase != 1 && phase != 2) return fail(c, RC2DGI_E_ARG, "phase is 1 or 2");
   const FramePlan plan = make_plan(c);
   return phase == 1 ? do_phase1(c, plan) : do_phase2(c, plan);
+}
+
+int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
+  if (!c) return RC2DGI_E_ARG;
+  if (c->world > 1) return fail(c, RC2DGI_E_STATE, "autotune an unsharded context (the orders carry over)");
+  if (frames < 1) frames = 1;
+  const bool timing = c->timing;
+  c->timing = true;
+  const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
+  std::vector<float> best(c->N, 1e30f);
+  std::vector<int> pick(c->rc_order);
+  std::vector<float> lv(c->N);
+  for (int k = 0; k < nc; ++k) {
+    for (int L = 0; L < c->N; ++L)
+      c->rc_order[L] = order_code(kOrderCandidates[k][0], kOrderCandidates[k][1], kOrderCandidates[k][2]);
+    std::vector<float> acc(c->N, 1e30f);
+    for (int f = 0; f <= frames; ++f) {  // the first frame warms the caches for this order
+      int rc = rc2dgi_do(c);
+      if (rc == RC2DGI_OK) rc = rc2dgi_pass_times(c, nullptr, 0, lv.data(), c->N);
+      if (rc != RC2DGI_OK) {
+        c->timing = timing;
+        return rc;
+      }
+      if (f > 0)
+        for (int L = 0; L < c->N; ++L) acc[L] = std::min(acc[L], lv[L]);
+    }
+    for (int L = 0; L < c->N; ++L)
+      if (acc[L] < best[L]) {
+        best[L] = acc[L];
+        pick[L] = c->rc_order[L];
+      }
+  }
+  c->rc_order = pick;
+  c->timing = timing;
+  return RC2DGI_OK;
 }
 
 int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
@@ -881,6 +936,13 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->poison = value != 0;
     return RC2DGI_OK;
   }
+  if (k.rfind("rc_order_L", 0) == 0) {
+    const int L = std::atoi(k.c_str() + 10);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    if (value < 0) return fail(c, RC2DGI_E_ARG, "rc_order is px | py << 8 | dg << 16");
+    c->rc_order[L] = value;
+    return RC2DGI_OK;
+  }
   return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);
 }
 
@@ -903,6 +965,12 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "poison") {
     *value = c->poison ? 1 : 0;
+    return RC2DGI_OK;
+  }
+  if (k.rfind("rc_order_L", 0) == 0) {
+    const int L = std::atoi(k.c_str() + 10);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    *value = c->rc_order[L];
     return RC2DGI_OK;
   }
   return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);

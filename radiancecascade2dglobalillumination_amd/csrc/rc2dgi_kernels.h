@@ -56,6 +56,7 @@ struct RcLevelArgs {
   float ray_range, reflectivity;
   int variant;           // tile shape (rc_variant_name)
   int p0 = 0, p1 = -1;   // probe rows [p0, p1) of every direction block (-1 = all)
+  int order_px = 0, order_py = 0, order_dg = 0;  // workgroup order (0: tile-major, direction-minor)
 };
 
 int rc_variant_count();

@@ -233,6 +233,7 @@ struct RcParams {
   CascadeDims c;
   int level, bsc, bdx, bdy, tiles_x, tiles_per_block;
   int p0, p1;  // probe rows [p0, p1) of every direction block (row-strip shards; 0, bdy otherwise)
+  int opx, opy, odg;  // workgroup order: patches of opx x opy tiles x groups of odg direction blocks (odg 0: tile-major)
   float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
   float aspx, aspy, t0, t1, reflectivity;
 };
@@ -290,8 +291,35 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
 
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
   const int logical = xcd_logical_id((int)blockIdx.x, (int)gridDim.x);
-  const int tile = logical / ngrp;
-  const int bi0 = (logical - tile * ngrp) * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
+  int tile, dgi;
+  if (P.odg > 0) {
+    // for patch: for direction group: for tile in patch: for direction in group -- the workgroups
+    // an XCD runs together trace a few neighbouring tiles in a narrow fan of directions.  Patches
+    // of opx x opy tiles cover the tile grid row by row; the last patch row / column may be
+    // partial (w x h tiles), which keeps the map a bijection for any grid.
+    const int tiles_y = P.tiles_per_block / P.tiles_x;
+    const int prow = P.tiles_x * P.opy * ngrp;  // workgroups in a full patch row
+    const int pr = logical / prow;
+    int r = logical - pr * prow;
+    const int h = min(P.opy, tiles_y - pr * P.opy);
+    const int pfull = P.opx * h * ngrp;  // workgroups in a full-width patch of this row
+    int pc = r / pfull;
+    const int nfull = P.tiles_x / P.opx;
+    if (pc > nfull) pc = nfull;  // the partial last column
+    r -= pc * pfull;
+    const int w = min(P.opx, P.tiles_x - pc * P.opx);
+    const int pt = w * h;
+    const int g = r / (pt * P.odg);
+    r -= g * pt * P.odg;
+    const int tip = r / P.odg, di = r - tip * P.odg;
+    const int iy = tip / w, ix = tip - iy * w;
+    tile = (pr * P.opy + iy) * P.tiles_x + pc * P.opx + ix;
+    dgi = g * P.odg + di;
+  } else {
+    tile = logical / ngrp;
+    dgi = logical - tile * ngrp;
+  }
+  const int bi0 = dgi * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
   const int ty = tile / P.tiles_x, tx = tile - ty * P.tiles_x;
   const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
   const int cx = cx0 + (int)(threadIdx.x % TX);
@@ -828,8 +856,15 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
 template <int TX, int TY, int PY, int PD = 1, bool MASKED = false>
 static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
-  P.tiles_per_block = P.tiles_x * ceil_div(P.p1 - P.p0, TY * PY);
+  const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
+  P.tiles_per_block = P.tiles_x * tiles_y;
   const int nwg = P.tiles_per_block * P.bsc * P.bsc / PD;
+  // workgroup order (tuning "rc_order"): only when patches and groups tile the grid exactly
+  P.opx = a.order_px;
+  P.opy = a.order_py;
+  P.odg = a.order_dg;
+  const int ngrp = P.bsc * P.bsc / PD;
+  if (P.odg <= 0 || P.opx <= 0 || P.opy <= 0 || ngrp % P.odg) P.opx = P.opy = P.odg = 0;
   if (a.level == a.N - 1)
     hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, true, MASKED>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper,
                        a.out, a.dist, a.color, a.emissive, a.dirs, a.sky);

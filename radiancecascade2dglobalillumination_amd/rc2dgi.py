@@ -90,6 +90,7 @@ def load_library(path: Optional[str] = None):
         "rc2dgi_set_tuning": ([vp, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
         "rc2dgi_get_tuning": ([vp, ctypes.c_char_p, ip], ctypes.c_int),
         "rc2dgi_download_level": ([vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_autotune": ([vp, ctypes.c_int], ctypes.c_int),
         "rc2dgi_set_shard": ([vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "rc2dgi_shard_rows": ([vp, ip, ip], ctypes.c_int),
         "rc2dgi_shard_unique_id": ([vp, ctypes.c_int], ctypes.c_int),
@@ -275,6 +276,12 @@ class RC2DGI:
         v = ctypes.c_int()
         self._check(self._L.rc2dgi_get_tuning(self._h, key.encode(), ctypes.byref(v)), f"get_tuning {key}")
         return v.value
+
+    def autotune(self, frames: int = 2) -> list:
+        """Pick the fastest RC workgroup order per level on the uploaded scene (results are
+        identical for every order); returns the chosen per-level codes."""
+        self._check(self._L.rc2dgi_autotune(self._h, int(frames)), "autotune")
+        return [self.get_tuning(f"rc_order_L{L}") for L in range(self._N)]
 
     def set_keep_levels(self, enable: bool = True) -> None:
         """Debug: keep every cascade level G_L as stored by its pass."""

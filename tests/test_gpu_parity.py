@@ -372,3 +372,28 @@ def test_every_blur_path_matches_oracle(RC2DGI, W, H, rs, radius):
         got = {k: ctx.download(k) for k in ("color", "temp", "gi1", "gi2", "blur", "final_gi")}
         assert_parity(got, fr, list(got), exact=True, what=f"blur_path {path}")
     ctx.close()
+
+
+def test_rc_orders_and_autotune_are_bit_identical(RC2DGI):
+    """Workgroup orders (tuning rc_order_L<n>, autotune) change the schedule only."""
+    W, H, N = 512, 512, 6
+    color, emis = make_scene("demo", W, H)
+    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=2.0), color, emis, keep_levels=True)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0)
+    ctx.set_keep_levels(True)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    codes = [0, 2 | 2 << 8 | 8 << 16, 4 | 4 << 8 | 4 << 16, 1 | 16 << 8 | 16 << 16, 2 | 3 << 8 | 5 << 16]
+    for code in codes:  # the last does not tile any grid: tile-major fallback
+        for L in range(N):
+            ctx.set_tuning(f"rc_order_L{L}", code)
+        ctx.do_rc2dgi()
+        ctx.sync()
+        for L in range(N):
+            assert np.array_equal(ctx.download_level(L), fr.gi_levels[L]), f"order {code:#x} level {L}"
+    picked = ctx.autotune(1)
+    assert len(picked) == N
+    ctx.do_rc2dgi()
+    ctx.sync()
+    assert np.array_equal(ctx.download("color"), fr.color_out)
+    ctx.close()

@@ -94,3 +94,34 @@ def test_jfa_scaled_float_key_matches_shader_distance():
         dy = (sj - j).astype(f) * f(mx // H)
         got = (dx * dx + dy * dy) * f(1.0 / mx) * f(1.0 / mx)
         assert np.array_equal(got, want), (W, H)
+
+
+def _rc_order_map(logical, tiles_x, tiles_y, ngrp, opx, opy, odg):
+    """k_rc_level's workgroup order (rc_order): logical id -> (tile, direction group)."""
+    prow = tiles_x * opy * ngrp
+    pr = logical // prow
+    r = logical - pr * prow
+    h = min(opy, tiles_y - pr * opy)
+    pfull = opx * h * ngrp
+    pc = min(r // pfull, tiles_x // opx)
+    r -= pc * pfull
+    w = min(opx, tiles_x - pc * opx)
+    g = r // (w * h * odg)
+    r -= g * w * h * odg
+    tip, di = r // odg, r % odg
+    iy, ix = tip // w, tip % w
+    return (pr * opy + iy) * tiles_x + pc * opx + ix, g * odg + di
+
+
+def test_rc_workgroup_order_is_a_bijection():
+    """Every (tile, direction group) is visited exactly once for any grid, partial patches
+    included (row-strip shards give tile grids the patches do not divide)."""
+    import itertools
+
+    for tx, ty, ng, px, py, dg in itertools.product([1, 3, 5, 16], [1, 2, 5, 7, 16], [1, 4, 16], [1, 2, 3, 4, 16],
+                                                    [1, 2, 4, 5], [1, 2, 4, 16]):
+        if ng % dg:
+            continue
+        n = tx * ty * ng
+        seen = {_rc_order_map(q, tx, ty, ng, px, py, dg) for q in range(n)}
+        assert len(seen) == n and all(0 <= t < tx * ty and 0 <= d < ng for t, d in seen)
