@@ -111,7 +111,7 @@ def sweep_rc(ctx, N, steps, rounds=3):
 
 def lib_variant_name(v):
     names = ["16x16x1", "16x8x2", "16x16x2", "32x8x1", "64x4x1", "8x8x1", "32x8x2", "16x16x1d2", "16x16x1d4",
-             "16x8x1d2", "32x8x1d2", "16x8x1d4", "8x8x1d4"]
+             "16x8x1d2", "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u"]
     return names[v] if v < len(names) else str(v)
 
 
@@ -283,6 +283,7 @@ def main():
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
     orders = None if a.no_autotune else ctx.autotune(2)  # setup: schedule choice, results identical
+    variants = [ctx.get_tuning(f"rc_variant_L{L}") for L in range(N)]
     ctx.set_timing(True)
     if a.sweep_rc:
         sweep_rc(ctx, N, a.steps, rounds=3)
@@ -335,7 +336,7 @@ def main():
         "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}", "screen": [W, H],
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
                    "parallelism": f"replicas{world}",
-                   "rc_order": orders or "default"},
+                   "rc_order": orders or "default", "rc_variant": variants},
         "rc_ms_per_frame": round(t_rc / a.steps, 4),
         "rc_level_ms": [round(x / a.steps, 4) for x in lvl_ms.tolist()],
         "full_pipeline_ms": round(t_tot / a.steps, 4),

@@ -180,11 +180,9 @@ hipError_t alloc(T **p, size_t bytes) {
   return hipMalloc(reinterpret_cast<void **>(p), bytes);
 }
 
-// measured default tile shape per level (profiles/, bench.py --sweep-rc)
-int default_rc_variant(int level) {
-  (void)level;
-  return 0;
-}
+// measured default tile shape per level (profiles/, bench.py --sweep-rc): from level 3 up the
+// gather-bound levels prefer the fully unrolled march ("16x16x1u")
+int default_rc_variant(int level) { return level >= 3 ? 13 : 0; }
 
 inline int order_code(int px, int py, int dg) { return px | (py << 8) | (dg << 16); }
 
@@ -680,12 +678,16 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   const bool timing = c->timing;
   c->timing = true;
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
+  const int kVariants[] = {0, 13};  // march loop rolled / fully unrolled
   std::vector<float> best(c->N, 1e30f);
-  std::vector<int> pick(c->rc_order);
+  std::vector<int> pick(c->rc_order), pickv(c->rc_variant);
   std::vector<float> lv(c->N);
-  for (int k = 0; k < nc; ++k) {
-    for (int L = 0; L < c->N; ++L)
-      c->rc_order[L] = order_code(kOrderCandidates[k][0], kOrderCandidates[k][1], kOrderCandidates[k][2]);
+  for (int k = 0; k < 2 * nc; ++k) {
+    const int v = kVariants[k / nc], o = k % nc;
+    for (int L = 0; L < c->N; ++L) {
+      c->rc_order[L] = order_code(kOrderCandidates[o][0], kOrderCandidates[o][1], kOrderCandidates[o][2]);
+      c->rc_variant[L] = v;
+    }
     std::vector<float> acc(c->N, 1e30f);
     for (int f = 0; f <= frames; ++f) {  // the first frame warms the caches for this order
       int rc = rc2dgi_do(c);
@@ -701,9 +703,11 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
       if (acc[L] < best[L]) {
         best[L] = acc[L];
         pick[L] = c->rc_order[L];
+        pickv[L] = c->rc_variant[L];
       }
   }
   c->rc_order = pick;
+  c->rc_variant = pickv;
   c->timing = timing;
   return RC2DGI_OK;
 }

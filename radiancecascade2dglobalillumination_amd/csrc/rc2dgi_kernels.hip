@@ -236,6 +236,7 @@ struct RcParams {
   int opx, opy, odg;  // workgroup order: patches of opx x opy tiles x groups of odg direction blocks (odg 0: tile-major)
   float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
   float aspx, aspy, t0, t1, reflectivity;
+  float sWf, sHf;  // screen size as floats (power-of-two screen path)
 };
 
 // q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
@@ -274,7 +275,19 @@ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
 // The level-(L+1) bilinear footprint of the tile -- block-local by the reference's clamp -- is
 // staged in LDS once per ray direction; its loads are issued before the march and written to
 // LDS after it (their latency hides under the march).
-template <int TX, int TY, int PY, int PD, bool TOP, bool MASKED>
+// floor(x) as an int in one instruction (x finite, within int range)
+__device__ __forceinline__ int cvt_floor(float x) {
+  int r;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// P2S: power-of-two screen and cascade sizes.  NEAREST + REPEAT of a position in [0, 1] is then
+// floor(p * n) & (n - 1) exactly, and the march's screen test is one unsigned compare per axis
+// (p is never NaN, and never -0: the origin term is > 0, and x + (-x) rounds to +0).
+// UNR: unroll factor of the march loop.  Fully unrolled (32) suits the gather-bound high levels;
+// rolled (1) the VALU-bound low levels (no SGPR spills, occupancy 8).
+template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR>
 __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *__restrict__ upper,
                                                      float4 *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
@@ -383,7 +396,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
 #ifndef RC2DGI_DIAG_MAX_ITERS
 #define RC2DGI_DIAG_MAX_ITERS 32  // RadianceCascades.fs:64 (diagnostic builds may cap it; never shipped)
 #endif
-#pragma unroll
+#pragma unroll UNR
   for (int it = 0; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
     int idx[NR];
     bool live[NR];
@@ -393,22 +406,24 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       const int r = k % ND, p = k / ND;
       const float px = ox + (t[k] * rdx[r]) * P.aspy;
       const float py = oy[p] + (t[k] * rdy[r]) * P.aspx;
-      live[k] = act[k] && !(t[k] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+      if constexpr (P2S) {
+        live[k] = act[k] && !(t[k] > P.t1) && __float_as_uint(px) <= 0x3f800000u &&
+                  __float_as_uint(py) <= 0x3f800000u;
+        const int ix = cvt_floor(px * P.sWf) & (P.s.W - 1), iy = cvt_floor(py * P.sHf) & (P.s.H - 1);
+        idx[k] = live[k] ? (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix : 0;  // < 2^24 operands
+      } else {
+        live[k] = act[k] && !(t[k] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+        idx[k] = live[k] ? wrap_nearest(py, say) * P.s.pitch + wrap_nearest(px, sax) : 0;
+      }
       act[k] = live[k];
       any_live |= live[k];
-      idx[k] = live[k] ? wrap_nearest(py, say) * P.s.pitch + wrap_nearest(px, sax) : 0;
     }
     if (!any_live) break;  // every ray left its interval or the screen: no more samples
     unsigned q[NR];
 #pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      if (MASKED) {
-        q[k] = 0xFFFFu;  // dead rays issue no load (exec-masked lanes generate no requests)
-        if (live[k]) q[k] = dist[idx[k]];
-      } else {
-        q[k] = dist[idx[k]];  // dead rays re-read texel 0 (one cached line)
-      }
-    }
+    for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
+      q[k] = *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) +
+                                                       ((unsigned)idx[k] << 1));
     bool any = false;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {  // branch-free: selects, no exec-mask juggling
@@ -432,7 +447,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   }
 
   // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
-  const bool pow2c = P.c.powW && P.c.powH;
+  const bool pow2c = P2S || (P.c.powW && P.c.powH);  // P2S implies power-of-two cascades
 #pragma unroll
   for (int p = 0; p < PY; ++p) {
     if (!pok[p]) continue;
@@ -483,7 +498,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
               t10 = sr[ly0 * RW + lx0 + 1];
               t01 = sr[(ly0 + 1) * RW + lx0];
               t11 = sr[(ly0 + 1) * RW + lx0 + 1];
-            } else {
+            } else if constexpr (!P2S) {
               // general GL path (mod(float(angleIndex), 2b), floor(float(angleIndex)/2b) are exact integers)
               const float offx = (float)(ai & umask), offy = (float)(ai >> ushift);
               const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
@@ -853,7 +868,7 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   return hipGetLastError();
 }
 
-template <int TX, int TY, int PY, int PD = 1, bool MASKED = false>
+template <int TX, int TY, int PY, int PD = 1, int UNR = 1>
 static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
   const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
@@ -865,19 +880,27 @@ static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.odg = a.order_dg;
   const int ngrp = P.bsc * P.bsc / PD;
   if (P.odg <= 0 || P.opx <= 0 || P.opy <= 0 || ngrp % P.odg) P.opx = P.opy = P.odg = 0;
-  if (a.level == a.N - 1)
-    hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, true, MASKED>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper,
-                       a.out, a.dist, a.color, a.emissive, a.dirs, a.sky);
-  else
-    hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, false, MASKED>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper,
-                       a.out, a.dist, a.color, a.emissive, a.dirs, a.sky);
+  P.sWf = (float)P.s.W;
+  P.sHf = (float)P.s.H;
+#define RC2DGI_RC(TOPV, P2V)                                                                                      \
+  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out, \
+                     a.dist, a.color, a.emissive, a.dirs, a.sky)
+  const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
+  const bool top = a.level == a.N - 1;
+  if (top) {
+    if (p2s) RC2DGI_RC(true, true); else RC2DGI_RC(true, false);
+  } else {
+    if (p2s) RC2DGI_RC(false, true); else RC2DGI_RC(false, false);
+  }
+#undef RC2DGI_RC
 }
 
 // RC tile variants (tuning knob "rc_variant"): TXxTYxPY probes per workgroup, "dD" = D direction
 // blocks per workgroup (needs 4^level >= D; falls back to d1 below that)
+// ("u": march loop fully unrolled)
 static const char *kRcVariantNames[] = {"16x16x1", "16x8x2",   "16x16x2",  "32x8x1",   "64x4x1",
                                         "8x8x1",   "32x8x2",   "16x16x1d2", "16x16x1d4", "16x8x1d2",
-                                        "32x8x1d2", "16x8x1d4", "8x8x1d4"};
+                                        "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u"};
 int rc_variant_count() { return (int)(sizeof(kRcVariantNames) / sizeof(kRcVariantNames[0])); }
 const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
@@ -922,6 +945,7 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
     case 10: nblk >= 2 ? launch_rc_tiles<32, 8, 1, 2>(a, P, st) : launch_rc_tiles<32, 8, 1>(a, P, st); break;
     case 11: nblk >= 4 ? launch_rc_tiles<16, 8, 1, 4>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
     case 12: nblk >= 4 ? launch_rc_tiles<8, 8, 1, 4>(a, P, st) : launch_rc_tiles<8, 8, 1>(a, P, st); break;
+    case 13: launch_rc_tiles<16, 16, 1, 1, 32>(a, P, st); break;
     default: launch_rc_tiles<16, 16, 1>(a, P, st); break;
   }
   return hipGetLastError();

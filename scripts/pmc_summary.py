@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--levels", type=int, default=6)
     ap.add_argument("--json")
     ap.add_argument("--config", default="4096x4096_N6")
+    ap.add_argument("--all", action="store_true", help="print every collected counter")
     a = ap.parse_args()
     rows = load(a.dir)
     # per (file, dispatch): counters
@@ -74,8 +75,10 @@ def main():
         if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
             h, m = avg["TCC_HIT_sum"], avg["TCC_MISS_sum"]
             s += f"  L2hit {h / max(h + m, 1):.3f} (req {(h + m) / 1e6:.1f}M)"
-        for c in ("SQ_WAVES", "SQ_INSTS_VMEM", "SQ_WAIT_INST_ANY", "SQ_BUSY_CYCLES", "TA_BUSY_avr",
-                  "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum"):
+        shown = ("SQ_WAVES", "SQ_INSTS_VMEM", "SQ_WAIT_INST_ANY", "SQ_BUSY_CYCLES", "TA_BUSY_avr",
+                 "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum")
+        for c in (sorted(k for k in avg if not k.startswith("_") and k not in ("FETCH_SIZE", "WRITE_SIZE"))
+                  if a.all else shown):
             if c in avg:
                 s += f"  {c} {avg[c]:.3g}"
         print(s)
