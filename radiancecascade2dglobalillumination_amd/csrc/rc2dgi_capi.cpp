@@ -107,6 +107,7 @@ struct rc2dgi_ctx {
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
   // row-strip sharding
+  RcMapCache rc_maps;  // host-built k_rc_level workgroup maps
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
   hipEvent_t ev_phase1 = nullptr;   // end of phase 1 (group exchange)
@@ -162,6 +163,7 @@ void free_level_bufs(rc2dgi_ctx *c) {
 
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
+  c->rc_maps.clear();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare};
   for (void *p : bufs)
@@ -578,6 +580,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.order_px = c->rc_order[L] & 0xFF;
     a.order_py = (c->rc_order[L] >> 8) & 0xFF;
     a.order_dg = c->rc_order[L] >> 16;
+    a.map_cache = &c->rc_maps;
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
       a.p1 = r.second;

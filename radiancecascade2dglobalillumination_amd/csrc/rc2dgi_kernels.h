@@ -1,5 +1,7 @@
 // rc2dgi_kernels.h -- host-side launchers for the DoRC2DGI() pass kernels (gfx950).
 #pragma once
+
+#include <vector>
 #include <hip/hip_runtime.h>
 
 namespace rc2dgi {
@@ -44,6 +46,17 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
 // row-strip planner
 bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp);
 
+// device copies of the host-built workgroup maps of k_rc_level, one per launch geometry
+struct RcMapCache {
+  struct Entry {
+    int nwg, tiles_x, tiles_y, ngrp, opx, opy, odg;
+    uint2 *dev;
+  };
+  std::vector<Entry> entries;
+  void clear();
+  ~RcMapCache();
+};
+
 struct RcLevelArgs {
   const float4 *upper;   // G_{L+1} (nullptr at the top level)
   float4 *out;           // G_L
@@ -57,6 +70,7 @@ struct RcLevelArgs {
   int variant;           // tile shape (rc_variant_name)
   int p0 = 0, p1 = -1;   // probe rows [p0, p1) of every direction block (-1 = all)
   int order_px = 0, order_py = 0, order_dg = 0;  // workgroup order (0: tile-major, direction-minor)
+  RcMapCache *map_cache = nullptr;  // where the launch finds / builds its workgroup map
 };
 
 int rc_variant_count();

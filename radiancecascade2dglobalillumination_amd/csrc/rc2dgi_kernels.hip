@@ -22,6 +22,8 @@
 #include "rc2dgi_device.h"
 #include "rc2dgi_kernels.h"
 
+#include <vector>
+
 namespace rc2dgi {
 
 static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
@@ -237,6 +239,7 @@ struct RcParams {
   float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
   float aspx, aspy, t0, t1, reflectivity;
   float sWf, sHf;  // screen size as floats (power-of-two screen path)
+  const uint2 *wg_map;  // workgroup -> (tile, direction group), host-built (XCD remap + order); may be null
 };
 
 // q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
@@ -261,9 +264,40 @@ __device__ __forceinline__ float div_res(float a, float n, float inv_n, int pow2
 // together trace ALL directions of neighbouring probe tiles, so their distance-field
 // samples stay in a ring around those tiles (L2-resident) instead of sweeping the whole
 // field once per direction.
-__device__ __forceinline__ int xcd_logical_id(int p, int n) {
+__host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
   const int q = n >> 3, r = n & 7, x = p & 7;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (p >> 3);
+}
+
+// logical workgroup -> (tile, direction group).  odg == 0: tile-major, direction-minor.
+// Otherwise for patch: for direction group: for tile in patch: for direction in group -- the
+// workgroups an XCD runs together trace a few neighbouring tiles in a narrow fan of directions.
+// Patches of opx x opy tiles cover the tile grid row by row; the last patch row / column may be
+// partial (w x h tiles), which keeps the map a bijection for any grid.
+__host__ __device__ __forceinline__ void rc_order_map(int logical, int tiles_x, int tiles_y, int ngrp, int opx,
+                                                      int opy, int odg, int &tile, int &dgi) {
+  if (odg <= 0) {
+    tile = logical / ngrp;
+    dgi = logical - tile * ngrp;
+    return;
+  }
+  const int prow = tiles_x * opy * ngrp;  // workgroups in a full patch row
+  const int pr = logical / prow;
+  int r = logical - pr * prow;
+  const int h = min(opy, tiles_y - pr * opy);
+  const int pfull = opx * h * ngrp;  // workgroups in a full-width patch of this row
+  int pc = r / pfull;
+  const int nfull = tiles_x / opx;
+  if (pc > nfull) pc = nfull;  // the partial last column
+  r -= pc * pfull;
+  const int w = min(opx, tiles_x - pc * opx);
+  const int pt = w * h;
+  const int g = r / (pt * odg);
+  r -= g * pt * odg;
+  const int tip = r / odg, di = r - tip * odg;
+  const int iy = tip / w, ix = tip - iy * w;
+  tile = (pr * opy + iy) * tiles_x + pc * opx + ix;
+  dgi = g * odg + di;
 }
 
 // One workgroup = one TX x (TY*PY) tile of probes (coordsInBlock) and PD consecutive direction
@@ -275,6 +309,12 @@ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
 // The level-(L+1) bilinear footprint of the tile -- block-local by the reference's clamp -- is
 // staged in LDS once per ray direction; its loads are issued before the march and written to
 // LDS after it (their latency hides under the march).
+#ifdef RC2DGI_DIAG_STATS
+// diagnostic builds only (python _build.py stats): per level, [0] lockstep ray slots executed
+// (iterations x rays per lane), [1] samples of live rays, [2] waves
+__device__ unsigned long long g_rc_stats[16][3];
+#endif
+
 // floor(x) as an int in one instruction (x finite, within int range)
 __device__ __forceinline__ int cvt_floor(float x) {
   int r;
@@ -303,37 +343,20 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   __shared__ float4 s_up[TOP ? 1 : NSTAGE];
 
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
-  const int logical = xcd_logical_id((int)blockIdx.x, (int)gridDim.x);
-  int tile, dgi;
-  if (P.odg > 0) {
-    // for patch: for direction group: for tile in patch: for direction in group -- the workgroups
-    // an XCD runs together trace a few neighbouring tiles in a narrow fan of directions.  Patches
-    // of opx x opy tiles cover the tile grid row by row; the last patch row / column may be
-    // partial (w x h tiles), which keeps the map a bijection for any grid.
-    const int tiles_y = P.tiles_per_block / P.tiles_x;
-    const int prow = P.tiles_x * P.opy * ngrp;  // workgroups in a full patch row
-    const int pr = logical / prow;
-    int r = logical - pr * prow;
-    const int h = min(P.opy, tiles_y - pr * P.opy);
-    const int pfull = P.opx * h * ngrp;  // workgroups in a full-width patch of this row
-    int pc = r / pfull;
-    const int nfull = P.tiles_x / P.opx;
-    if (pc > nfull) pc = nfull;  // the partial last column
-    r -= pc * pfull;
-    const int w = min(P.opx, P.tiles_x - pc * P.opx);
-    const int pt = w * h;
-    const int g = r / (pt * P.odg);
-    r -= g * pt * P.odg;
-    const int tip = r / P.odg, di = r - tip * P.odg;
-    const int iy = tip / w, ix = tip - iy * w;
-    tile = (pr * P.opy + iy) * P.tiles_x + pc * P.opx + ix;
-    dgi = g * P.odg + di;
+  int tx, ty, dgi;
+  if (P.wg_map) {  // one scalar load: the XCD remap + order below, precomputed on the host
+    const uint2 m = P.wg_map[blockIdx.x];
+    tx = (int)(m.x & 0xFFFFu);
+    ty = (int)(m.x >> 16);
+    dgi = (int)m.y;
   } else {
-    tile = logical / ngrp;
-    dgi = logical - tile * ngrp;
+    int tile;
+    rc_order_map(xcd_logical_id((int)blockIdx.x, (int)gridDim.x), P.tiles_x, P.tiles_per_block / P.tiles_x, ngrp,
+                 P.opx, P.opy, P.odg, tile, dgi);
+    ty = tile / P.tiles_x;
+    tx = tile - ty * P.tiles_x;
   }
   const int bi0 = dgi * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
-  const int ty = tile / P.tiles_x, tx = tile - ty * P.tiles_x;
   const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
   const int cx = cx0 + (int)(threadIdx.x % TX);
   const int cyb = cy0 + (int)(threadIdx.x / TX);
@@ -365,14 +388,14 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   }
 
   const float cxf = (float)cx;
-  const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P.c.powW);  // rayOrigin / _CascadeResolution
+  const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);  // rayOrigin / _CascadeResolution
   float oy[PY];
   bool pok[PY];
 #pragma unroll
   for (int p = 0; p < PY; ++p) {
     const int cy = cyb + p * TY;
     pok[p] = xok && cy < P.p1;
-    oy[p] = div_res(((float)cy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P.c.powH);
+    oy[p] = div_res(((float)cy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P2S || P.c.powH);
   }
   const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
 
@@ -395,6 +418,9 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   }
 #ifndef RC2DGI_DIAG_MAX_ITERS
 #define RC2DGI_DIAG_MAX_ITERS 32  // RadianceCascades.fs:64 (diagnostic builds may cap it; never shipped)
+#endif
+#ifdef RC2DGI_DIAG_STATS
+  unsigned diag_slots = 0, diag_samples = 0;
 #endif
 #pragma unroll UNR
   for (int it = 0; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
@@ -419,6 +445,10 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       any_live |= live[k];
     }
     if (!any_live) break;  // every ray left its interval or the screen: no more samples
+#ifdef RC2DGI_DIAG_STATS
+    diag_slots += NR;
+    for (int k = 0; k < NR; ++k) diag_samples += live[k] ? 1u : 0u;
+#endif
     unsigned q[NR];
 #pragma unroll
     for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
@@ -436,6 +466,13 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
     }
     if (!any) break;
   }
+#ifdef RC2DGI_DIAG_STATS
+  if (pok[0] || true) {
+    atomicAdd(&g_rc_stats[P.level][0], (unsigned long long)diag_slots);
+    atomicAdd(&g_rc_stats[P.level][1], (unsigned long long)diag_samples);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_rc_stats[P.level][2], 1ull);
+  }
+#endif
 
   if (!TOP) {
 #pragma unroll
@@ -868,6 +905,39 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   return hipGetLastError();
 }
 
+RcMapCache::~RcMapCache() { clear(); }
+
+void RcMapCache::clear() {
+  for (auto &e : entries)
+    if (e.dev) (void)hipFree(e.dev);
+  entries.clear();
+}
+
+// the host-built workgroup map for one launch geometry (built once, then reused)
+static const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int ngrp, int opx, int opy,
+                              int odg) {
+  if (!cache) return nullptr;
+  for (auto &e : cache->entries)
+    if (e.nwg == nwg && e.tiles_x == tiles_x && e.tiles_y == tiles_y && e.ngrp == ngrp && e.opx == opx &&
+        e.opy == opy && e.odg == odg)
+      return e.dev;
+  std::vector<uint2> m(nwg);
+  for (int p = 0; p < nwg; ++p) {
+    int tile, dgi;
+    rc_order_map(xcd_logical_id(p, nwg), tiles_x, tiles_y, ngrp, opx, opy, odg, tile, dgi);
+    const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    m[p] = make_uint2((unsigned)tx | ((unsigned)ty << 16), (unsigned)dgi);
+  }
+  RcMapCache::Entry e{nwg, tiles_x, tiles_y, ngrp, opx, opy, odg, nullptr};
+  if (hipMalloc(reinterpret_cast<void **>(&e.dev), (size_t)nwg * sizeof(uint2)) != hipSuccess) return nullptr;
+  if (hipMemcpy(e.dev, m.data(), (size_t)nwg * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(e.dev);
+    return nullptr;
+  }
+  cache->entries.push_back(e);
+  return e.dev;
+}
+
 template <int TX, int TY, int PY, int PD = 1, int UNR = 1>
 static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
@@ -880,6 +950,10 @@ static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.odg = a.order_dg;
   const int ngrp = P.bsc * P.bsc / PD;
   if (P.odg <= 0 || P.opx <= 0 || P.opy <= 0 || ngrp % P.odg) P.opx = P.opy = P.odg = 0;
+  // tile coordinates must fit the map's 16-bit fields
+  P.wg_map = (P.tiles_x < 65536 && tiles_y < 65536)
+                 ? rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, P.opx, P.opy, P.odg)
+                 : nullptr;
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
 #define RC2DGI_RC(TOPV, P2V)                                                                                      \
@@ -1041,3 +1115,15 @@ hipError_t launch_unorm8_to_f32(const unsigned char *src, int src_pitch_bytes, f
 }
 
 }  // namespace rc2dgi
+
+#ifdef RC2DGI_DIAG_STATS
+extern "C" int rc2dgi_diag_stats(unsigned long long *out, int reset) {
+  hipDeviceSynchronize();
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rc2dgi::g_rc_stats), sizeof(rc2dgi::g_rc_stats)) != hipSuccess) return -3;
+  if (reset) {
+    static unsigned long long zero[16][3] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rc2dgi::g_rc_stats), zero, sizeof(zero)) != hipSuccess) return -3;
+  }
+  return 0;
+}
+#endif

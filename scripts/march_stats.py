@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Lockstep efficiency of the RC march per level (diagnostic build librc2dgi_stats.so):
+samples of live rays / ray slots the lockstep loop executed.  Prints one JSON line."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["RC2DGI_LIB"] = os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "librc2dgi_stats.so")
+
+
+def main():
+    import numpy as np
+
+    from radiancecascade2dglobalillumination_amd import RC2DGI, scenes
+    from radiancecascade2dglobalillumination_amd.rc2dgi import load_library
+
+    W = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    rr = float(sys.argv[3]) if len(sys.argv) > 3 else 2.0
+    L = load_library()
+    L.rc2dgi_diag_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ctx = RC2DGI(W, W, cascade_count=N, ray_range=rr)
+    c, e = scenes.demo(W, W)
+    ctx.upload("color", c)
+    ctx.upload("emissive", e)
+    buf = np.zeros((16, 3), np.uint64)
+    ctx.do_rc2dgi()
+    ctx.sync()
+    L.rc2dgi_diag_stats(buf.ctypes.data, 1)
+    ctx.do_rc2dgi()
+    ctx.sync()
+    L.rc2dgi_diag_stats(buf.ctypes.data, 1)
+    out = {}
+    for lv in range(N):
+        slots, samples, waves = (int(x) for x in buf[lv])
+        rays = 4 * W * W
+        out[f"L{lv}"] = {"samples_per_ray": round(samples / rays, 3), "slot_iters_per_ray": round(slots / rays, 3),
+                         "lockstep_efficiency": round(samples / max(slots, 1), 3),
+                         "wave_iterations": round(slots / max(waves * 64 * 4, 1), 2)}
+    print(json.dumps({"size": W, "N": N, "ray_range": rr, "levels": out}))
+
+
+if __name__ == "__main__":
+    main()
