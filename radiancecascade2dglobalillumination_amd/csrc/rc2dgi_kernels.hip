@@ -239,7 +239,7 @@ struct RcParams {
   float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
   float aspx, aspy, t0, t1, reflectivity;
   float sWf, sHf;  // screen size as floats (power-of-two screen path)
-  const uint2 *wg_map;  // workgroup -> (tile, direction group), host-built (XCD remap + order); may be null
+  const uint2 *wg_map;  // workgroup -> (tile x | y << 16, direction group), host-built (XCD remap + order)
 };
 
 // q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
@@ -343,19 +343,10 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   __shared__ float4 s_up[TOP ? 1 : NSTAGE];
 
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
-  int tx, ty, dgi;
-  if (P.wg_map) {  // one scalar load: the XCD remap + order below, precomputed on the host
-    const uint2 m = P.wg_map[blockIdx.x];
-    tx = (int)(m.x & 0xFFFFu);
-    ty = (int)(m.x >> 16);
-    dgi = (int)m.y;
-  } else {
-    int tile;
-    rc_order_map(xcd_logical_id((int)blockIdx.x, (int)gridDim.x), P.tiles_x, P.tiles_per_block / P.tiles_x, ngrp,
-                 P.opx, P.opy, P.odg, tile, dgi);
-    ty = tile / P.tiles_x;
-    tx = tile - ty * P.tiles_x;
-  }
+  // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
+  const uint2 wgm = P.wg_map[blockIdx.x];
+  const int tx = (int)(wgm.x & 0xFFFFu), ty = (int)(wgm.x >> 16), dgi = (int)wgm.y;
+  (void)ngrp;
   const int bi0 = dgi * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
   const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
   const int cx = cx0 + (int)(threadIdx.x % TX);
@@ -939,7 +930,7 @@ static const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles
 }
 
 template <int TX, int TY, int PY, int PD = 1, int UNR = 1>
-static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
+static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
   const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
   P.tiles_per_block = P.tiles_x * tiles_y;
@@ -950,10 +941,9 @@ static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.odg = a.order_dg;
   const int ngrp = P.bsc * P.bsc / PD;
   if (P.odg <= 0 || P.opx <= 0 || P.opy <= 0 || ngrp % P.odg) P.opx = P.opy = P.odg = 0;
-  // tile coordinates must fit the map's 16-bit fields
-  P.wg_map = (P.tiles_x < 65536 && tiles_y < 65536)
-                 ? rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, P.opx, P.opy, P.odg)
-                 : nullptr;
+  // tile coordinates fit the map's 16-bit fields (<= 32768 probes per axis)
+  P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, P.opx, P.opy, P.odg);
+  if (!P.wg_map) return hipErrorOutOfMemory;
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
 #define RC2DGI_RC(TOPV, P2V)                                                                                      \
@@ -967,6 +957,7 @@ static void launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
     if (p2s) RC2DGI_RC(false, true); else RC2DGI_RC(false, false);
   }
 #undef RC2DGI_RC
+  return hipGetLastError();
 }
 
 // RC tile variants (tuning knob "rc_variant"): TXxTYxPY probes per workgroup, "dD" = D direction
@@ -1006,22 +997,24 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
   const int nblk = P.bsc * P.bsc;
+  hipError_t e = hipSuccess;
   switch (a.variant) {
-    case 1: launch_rc_tiles<16, 8, 2>(a, P, st); break;
-    case 2: launch_rc_tiles<16, 16, 2>(a, P, st); break;
-    case 3: launch_rc_tiles<32, 8, 1>(a, P, st); break;
-    case 4: launch_rc_tiles<64, 4, 1>(a, P, st); break;
-    case 5: launch_rc_tiles<8, 8, 1>(a, P, st); break;
-    case 6: launch_rc_tiles<32, 8, 2>(a, P, st); break;
-    case 7: nblk >= 2 ? launch_rc_tiles<16, 16, 1, 2>(a, P, st) : launch_rc_tiles<16, 16, 1>(a, P, st); break;
-    case 8: nblk >= 4 ? launch_rc_tiles<16, 16, 1, 4>(a, P, st) : launch_rc_tiles<16, 16, 1>(a, P, st); break;
-    case 9: nblk >= 2 ? launch_rc_tiles<16, 8, 1, 2>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
-    case 10: nblk >= 2 ? launch_rc_tiles<32, 8, 1, 2>(a, P, st) : launch_rc_tiles<32, 8, 1>(a, P, st); break;
-    case 11: nblk >= 4 ? launch_rc_tiles<16, 8, 1, 4>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
-    case 12: nblk >= 4 ? launch_rc_tiles<8, 8, 1, 4>(a, P, st) : launch_rc_tiles<8, 8, 1>(a, P, st); break;
-    case 13: launch_rc_tiles<16, 16, 1, 1, 32>(a, P, st); break;
-    default: launch_rc_tiles<16, 16, 1>(a, P, st); break;
+    case 1: e = launch_rc_tiles<16, 8, 2>(a, P, st); break;
+    case 2: e = launch_rc_tiles<16, 16, 2>(a, P, st); break;
+    case 3: e = launch_rc_tiles<32, 8, 1>(a, P, st); break;
+    case 4: e = launch_rc_tiles<64, 4, 1>(a, P, st); break;
+    case 5: e = launch_rc_tiles<8, 8, 1>(a, P, st); break;
+    case 6: e = launch_rc_tiles<32, 8, 2>(a, P, st); break;
+    case 7: e = nblk >= 2 ? launch_rc_tiles<16, 16, 1, 2>(a, P, st) : launch_rc_tiles<16, 16, 1>(a, P, st); break;
+    case 8: e = nblk >= 4 ? launch_rc_tiles<16, 16, 1, 4>(a, P, st) : launch_rc_tiles<16, 16, 1>(a, P, st); break;
+    case 9: e = nblk >= 2 ? launch_rc_tiles<16, 8, 1, 2>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
+    case 10: e = nblk >= 2 ? launch_rc_tiles<32, 8, 1, 2>(a, P, st) : launch_rc_tiles<32, 8, 1>(a, P, st); break;
+    case 11: e = nblk >= 4 ? launch_rc_tiles<16, 8, 1, 4>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
+    case 12: e = nblk >= 4 ? launch_rc_tiles<8, 8, 1, 4>(a, P, st) : launch_rc_tiles<8, 8, 1>(a, P, st); break;
+    case 13: e = launch_rc_tiles<16, 16, 1, 1, 32>(a, P, st); break;
+    default: e = launch_rc_tiles<16, 16, 1>(a, P, st); break;
   }
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
