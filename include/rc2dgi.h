@@ -148,7 +148,7 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     frame (rows a sharded frame never computes then read as NaN)
  * rc2dgi_get_tuning also answers "rc_variant_count". */
 int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
-/* time `frames` frames per candidate workgroup order x march unrolling ("rc_variant" 0 / 13) on
+/* time `frames` frames per candidate workgroup order x march variant ("rc_variant" 0 / 13 / 14 / 15) on
  * the uploaded scene and keep the fastest per level (like a convolution library's benchmark mode; results are identical for every
  * order).  Runs whole frames on the context stream; synchronous. */
 int rc2dgi_autotune(rc2dgi_ctx *ctx, int frames);

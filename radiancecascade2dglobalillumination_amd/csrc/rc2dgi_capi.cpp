@@ -86,6 +86,7 @@ struct rc2dgi_ctx {
   unsigned *occ = nullptr;                      // ScreenUV occupancy mask
   int mpitch = 0;                               // mask row pitch (words)
   unsigned short *dist = nullptr;  // packUNorm16 q
+  unsigned short *dist_t = nullptr;  // 8x8-tiled copy for the "t" RC variants
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
@@ -165,13 +166,13 @@ void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
   c->rc_maps.clear();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
-                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare};
+                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   c->color_in = c->emissive = c->temp = c->color_out = nullptr;
   c->jump1 = c->jump2 = nullptr;
   c->occ = nullptr;
-  c->dist = nullptr;
+  c->dist = c->dist_t = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
   c->sky = nullptr;
@@ -216,6 +217,7 @@ int allocate(rc2dgi_ctx *c) {
   c->mpitch = ((c->W + 63) / 64) * 2;
   HIPCHK(c, alloc(&c->occ, (size_t)c->mpitch * c->H * sizeof(unsigned)));
   HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
+  HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->gi1, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->gi2, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
@@ -558,7 +560,10 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
   const bool T = c->timing;
-  // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362)
+  // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362); the "t" variants read an 8x8-tiled copy
+  bool tiled = false;
+  for (int v : c->rc_variant) tiled |= rc_variant_tiled(v);
+  if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
@@ -581,6 +586,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.order_py = (c->rc_order[L] >> 8) & 0xFF;
     a.order_dg = c->rc_order[L] >> 16;
     a.map_cache = &c->rc_maps;
+    a.dist_tiled = c->dist_t;
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
       a.p1 = r.second;
@@ -681,11 +687,12 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   const bool timing = c->timing;
   c->timing = true;
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
-  const int kVariants[] = {0, 13};  // march loop rolled / fully unrolled
+  const int kVariants[] = {0, 13, 14, 15};  // march rolled / unrolled, linear / tiled distance field
+  const int nv = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
   std::vector<float> best(c->N, 1e30f);
   std::vector<int> pick(c->rc_order), pickv(c->rc_variant);
   std::vector<float> lv(c->N);
-  for (int k = 0; k < 2 * nc; ++k) {
+  for (int k = 0; k < nv * nc; ++k) {
     const int v = kVariants[k / nc], o = k % nc;
     for (int L = 0; L < c->N; ++L) {
       c->rc_order[L] = order_code(kOrderCandidates[o][0], kOrderCandidates[o][1], kOrderCandidates[o][2]);

@@ -71,10 +71,16 @@ struct RcLevelArgs {
   int p0 = 0, p1 = -1;   // probe rows [p0, p1) of every direction block (-1 = all)
   int order_px = 0, order_py = 0, order_dg = 0;  // workgroup order (0: tile-major, direction-minor)
   RcMapCache *map_cache = nullptr;  // where the launch finds / builds its workgroup map
+  const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
 };
+
+// distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
+hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,
+                            hipStream_t st);
 
 int rc_variant_count();
 const char *rc_variant_name(int v);
+bool rc_variant_tiled(int v);  // reads the 8x8-tiled distance field
 
 // one RadianceCascades.fs level
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);

@@ -240,6 +240,7 @@ struct RcParams {
   float aspx, aspy, t0, t1, reflectivity;
   float sWf, sHf;  // screen size as floats (power-of-two screen path)
   const uint2 *wg_map;  // workgroup -> (tile x | y << 16, direction group), host-built (XCD remap + order)
+  int tpr;              // 8x8 tiles per row of the tiled distance field (TILED)
 };
 
 // q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
@@ -327,7 +328,9 @@ __device__ __forceinline__ int cvt_floor(float x) {
 // (p is never NaN, and never -0: the origin term is > 0, and x + (-x) rounds to +0).
 // UNR: unroll factor of the march loop.  Fully unrolled (32) suits the gather-bound high levels;
 // rolled (1) the VALU-bound low levels (no SGPR spills, occupancy 8).
-template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR>
+// TILED: `dist` is the 8x8-tiled copy (k_dist_tile): one 128-byte line holds an 8x8 texel tile,
+// so the nearly parallel rays of a lane (and vertical-ish steps) share lines.
+template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, bool TILED>
 __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *__restrict__ upper,
                                                      float4 *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
@@ -416,6 +419,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
 #pragma unroll UNR
   for (int it = 0; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
     int idx[NR];
+    unsigned didx[NR];  // distance-field index (tiled or linear)
     bool live[NR];
     bool any_live = false;
 #pragma unroll
@@ -423,15 +427,24 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       const int r = k % ND, p = k / ND;
       const float px = ox + (t[k] * rdx[r]) * P.aspy;
       const float py = oy[p] + (t[k] * rdy[r]) * P.aspx;
+      int ix, iy;
       if constexpr (P2S) {
         live[k] = act[k] && !(t[k] > P.t1) && __float_as_uint(px) <= 0x3f800000u &&
                   __float_as_uint(py) <= 0x3f800000u;
-        const int ix = cvt_floor(px * P.sWf) & (P.s.W - 1), iy = cvt_floor(py * P.sHf) & (P.s.H - 1);
-        idx[k] = live[k] ? (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix : 0;  // < 2^24 operands
+        ix = cvt_floor(px * P.sWf) & (P.s.W - 1);
+        iy = cvt_floor(py * P.sHf) & (P.s.H - 1);
       } else {
         live[k] = act[k] && !(t[k] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
-        idx[k] = live[k] ? wrap_nearest(py, say) * P.s.pitch + wrap_nearest(px, sax) : 0;
+        ix = wrap_nearest(px, sax);
+        iy = wrap_nearest(py, say);
       }
+      if (!live[k]) ix = iy = 0;
+      idx[k] = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;  // < 2^24 operands
+      if constexpr (TILED)
+        didx[k] = ((__umul24((unsigned)iy >> 3, (unsigned)P.tpr) + ((unsigned)ix >> 3)) << 6) |
+                  (((unsigned)iy & 7u) << 3) | ((unsigned)ix & 7u);
+      else
+        didx[k] = (unsigned)idx[k];
       act[k] = live[k];
       any_live |= live[k];
     }
@@ -443,8 +456,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
     unsigned q[NR];
 #pragma unroll
     for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
-      q[k] = *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) +
-                                                       ((unsigned)idx[k] << 1));
+      q[k] = *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + (didx[k] << 1));
     bool any = false;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {  // branch-free: selects, no exec-mask juggling
@@ -579,6 +591,19 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       out[(size_t)j * P.c.pitch + i] = blend_over_black(acc);
     }
   }
+}
+
+// ---------------------------------------------------------------- tiled distance field
+// dist (pitch-linear) -> 8x8 tiles of 64 texels (one 128-byte line), tiles row-major, tpr tiles per
+// row; a thread moves one 16-byte row segment (8 texels) of one tile
+__global__ __launch_bounds__(256) void k_dist_tile(const unsigned short *__restrict__ dist, int pitch,
+                                                   unsigned short *__restrict__ tiled, int tpr, int W, int H) {
+  const int seg = blockIdx.x * 64 + (threadIdx.x & 63);  // 8-texel segment = tile column
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (seg >= tpr || j >= H) return;
+  const uint4 v = *reinterpret_cast<const uint4 *>(dist + (size_t)j * pitch + seg * 8);
+  *reinterpret_cast<uint4 *>(tiled + (((size_t)(j >> 3) * tpr + seg) << 6) + ((j & 7) << 3)) = v;
+  (void)W;
 }
 
 // ---------------------------------------------------------------- Blur + copy-back
@@ -929,7 +954,7 @@ static const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles
   return e.dev;
 }
 
-template <int TX, int TY, int PY, int PD = 1, int UNR = 1>
+template <int TX, int TY, int PY, int PD = 1, int UNR = 1, bool TILED = false>
 static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
   const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
@@ -944,11 +969,13 @@ static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t 
   // tile coordinates fit the map's 16-bit fields (<= 32768 probes per axis)
   P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, P.opx, P.opy, P.odg);
   if (!P.wg_map) return hipErrorOutOfMemory;
+  P.tpr = (P.s.W + 7) / 8;
+  if (TILED && !a.dist_tiled) return hipErrorInvalidValue;
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
 #define RC2DGI_RC(TOPV, P2V)                                                                                      \
-  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR>), dim3(nwg), dim3(TX * TY), 0, st, P, a.upper, a.out, \
-                     a.dist, a.color, a.emissive, a.dirs, a.sky)
+  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, TILED>), dim3(nwg), dim3(TX * TY), 0, st, P,      \
+                     a.upper, a.out, TILED ? a.dist_tiled : a.dist, a.color, a.emissive, a.dirs, a.sky)
   const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
   const bool top = a.level == a.N - 1;
   if (top) {
@@ -962,11 +989,12 @@ static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t 
 
 // RC tile variants (tuning knob "rc_variant"): TXxTYxPY probes per workgroup, "dD" = D direction
 // blocks per workgroup (needs 4^level >= D; falls back to d1 below that)
-// ("u": march loop fully unrolled)
+// ("u": march loop fully unrolled, "t": 8x8-tiled distance field)
 static const char *kRcVariantNames[] = {"16x16x1", "16x8x2",   "16x16x2",  "32x8x1",   "64x4x1",
                                         "8x8x1",   "32x8x2",   "16x16x1d2", "16x16x1d4", "16x8x1d2",
-                                        "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u"};
+                                        "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t"};
 int rc_variant_count() { return (int)(sizeof(kRcVariantNames) / sizeof(kRcVariantNames[0])); }
+bool rc_variant_tiled(int v) { return v == 14 || v == 15; }
 const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
@@ -1012,6 +1040,8 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
     case 11: e = nblk >= 4 ? launch_rc_tiles<16, 8, 1, 4>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
     case 12: e = nblk >= 4 ? launch_rc_tiles<8, 8, 1, 4>(a, P, st) : launch_rc_tiles<8, 8, 1>(a, P, st); break;
     case 13: e = launch_rc_tiles<16, 16, 1, 1, 32>(a, P, st); break;
+    case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, true>(a, P, st); break;
+    case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, true>(a, P, st); break;
     default: e = launch_rc_tiles<16, 16, 1>(a, P, st); break;
   }
   if (e != hipSuccess) return e;
@@ -1098,6 +1128,14 @@ hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, 
   if (row0 >= row1) return hipSuccess;
   hipLaunchKernelGGL(k_merge, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in, gi, temp, color_out, s, c,
                      row0, row1);
+  return hipGetLastError();
+}
+
+hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,
+                            hipStream_t st) {
+  const int tpr = (W + 7) / 8;
+  hipLaunchKernelGGL(k_dist_tile, dim3(ceil_div(tpr, 64), ceil_div(H, 4)), dim3(256), 0, st, dist, pitch, tiled, tpr,
+                     W, H);
   return hipGetLastError();
 }
 
