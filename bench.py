@@ -254,6 +254,10 @@ def main():
                     help="strips: one frame split into row strips over the ranks (BASELINE configs[3])")
     ap.add_argument("--no-autotune", action="store_true",
                     help="keep the default RC workgroup order (setup otherwise times the candidates per level)")
+    ap.add_argument("--save-tuning", default="", help="write the chosen per-level rc_order / rc_variant (JSON)")
+    ap.add_argument("--load-tuning", default="",
+                    help="apply per-level rc_order / rc_variant from a --save-tuning file instead of autotuning "
+                         "(profiler runs replay the bench's schedule)")
     ap.add_argument("--shards", type=int, default=1,
                     help="strips on one process: run this many shards as in-process contexts")
     a = ap.parse_args()
@@ -282,8 +286,20 @@ def main():
     # inputs resident in HBM before the timed region
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
-    orders = None if a.no_autotune else ctx.autotune(2)  # setup: schedule choice, results identical
+    if a.load_tuning:
+        with open(a.load_tuning) as f:
+            tun = json.load(f)
+        for L in range(N):
+            ctx.set_tuning(f"rc_order_L{L}", tun["rc_order"][L])
+            ctx.set_tuning(f"rc_variant_L{L}", tun["rc_variant"][L])
+        orders = tun["rc_order"]
+    else:
+        orders = None if a.no_autotune else ctx.autotune(2)  # setup: schedule choice, results identical
     variants = [ctx.get_tuning(f"rc_variant_L{L}") for L in range(N)]
+    orders = [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)] if orders else None
+    if a.save_tuning and rank == 0:
+        with open(a.save_tuning, "w") as f:
+            json.dump({"rc_order": [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)], "rc_variant": variants}, f)
     ctx.set_timing(True)
     if a.sweep_rc:
         sweep_rc(ctx, N, a.steps, rounds=3)
