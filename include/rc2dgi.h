@@ -159,6 +159,23 @@ int rc2dgi_get_tuning(rc2dgi_ctx *ctx, const char *key, int *value);
 int rc2dgi_set_keep_levels(rc2dgi_ctx *ctx, int enable);
 int rc2dgi_download_level(rc2dgi_ctx *ctx, int level, void *host, int pitch_bytes, int format);
 
+/* ---- on-device scene producer: the painted inputs without a host upload.
+ * rc2dgi_paint(ctx, COLOR | EMISSIVE, clear, prims, n) is
+ *   BeginTextureMode(rt); ClearBackground(clear) [clear != NULL, RGBA 0..255]; draw prims in
+ *   order; EndTextureMode()
+ * as RenderScene / RedrawSceneToRTs do it (RC2DGI.cs:224-264, 528-545), with raylib 5.5 semantics:
+ *   RC2DGI_PRIM_RECT    DrawRectangleRec(x, y, w, h) / DrawRectangle
+ *   RC2DGI_PRIM_CIRCLE  DrawCircleV((x, y), radius = w)  (36-segment fan)
+ * in raylib screen coordinates (y down), colours as raylib Color, alpha-blended.  Coordinates
+ * must be finite with magnitude below 2^22 pixels.  Returns when the texture is painted. */
+typedef struct rc2dgi_prim {
+  int kind;                  /* RC2DGI_PRIM_RECT | RC2DGI_PRIM_CIRCLE */
+  float x, y, w, h;          /* rect: top-left corner and size; circle: centre, w = radius */
+  unsigned char r, g, b, a;  /* raylib Color */
+} rc2dgi_prim;
+enum { RC2DGI_PRIM_RECT = 0, RC2DGI_PRIM_CIRCLE = 1 };
+int rc2dgi_paint(rc2dgi_ctx *ctx, int which, const unsigned char *clear_rgba, const rc2dgi_prim *prims, int n);
+
 /* ---- row-strip sharding of one frame over `world` ranks.
  * rc2dgi_set_shard: the context computes screen rows [rank*H/world, (rank+1)*H/world) of the
  * merged colorRT / tempRT and exactly what they depend on (world = 1: the whole frame again).

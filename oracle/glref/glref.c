@@ -611,9 +611,117 @@ static int run_capture(int W, int H, int N, float renderScale, float skyRadiance
 }
 
 /* ---------------------------------------------------------------- main */
+/* ---------------------------------------------------------------- scene painting (raylib 5.5 shapes)
+ * --paint FILE: the painted inputs of RenderScene / RedrawSceneToRTs (RC2DGI.cs:224-264, 528-545):
+ * BeginTextureMode(rt); ClearBackground(c); DrawRectangleRec / DrawRectangle / DrawCircleV ...;
+ * EndTextureMode.  Restated from raylib 5.5 (rshapes.c, rlgl.h; external dependency pinned by
+ * Raylib-cs 7.0.1, not in the reference tree):
+ *   - projection rlOrtho(0, w, h, 0, 0, 1) (y down), modelview identity;
+ *   - rectangles: quad TL, BL, BR, TR (DrawRectanglePro, rotation 0);
+ *   - circles: DrawCircleSector(c, r, 0, 360, 36): vertices c + (cosf(DEG2RAD*a), sinf(DEG2RAD*a))*r,
+ *     a = 0, 10, ..., 360, emitted as quads (c, P(a+20), P(a+10), P(a));
+ *   - quads split (0,1,2), (0,2,3); unorm8 vertex colours; default shader over a white texture;
+ *     blending SRC_ALPHA / ONE_MINUS_SRC_ALPHA.
+ * File lines (colour components 0..255):  clear R G B A | rect X Y W H R G B A | circle X Y RADIUS R G B A */
+typedef struct {
+  float x, y, z, u, v;
+  unsigned char c[4];
+} PaintVertex;
+
+static void pv(PaintVertex *o, float x, float y, const unsigned char *c) {
+  o->x = x;
+  o->y = y;
+  o->z = 0.f;
+  o->u = 0.f;
+  o->v = 0.f;
+  memcpy(o->c, c, 4);
+}
+
+static int run_paint(const char *path, int W, int H) {
+  FILE *f = fopen(path, "r");
+  if (!f) die("cannot open paint file");
+  RT rt = make_rt(W, H, 0);
+  Program p = make_program(kDefaultFS, "default.fs");
+  const float rl = (float)W, tb = (float)(0 - H), fn = 1.0f; /* rlOrtho(0, W, H, 0, 0, 1) */
+  const float mvp[16] = {2.0f / rl, 0, 0, 0, 0, 2.0f / tb, 0, 0, 0, 0, -2.0f / fn, 0,
+                         -(0.0f + (float)W) / rl, -(0.0f + (float)H) / tb, -(1.0f + 0.0f) / fn, 1.0f};
+  p_glUseProgram(p.prog);
+  p_glUniformMatrix4fv(p_glGetUniformLocation(p.prog, "mvp"), 1, GL_FALSE, mvp);
+  GLuint white;
+  const float one[4] = {1.f, 1.f, 1.f, 1.f};
+  p_glGenTextures(1, &white);
+  p_glBindTexture(GL_TEXTURE_2D, white);
+  p_glTexImage2D(GL_TEXTURE_2D, 0, GL_RGBA32F, 1, 1, 0, GL_RGBA, GL_FLOAT, one);
+  p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_MIN_FILTER, GL_NEAREST);
+  p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_MAG_FILTER, GL_NEAREST);
+  GLuint vao, vbo;
+  p_glGenVertexArrays(1, &vao);
+  p_glBindVertexArray(vao);
+  p_glGenBuffers(1, &vbo);
+  p_glBindBuffer(GL_ARRAY_BUFFER, vbo);
+  p_glVertexAttribPointer(0, 3, GL_FLOAT, GL_FALSE, sizeof(PaintVertex), (void *)0);
+  p_glEnableVertexAttribArray(0);
+  p_glVertexAttribPointer(1, 2, GL_FLOAT, GL_FALSE, sizeof(PaintVertex), (void *)12);
+  p_glEnableVertexAttribArray(1);
+  p_glVertexAttribPointer(3, 4, GL_UNSIGNED_BYTE, GL_TRUE, sizeof(PaintVertex), (void *)20);
+  p_glEnableVertexAttribArray(3);
+  p_glEnable(GL_BLEND);
+  p_glBlendFunc(GL_SRC_ALPHA, GL_ONE_MINUS_SRC_ALPHA);
+  p_glBlendEquation(GL_FUNC_ADD);
+  const float DEG2RAD = 3.14159265358979323846f / 180.0f;
+  PaintVertex v[18 * 6];
+  char kind[32];
+  while (fscanf(f, "%31s", kind) == 1) {
+    int n = 0;
+    unsigned char c[4];
+    int ci[4];
+    if (!strcmp(kind, "clear")) {
+      if (fscanf(f, "%d %d %d %d", &ci[0], &ci[1], &ci[2], &ci[3]) != 4) die("bad clear");
+      clear_rt(rt, (float)ci[0] / 255, (float)ci[1] / 255, (float)ci[2] / 255, (float)ci[3] / 255);
+      continue;
+    }
+    float x, y, w = 0.f, h = 0.f;
+    if (!strcmp(kind, "rect")) {
+      if (fscanf(f, "%f %f %f %f %d %d %d %d", &x, &y, &w, &h, &ci[0], &ci[1], &ci[2], &ci[3]) != 8) die("bad rect");
+      for (int k = 0; k < 4; ++k) c[k] = (unsigned char)ci[k];
+      const float tl[2] = {x, y}, tr[2] = {x + w, y}, bl[2] = {x, y + h}, br[2] = {x + w, y + h};
+      pv(&v[n++], tl[0], tl[1], c); pv(&v[n++], bl[0], bl[1], c); pv(&v[n++], br[0], br[1], c);
+      pv(&v[n++], tl[0], tl[1], c); pv(&v[n++], br[0], br[1], c); pv(&v[n++], tr[0], tr[1], c);
+    } else if (!strcmp(kind, "circle")) {
+      if (fscanf(f, "%f %f %f %d %d %d %d", &x, &y, &w, &ci[0], &ci[1], &ci[2], &ci[3]) != 7) die("bad circle");
+      for (int k = 0; k < 4; ++k) c[k] = (unsigned char)ci[k];
+      const float step = 360.0f / 36.0f;
+      float a = 0.0f;
+      for (int i = 0; i < 18; ++i) {
+        const float a2 = a + step * 2.0f, a1 = a + step;
+        const float p2x = x + cosf(DEG2RAD * a2) * w, p2y = y + sinf(DEG2RAD * a2) * w;
+        const float p1x = x + cosf(DEG2RAD * a1) * w, p1y = y + sinf(DEG2RAD * a1) * w;
+        const float p0x = x + cosf(DEG2RAD * a) * w, p0y = y + sinf(DEG2RAD * a) * w;
+        pv(&v[n++], x, y, c); pv(&v[n++], p2x, p2y, c); pv(&v[n++], p1x, p1y, c);
+        pv(&v[n++], x, y, c); pv(&v[n++], p1x, p1y, c); pv(&v[n++], p0x, p0y, c);
+        a += step * 2.0f;
+      }
+    } else {
+      die("unknown paint command");
+    }
+    p_glBindFramebuffer(GL_FRAMEBUFFER, rt.fbo);
+    p_glViewport(0, 0, W, H);
+    p_glUseProgram(p.prog);
+    p_glActiveTexture(GL_TEXTURE0);
+    p_glBindTexture(GL_TEXTURE_2D, white);
+    p_glBindVertexArray(vao);
+    p_glBufferData(GL_ARRAY_BUFFER, (GLsizeiptr)(n * sizeof(PaintVertex)), v, GL_STREAM_DRAW);
+    p_glDrawArrays(GL_TRIANGLES, 0, n);
+  }
+  fclose(f);
+  p_glFinish();
+  dump_rt(rt, "paint");
+  return 0;
+}
+
 int main(int argc, char **argv) {
   const char *shaders = NULL, *in_color = NULL, *in_emis = NULL, *mode = "f32", *dump = "final";
-  const char *probe_fs = NULL;
+  const char *probe_fs = NULL, *paint = NULL;
   int W = 0, H = 0, N = 6, frames = 1, linux_merge = 0, probe_linear = 0, capture = 0;
   float rayRange = 2.0f, renderScale = 1.0f;
   /* defaults: RC2DGI.cs:34-41 */
@@ -642,6 +750,7 @@ int main(int argc, char **argv) {
     else if (ARG("--reflectivity")) reflectivity = (float)atof(v);
     else if (ARG("--blur-radius")) blurRadius = (float)atof(v);
     else if (ARG("--probe-fs")) probe_fs = v;
+    else if (ARG("--paint")) paint = v;
     else if (!strcmp(a, "--linux-merge-fallback")) linux_merge = 1;
     else if (!strcmp(a, "--probe-linear")) probe_linear = 1;
     else if (!strcmp(a, "--capture-tables")) capture = 1;
@@ -652,12 +761,13 @@ int main(int argc, char **argv) {
     }
 #undef ARG
   }
-  if (W <= 0 || H <= 0 || (!in_color && !capture)) die("need --w --h --in-color");
+  if (W <= 0 || H <= 0 || (!in_color && !capture && !paint)) die("need --w --h --in-color");
   g_rgba8 = !strcmp(mode, "rgba8");
   init_gl();
   init_quad();
   p_glDisable(GL_DEPTH_TEST);
   p_glDisable(GL_CULL_FACE);
+  if (paint) return run_paint(paint, W, H);
   if (capture)
     return run_capture(W, H, N, renderScale, skyRadiance, skyColor, sunColor, sunAngle);
   if (probe_fs) return run_probe(probe_fs, W, H, in_color, probe_linear, argc, argv);

@@ -13,8 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "librc2dgi.so")
-SOURCES = ["rc2dgi_kernels.hip", "rc2dgi_capi.cpp", "rc2dgi_shard.cpp"]
-HEADERS = ["rc2dgi_device.h", "rc2dgi_kernels.h", "rc2dgi_shard.h"]
+SOURCES = ["rc2dgi_kernels.hip", "rc2dgi_capi.cpp", "rc2dgi_shard.cpp", "rc2dgi_paint.hip"]
+HEADERS = ["rc2dgi_device.h", "rc2dgi_kernels.h", "rc2dgi_shard.h", "rc2dgi_paint.h"]
 ARCH = os.environ.get("RC2DGI_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: each a*b+c in the kernels is two IEEE roundings, exactly as the GLSL

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "rc2dgi_kernels.h"
+#include "rc2dgi_paint.h"
 #include "rc2dgi_shard.h"
 
 using namespace rc2dgi;
@@ -109,6 +110,7 @@ struct rc2dgi_ctx {
   std::vector<float4 *> level_bufs;  // debug copies of G_L
   // row-strip sharding
   RcMapCache rc_maps;  // host-built k_rc_level workgroup maps
+  PaintBuffers paint_buf;  // rc2dgi_paint primitive setup
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
   hipEvent_t ev_phase1 = nullptr;   // end of phase 1 (group exchange)
@@ -165,6 +167,7 @@ void free_level_bufs(rc2dgi_ctx *c) {
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
   c->rc_maps.clear();
+  c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t};
   for (void *p : bufs)
@@ -485,6 +488,31 @@ int rc2dgi_upload(rc2dgi_ctx *c, int which, const void *host, int pitch_bytes, i
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (which == RC2DGI_RT_COLOR) c->frame_done = false;
+  return RC2DGI_OK;
+}
+
+int rc2dgi_paint(rc2dgi_ctx *c, int which, const unsigned char *clear_rgba, const rc2dgi_prim *prims, int n) {
+  if (!c) return RC2DGI_E_ARG;
+  if (which != RC2DGI_RT_COLOR && which != RC2DGI_RT_EMISSIVE)
+    return fail(c, RC2DGI_E_ARG, "only COLOR and EMISSIVE are painted");
+  if (n < 0 || (n > 0 && !prims)) return fail(c, RC2DGI_E_ARG, "bad primitive list");
+  const float lim = 4194304.0f;  // 2^22 pixels
+  for (int k = 0; k < n; ++k) {
+    const rc2dgi_prim &q = prims[k];
+    if (q.kind != RC2DGI_PRIM_RECT && q.kind != RC2DGI_PRIM_CIRCLE)
+      return fail(c, RC2DGI_E_ARG, "primitive " + std::to_string(k) + ": unknown kind");
+    const float v[4] = {q.x, q.y, q.w, q.kind == RC2DGI_PRIM_RECT ? q.h : 0.0f};
+    for (float x : v)
+      if (!(std::fabs(x) < lim)) return fail(c, RC2DGI_E_ARG, "primitive " + std::to_string(k) + ": coordinates");
+    if (q.kind == RC2DGI_PRIM_RECT && !(std::fabs(q.x + q.w) < lim && std::fabs(q.y + q.h) < lim))
+      return fail(c, RC2DGI_E_ARG, "primitive " + std::to_string(k) + ": coordinates");
+    if (q.kind == RC2DGI_PRIM_CIRCLE && !(std::fabs(q.x) + std::fabs(q.w) < lim && std::fabs(q.y) + std::fabs(q.w) < lim))
+      return fail(c, RC2DGI_E_ARG, "primitive " + std::to_string(k) + ": coordinates");
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  float4 *dst = which == RC2DGI_RT_COLOR ? c->color_in : c->emissive;
+  HIPCHK(c, paint_prims(dst, c->W, c->H, c->sd.pitch, clear_rgba, prims, n, c->paint_buf, c->stream));
   if (which == RC2DGI_RT_COLOR) c->frame_done = false;
   return RC2DGI_OK;
 }

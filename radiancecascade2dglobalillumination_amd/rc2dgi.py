@@ -41,6 +41,13 @@ class RC2DGIError(RuntimeError):
         self.code = code
 
 
+class Prim(ctypes.Structure):
+    """rc2dgi_prim: raylib DrawRectangleRec (kind 0) / DrawCircleV (kind 1, w = radius)."""
+    _fields_ = [("kind", ctypes.c_int), ("x", ctypes.c_float), ("y", ctypes.c_float), ("w", ctypes.c_float),
+                ("h", ctypes.c_float), ("r", ctypes.c_ubyte), ("g", ctypes.c_ubyte), ("b", ctypes.c_ubyte),
+                ("a", ctypes.c_ubyte)]
+
+
 class _Config(ctypes.Structure):
     _fields_ = [("screen_width", ctypes.c_int), ("screen_height", ctypes.c_int), ("cascade_count", ctypes.c_int),
                 ("render_scale", ctypes.c_float), ("ray_range", ctypes.c_float), ("storage", ctypes.c_int),
@@ -91,6 +98,7 @@ def load_library(path: Optional[str] = None):
         "rc2dgi_get_tuning": ([vp, ctypes.c_char_p, ip], ctypes.c_int),
         "rc2dgi_download_level": ([vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "rc2dgi_autotune": ([vp, ctypes.c_int], ctypes.c_int),
+        "rc2dgi_paint": ([vp, ctypes.c_int, ctypes.POINTER(ctypes.c_ubyte), vp, ctypes.c_int], ctypes.c_int),
         "rc2dgi_set_shard": ([vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "rc2dgi_shard_rows": ([vp, ip, ip], ctypes.c_int),
         "rc2dgi_shard_unique_id": ([vp, ctypes.c_int], ctypes.c_int),
@@ -254,6 +262,17 @@ class RC2DGI:
             fmt, pitch = FMT_RGBA32F, self.screen_width * 16
         self._check(self._L.rc2dgi_upload(self._h, w, a.ctypes.data_as(ctypes.c_void_p), pitch, fmt),
                     f"upload {which}")
+
+    def paint(self, which: str, prims, clear=None) -> None:
+        """BeginTextureMode(colorRT | emissiveRT); ClearBackground(clear); raylib rectangles /
+        circles (RenderScene / RedrawSceneToRTs, RC2DGI.cs:224-264, 528-545) -- on the GPU.
+        prims: (kind, x, y, w_or_radius, h, r, g, b, a) in raylib screen coordinates."""
+        arr = (Prim * max(len(prims), 1))()
+        for k, p in enumerate(prims):
+            arr[k] = Prim(int(p[0]), float(p[1]), float(p[2]), float(p[3]), float(p[4]),
+                          *(int(v) for v in p[5:9]))
+        cl = None if clear is None else (ctypes.c_ubyte * 4)(*[int(v) for v in clear])
+        self._check(self._L.rc2dgi_paint(self._h, RT[which], cl, arr, len(prims)), f"paint {which}")
 
     def download(self, which: str, dtype=np.float32) -> np.ndarray:
         w = RT[which]

@@ -111,3 +111,31 @@ def random_scene(W: int, H: int, seed: int = 0, coverage: float = 0.05):
 def empty(W: int, H: int):
     """No occluders, no emitters: pure sky (known-answer case)."""
     return (_to_gl(_canvas(W, H, (0, 0, 0, 255))), _to_gl(_canvas(W, H, (0, 0, 0, 0))))
+
+
+# ---------------------------------------------------------------- raylib primitive lists
+# For rc2dgi_paint (the on-device scene producer): (kind, x, y, w_or_radius, h, r, g, b, a) in
+# raylib screen coordinates (y down), kind 0 = DrawRectangleRec / DrawRectangle, 1 = DrawCircleV.
+RECT, CIRCLE = 0, 1
+
+
+def demo_prims(W: int = 1200, H: int = 900, t: float = 3.0):
+    """RenderScene (RC2DGI.cs:224-264) at time t as primitive lists, scaled from 1200 x 900:
+    (color_clear, color_prims, emissive_clear, emissive_prims)."""
+    sx, sy = W / 1200.0, H / 900.0
+    sr = min(sx, sy)
+    col = [(RECT, x * sx, y * sy, w * sx, h * sy) + WHITE for (x, y, w, h) in DEMO_WALLS]
+    lime = ((t * 100.0) % 1200.0 * sx, (t * 75.0) % 900.0 * sy)
+    orange = ((t * 66.0) % 1200.0 * sx, (t * 46.0) % 900.0 * sy)
+    col.append((CIRCLE, lime[0], lime[1], 20.0 * sr, 0.0) + LIME)
+    col.append((CIRCLE, orange[0], orange[1], 80.0 * sr, 0.0) + ORANGE)
+    emis = [(CIRCLE, orange[0], orange[1], 100.0 * sr, 0.0) + ORANGE]
+    return (0, 0, 0, 255), col, (0, 0, 0, 0), emis
+
+
+def redraw_prims(wall_points, lights):
+    """RedrawSceneToRTs (RC2DGI.cs:528-545): user wall points as 10 x 10 white squares
+    (DrawRectangle((int)x - 5, (int)y - 5, 10, 10)) and lights as r = 10 discs."""
+    walls = [(RECT, float(int(x) - 5), float(int(y) - 5), 10.0, 10.0) + WHITE for (x, y) in wall_points]
+    lamps = [(CIRCLE, float(x), float(y), 10.0, 0.0) + tuple(c) for (x, y), c in lights]
+    return walls, lamps
