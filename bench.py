@@ -84,6 +84,30 @@ def cpu_baseline(W, H, N, rr, budget_s=12.0):
                        f"oracle/rc2dgi_oracle.c, {platform.processor() or platform.machine()})")
 
 
+def input_costs(ctx, W, H, color, emis, reps=5):
+    """Per-frame cost of producing the painted inputs (outside the timed frames): painting the
+    demo scene on the device (rc2dgi_paint) vs uploading both textures from host
+    memory (the reference app's path, PCIe).  Restores the bench's own inputs afterwards."""
+    from radiancecascade2dglobalillumination_amd import scenes
+
+    cc, cp, ec, ep = scenes.demo_prims(W, H)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.paint("color", cp, cc)
+        ctx.paint("emissive", ep, ec)
+    ctx.sync()
+    paint_ms = (time.perf_counter() - t0) * 1e3 / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.upload("color", color)
+        ctx.upload("emissive", emis)
+    ctx.sync()
+    upload_ms = (time.perf_counter() - t0) * 1e3 / reps
+    return {"device_paint_ms": round(paint_ms, 3), "host_upload_ms": round(upload_ms, 3),
+            "note": "both input textures per frame; not part of value"}
+
+
 def sweep_rc(ctx, N, steps, rounds=3):
     """Per-level HIP-event times of every RC tile variant, interleaved over rounds in one
     process (cdna_hip_programming.md §5.4 rule 24); prints one JSON line."""
@@ -362,6 +386,7 @@ def main():
                      "kernel": "k_rc_level", "bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(avg_launch_s * 1e3, 5)},
     }
+    line["inputs"] = input_costs(ctx, W, H, color, emis)
     if rank == 0 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(W, H, N, a.ray_range, a.cpu_budget)
     if rank == 0:

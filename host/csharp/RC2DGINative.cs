@@ -38,6 +38,16 @@ static unsafe class RC2DGINative
     [DllImport(Lib)] public static extern int rc2dgi_query(IntPtr ctx, out int cw, out int ch, out int jfaSteps, out int finalGi);
     [DllImport(Lib)] public static extern IntPtr rc2dgi_last_error(IntPtr ctx);
 
+    // rc2dgi_prim: DrawRectangleRec (Kind 0) / DrawCircleV (Kind 1, W = radius), raylib screen coordinates
+    [StructLayout(LayoutKind.Sequential)]
+    public struct Prim
+    {
+        public int Kind;
+        public float X, Y, W, H;
+        public byte R, G, B, A;
+    }
+    [DllImport(Lib)] public static extern int rc2dgi_paint(IntPtr ctx, int which, byte* clearRgba, Prim* prims, int n);
+
     static IntPtr ctx;
     static byte[] scratch = Array.Empty<byte>();
 
@@ -83,6 +93,20 @@ static unsafe class RC2DGINative
             Check(rc2dgi_download(ctx, (int)which, p, rt.Texture.Width * 4, (int)Format.RGBA8), "download");
             Raylib.UpdateTexture(rt.Texture, p);
         }
+    }
+
+    public static Prim Rect(Rectangle r, Color c) => new Prim { Kind = 0, X = r.X, Y = r.Y, W = r.Width, H = r.Height, R = c.R, G = c.G, B = c.B, A = c.A };
+    public static Prim Circle(System.Numerics.Vector2 p, float radius, Color c) => new Prim { Kind = 1, X = p.X, Y = p.Y, W = radius, R = c.R, G = c.G, B = c.B, A = c.A };
+
+    // BeginTextureMode(rt); ClearBackground(clear); draw prims; EndTextureMode -- on the GPU
+    // (RenderScene / RedrawSceneToRTs, RC2DGI.cs:224-264, 528-545)
+    public static void Paint(RT which, Color? clear, System.Collections.Generic.List<Prim> prims)
+    {
+        Prim[] a = prims.ToArray();
+        byte* cl = stackalloc byte[4];
+        if (clear is Color c) { cl[0] = c.R; cl[1] = c.G; cl[2] = c.B; cl[3] = c.A; }
+        fixed (Prim* p = a)
+            Check(rc2dgi_paint(ctx, (int)which, clear.HasValue ? cl : null, p, a.Length), "paint");
     }
 
     // DoRC2DGI() (RC2DGI.cs:267-406)
