@@ -27,8 +27,10 @@
  *     texture is giRT2 when N is even and giRT1 when N is odd (RC2DGI.cs:365).
  *
  * Storage: f32 semantics (RGBA32F render textures, the reference's own commented intent,
- * RC2DGI.cs:100-107).  RC2DGI_STORAGE_RGBA8_COMPAT (the literal 8-bit app) is reserved
- * and currently returns RC2DGI_E_UNSUPPORTED.
+ * RC2DGI.cs:100-107).  RC2DGI_STORAGE_F16 keeps that but stores giRT1 / giRT2 as RGBA16F,
+ * the format RC2DGI.cs:105-106 names (stores round toward zero as the GL reference
+ * implementation does; downloads convert exactly).  RC2DGI_STORAGE_RGBA8_COMPAT (the literal
+ * 8-bit app) is reserved and currently returns RC2DGI_E_UNSUPPORTED.
  */
 #ifndef RC2DGI_H
 #define RC2DGI_H
@@ -53,7 +55,8 @@ typedef enum rc2dgi_status {
 
 typedef enum rc2dgi_storage {
   RC2DGI_STORAGE_F32 = 0,
-  RC2DGI_STORAGE_RGBA8_COMPAT = 1
+  RC2DGI_STORAGE_RGBA8_COMPAT = 1,
+  RC2DGI_STORAGE_F16 = 2
 } rc2dgi_storage;
 
 /* render textures of the reference (RC2DGI.cs:19-25) */

@@ -34,7 +34,7 @@ class _Cfg(ctypes.Structure):
         ("render_scale", ctypes.c_float), ("ray_range", ctypes.c_float),
         ("sky_radiance", ctypes.c_float), ("sky_color", ctypes.c_float * 3),
         ("sun_color", ctypes.c_float * 3), ("sun_angle", ctypes.c_float),
-        ("reflectivity", ctypes.c_float), ("blur_radius", ctypes.c_float),
+        ("reflectivity", ctypes.c_float), ("blur_radius", ctypes.c_float), ("gi_f16", ctypes.c_int),
     ]
 
 
@@ -82,6 +82,9 @@ def lib():
         L.orc_merge.argtypes = [_f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 _f32p]
         L.orc_set_rows.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_set_gi_f16.argtypes = [ctypes.c_int]
+        L.orc_half_rtz.argtypes = [ctypes.c_float]
+        L.orc_half_rtz.restype = ctypes.c_float
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_set_num_threads.argtypes = [ctypes.c_int]
         _lib = L
@@ -102,11 +105,12 @@ class Params:
     sun_angle: float = 0.3
     reflectivity: float = 0.0
     blur_radius: float = 1.5
+    gi_f16: bool = False  # giRT1/2 stored as RGBA16F (RC2DGI.cs:105-106)
 
     def c(self) -> _Cfg:
         return _Cfg(self.W, self.H, self.N, self.render_scale, self.ray_range, self.sky_radiance,
                     (ctypes.c_float * 3)(*self.sky_color), (ctypes.c_float * 3)(*self.sun_color),
-                    self.sun_angle, self.reflectivity, self.blur_radius)
+                    self.sun_angle, self.reflectivity, self.blur_radius, int(self.gi_f16))
 
 
 def _p(a):

@@ -299,6 +299,7 @@ typedef struct {
 } RT;
 
 static int g_rgba8 = 0;
+static int g_next_f16 = 0; /* the next make_rt is RGBA16F (giRT1/2 with --gi-f16, probe target) */
 
 static RT make_rt(int w, int h, int linear) {
   RT rt;
@@ -306,7 +307,10 @@ static RT make_rt(int w, int h, int linear) {
   rt.h = h;
   p_glGenTextures(1, &rt.tex);
   p_glBindTexture(GL_TEXTURE_2D, rt.tex);
-  if (g_rgba8)
+  if (g_next_f16) {
+    p_glTexImage2D(GL_TEXTURE_2D, 0, GL_RGBA16F, w, h, 0, GL_RGBA, GL_FLOAT, NULL);
+    g_next_f16 = 0;
+  } else if (g_rgba8)
     p_glTexImage2D(GL_TEXTURE_2D, 0, GL_RGBA8, w, h, 0, GL_RGBA, GL_UNSIGNED_BYTE, NULL);
   else
     p_glTexImage2D(GL_TEXTURE_2D, 0, GL_RGBA32F, w, h, 0, GL_RGBA, GL_FLOAT, NULL);
@@ -442,7 +446,10 @@ static int run_probe(const char *fs_path, int W, int H, const char *in_path, int
   char *src = read_text(fs_path);
   if (!src) die("cannot read probe fs");
   Program p = make_program(src, fs_path);
-  RT in = make_rt(W, H, linear), out = make_rt(W, H, 0);
+  RT in = make_rt(W, H, linear);
+  for (int i = 1; i < argc; ++i)
+    if (!strcmp(argv[i], "--probe-out-f16")) g_next_f16 = 1;
+  RT out = make_rt(W, H, 0);
   float *img = load_f32(in_path, (size_t)W * H * 4);
   upload_rt(in, img);
   p_glDisable(GL_BLEND);
@@ -722,7 +729,7 @@ static int run_paint(const char *path, int W, int H) {
 int main(int argc, char **argv) {
   const char *shaders = NULL, *in_color = NULL, *in_emis = NULL, *mode = "f32", *dump = "final";
   const char *probe_fs = NULL, *paint = NULL;
-  int W = 0, H = 0, N = 6, frames = 1, linux_merge = 0, probe_linear = 0, capture = 0;
+  int W = 0, H = 0, N = 6, frames = 1, linux_merge = 0, probe_linear = 0, capture = 0, gi_f16 = 0;
   float rayRange = 2.0f, renderScale = 1.0f;
   /* defaults: RC2DGI.cs:34-41 */
   float blurRadius = 1.5f, sunAngle = 0.3f, skyRadiance = 1.0f, reflectivity = 0.0f;
@@ -753,6 +760,8 @@ int main(int argc, char **argv) {
     else if (ARG("--paint")) paint = v;
     else if (!strcmp(a, "--linux-merge-fallback")) linux_merge = 1;
     else if (!strcmp(a, "--probe-linear")) probe_linear = 1;
+    else if (!strcmp(a, "--probe-out-f16")) {}
+    else if (!strcmp(a, "--gi-f16")) gi_f16 = 1; /* giRT1/2 as R16G16B16A16 (RC2DGI.cs:105-106) */
     else if (!strcmp(a, "--capture-tables")) capture = 1;
     else if (!strcmp(a, "--u") || !strcmp(a, "--ui")) ++i; /* probe-mode uniforms */
     else {
@@ -789,7 +798,10 @@ int main(int argc, char **argv) {
   /* RC2DGI.cs:79-98 */
   RT emissiveRT = make_rt(W, H, 0), colorRT = make_rt(W, H, 0), distRT = make_rt(W, H, 0);
   RT jumpRT1 = make_rt(W, H, 0), jumpRT2 = make_rt(W, H, 0);
-  RT giRT1 = make_rt(CW, CH, 1), giRT2 = make_rt(CW, CH, 1);
+  g_next_f16 = gi_f16;
+  RT giRT1 = make_rt(CW, CH, 1);
+  g_next_f16 = gi_f16;
+  RT giRT2 = make_rt(CW, CH, 1);
   RT tempRT = make_rt(W, H, 0), cascadeBlurRT = make_rt(CW, CH, 1);
 
   /* raylib: blending on, alpha mode */

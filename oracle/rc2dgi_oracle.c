@@ -19,6 +19,7 @@
 #include "rc2dgi_oracle.h"
 
 #include <math.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -173,6 +174,31 @@ int orc_sky_table(const orc_cfg *c, float *rgb) {
 
 /* ------------------------------------------------------------ passes */
 /* shaders/ScreenUV.fs:10-28 over a target cleared to (0,0,0,1) (RC2DGI.cs:278-285) */
+/* ---------------------------------------------------------------- RGBA16F giRT storage */
+float orc_half_rtz(float x) {
+  if (x != x || isinf(x)) return x;
+  float a = fabsf(x), r;
+  if (a >= 65504.0f) {
+    r = 65504.0f; /* round toward zero never reaches infinity */
+  } else if (a < 6.103515625e-05f) {
+    r = floorf(a * 16777216.0f) / 16777216.0f; /* half subnormals: multiples of 2^-24 */
+  } else {
+    uint32_t u;
+    memcpy(&u, &a, 4);
+    u &= ~((1u << 13) - 1u); /* keep 10 mantissa bits */
+    memcpy(&r, &u, 4);
+  }
+  return x < 0.0f ? -r : r;
+}
+
+static int g_gi_f16 = 0;
+void orc_set_gi_f16(int on) { g_gi_f16 = on; }
+
+static void gi_store_round(float *d) {
+  if (!g_gi_f16) return;
+  for (int k = 0; k < 4; ++k) d[k] = orc_half_rtz(d[k]);
+}
+
 /* test-only row window (row-strip sharding tests): the JFA, DF, blur, copy-back and merge
  * passes write only rows [g_row0, g_row1) when set; the default is every row */
 static int g_row0 = 0, g_row1 = 1 << 30;
@@ -354,6 +380,8 @@ void orc_rc_level(const orc_cfg *c, int level, const float *upper, const float *
       float *d = out + ((size_t)j * CW + i) * 4;
       d[0] = 0.0f; d[1] = 0.0f; d[2] = 0.0f; d[3] = 1.0f;
       blend_store(d, acc);
+      if (c->gi_f16)
+        for (int k = 0; k < 4; ++k) d[k] = orc_half_rtz(d[k]);
     }
 }
 
@@ -397,6 +425,7 @@ void orc_blur_copyback(const float *blur, float *gi, int CW, int CH, const float
       float s[4];
       sample_bilinear(blur, CW, CH, u, v, s);
       blend_store(gi + ((size_t)j * CW + i) * 4, s);
+      gi_store_round(gi + ((size_t)j * CW + i) * 4);
     }
 }
 
@@ -444,6 +473,7 @@ int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,
   int mx = c->W > c->H ? c->W : c->H;
   float aspx = (float)c->W / (float)mx, aspy = (float)c->H / (float)mx;
 
+  g_gi_f16 = c->gi_f16;
   /* 1. ScreenUV into jumpRT1 */
   orc_screen_uv(color_in, out->jump1, c->W, c->H, tcs);
   /* 2. jump flood ping-pong; jumpRT2 keeps its ClearAllRTs content until written */
@@ -511,5 +541,6 @@ int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,
   orc_merge(color_in, finalGI, out->temp, out->color_out, c->W, c->H, CW, CH, tcs);
   free(dirs);
   free(sky);
+  g_gi_f16 = 0; /* the per-pass API defaults to RGBA32F again */
   return 0;
 }

@@ -35,6 +35,7 @@ typedef struct orc_cfg {
   float sun_angle;      /* _SunAngle, RC2DGI.cs:35 */
   float reflectivity;   /* _Reflectivity, RC2DGI.cs:41 */
   float blur_radius;    /* cascadeBlurRadius / _BlurRadius, RC2DGI.cs:34 */
+  int gi_f16;           /* giRT1/2 as RGBA16F (RC2DGI.cs:105-106): stores round toward zero */
 } orc_cfg;
 
 /* Optional overrides used only to pin the restatement against llvmpipe goldens:
@@ -81,6 +82,11 @@ void orc_merge(const float *color, const float *gi, float *temp, float *color_ou
 /* whole frame = ClearAllRTs + DoRC2DGI on the given painted inputs. returns 0 on success */
 int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,
               const orc_overrides *ov, orc_frame_out *out);
+
+/* float -> RGBA16F storage -> float: round toward zero (llvmpipe's half store, probed) */
+float orc_half_rtz(float x);
+/* giRT stores of orc_blur_copyback round to half when set (orc_frame sets it from cfg) */
+void orc_set_gi_f16(int on);
 
 /* test-only: restrict the JFA / DF / blur / copy-back / merge passes to rows [row0, row1)
  * (row1 < 0: all rows) -- row-strip sharding tests */

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -74,6 +75,7 @@ struct rc2dgi_ctx {
   // knobs (RC2DGI.cs:28-41, 66-68)
   int W = 0, H = 0, N = 0;
   float render_scale = 1.0f;
+  int storage = RC2DGI_STORAGE_F32;
   float ray_range = 2.0f;
   float sky_radiance = 1.0f, sky_color[3] = {0.5f, 0.6f, 0.8f}, sun_color[3] = {1.0f, 0.9f, 0.6f};
   float sun_angle = 0.3f, reflectivity = 0.0f, blur_radius = 1.5f;
@@ -120,6 +122,9 @@ struct rc2dgi_ctx {
 };
 
 namespace {
+
+// giRT1 / giRT2 texel size of the context's storage
+size_t gi_bytes(const rc2dgi_ctx *c) { return c->storage == RC2DGI_STORAGE_F16 ? 8 : 16; }
 
 int fail(rc2dgi_ctx *c, int code, const std::string &msg) {
   if (c) c->err = msg;
@@ -209,7 +214,7 @@ int allocate(rc2dgi_ctx *c) {
   derive_sizes(c->W, c->H, c->N, c->render_scale, c->CW, c->CH, c->S);
   const int sp = round_up(c->W, 64), cp = round_up(c->CW, 64);
   c->sd = ScreenDims{c->W, c->H, sp, is_pow2(c->W), is_pow2(c->H)};
-  c->cd = CascadeDims{c->CW, c->CH, cp, is_pow2(c->CW), is_pow2(c->CH)};
+  c->cd = CascadeDims{c->CW, c->CH, cp, is_pow2(c->CW), is_pow2(c->CH), c->storage == RC2DGI_STORAGE_F16};
   const size_t ns = (size_t)sp * c->H, nc = (size_t)cp * c->CH;
   HIPCHK(c, alloc(&c->color_in, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->emissive, ns * sizeof(float4)));
@@ -221,10 +226,11 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->occ, (size_t)c->mpitch * c->H * sizeof(unsigned)));
   HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
-  HIPCHK(c, alloc(&c->gi1, nc * sizeof(float4)));
-  HIPCHK(c, alloc(&c->gi2, nc * sizeof(float4)));
+  const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
+  HIPCHK(c, alloc(&c->gi1, nc * gsz));
+  HIPCHK(c, alloc(&c->gi2, nc * gsz));
   HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
-  HIPCHK(c, alloc(&c->gi_spare, nc * sizeof(float4)));
+  HIPCHK(c, alloc(&c->gi_spare, nc * gsz));
   HIPCHK(c, alloc(&c->dirs, dir_table_len(c->N) * sizeof(float2)));
   HIPCHK(c, alloc(&c->sky, ((size_t)4 << (2 * (c->N - 1))) * sizeof(float4)));
   // initial contents: ClearAllRTs (RC2DGI.cs:109) -> (0,0,0,1) is implied by the frame
@@ -244,7 +250,7 @@ int allocate(rc2dgi_ctx *c) {
   for (int L = 0; L < c->N; ++L) c->rc_order[L] = default_rc_order(L);
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
-    for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, nc * sizeof(float4)));
+    for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, nc * gsz));
   }
   return RC2DGI_OK;
 }
@@ -307,6 +313,32 @@ int upload_tables(rc2dgi_ctx *c) {
   return RC2DGI_OK;
 }
 
+float half_to_float(uint16_t h) {  // exact
+  const unsigned s = (h >> 15) & 1u, e = (h >> 10) & 31u, m = h & 1023u;
+  float v;
+  if (e == 0) v = std::ldexp((float)m, -24);
+  else if (e == 31) v = m ? NAN : INFINITY;
+  else v = std::ldexp((float)(m | 1024u), (int)e - 25);
+  return s ? -v : v;
+}
+
+// a GI-format cascade texture -> float4 (CW x CH, tight)
+int fetch_gi(rc2dgi_ctx *c, const void *src, std::vector<float4> &img) {
+  const size_t gsz = gi_bytes(c);
+  if (gsz == 16) {
+    HIPCHK(c, hipMemcpy2D(img.data(), (size_t)c->CW * 16, src, (size_t)c->cd.pitch * 16, (size_t)c->CW * 16, c->CH,
+                          hipMemcpyDeviceToHost));
+    return RC2DGI_OK;
+  }
+  std::vector<uint16_t> h((size_t)c->CW * c->CH * 4);
+  HIPCHK(c, hipMemcpy2D(h.data(), (size_t)c->CW * 8, src, (size_t)c->cd.pitch * 8, (size_t)c->CW * 8, c->CH,
+                        hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < img.size(); ++k)
+    img[k] = make_float4(half_to_float(h[4 * k]), half_to_float(h[4 * k + 1]), half_to_float(h[4 * k + 2]),
+                         half_to_float(h[4 * k + 3]));
+  return RC2DGI_OK;
+}
+
 FramePlan make_plan(const rc2dgi_ctx *c) {
   return plan_frame(PlanInputs{c->W, c->H, c->CW, c->CH, c->S, c->N, c->blur_radius, c->rank, c->world});
 }
@@ -338,7 +370,7 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
   for (int r : cfg->reserved)
     if (r != 0) return RC2DGI_E_ARG;
   if (cfg->storage == RC2DGI_STORAGE_RGBA8_COMPAT) return RC2DGI_E_UNSUPPORTED;
-  if (cfg->storage != RC2DGI_STORAGE_F32) return RC2DGI_E_ARG;
+  if (cfg->storage != RC2DGI_STORAGE_F32 && cfg->storage != RC2DGI_STORAGE_F16) return RC2DGI_E_ARG;
   rc2dgi_ctx *c = new (std::nothrow) rc2dgi_ctx();
   if (!c) return RC2DGI_E_OOM;
   c->device = cfg->device;
@@ -346,6 +378,7 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
   c->H = cfg->screen_height;
   c->N = cfg->cascade_count;
   c->render_scale = cfg->render_scale;
+  c->storage = cfg->storage;
   c->ray_range = cfg->ray_range;
   int rc = RC2DGI_OK;
   hipError_t e = hipSetDevice(c->device);
@@ -556,7 +589,8 @@ int do_phase1(rc2dgi_ctx *c, const FramePlan &plan) {
     HIPCHK(c, hipMemsetAsync(c->dist, 0xFF, ns * 2, st));
     HIPCHK(c, hipMemsetAsync(c->temp, 0xFF, ns * 16, st));
     HIPCHK(c, hipMemsetAsync(c->color_out, 0xFF, ns * 16, st));
-    for (float4 *b : {c->gi1, c->gi2, c->blur, c->gi_spare}) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * 16, st));
+    for (float4 *b : {c->gi1, c->gi2, c->gi_spare}) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * gi_bytes(c), st));
+    HIPCHK(c, hipMemsetAsync(c->blur, 0xFF, nc * 16, st));
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[0], st));
 
@@ -621,7 +655,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
       HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
     }
     if (c->keep_levels)
-      HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], dstGI, (size_t)c->cd.pitch * c->CH * sizeof(float4),
+      HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], dstGI, (size_t)c->cd.pitch * c->CH * gi_bytes(c),
                                hipMemcpyDeviceToDevice, st));
     gi1final = !gi1final;
   }
@@ -853,8 +887,8 @@ int rc2dgi_device_buffer(rc2dgi_ctx *c, int which, void **dev, int *pitch_bytes)
     case RC2DGI_RT_JUMP1: *dev = c->jump1; *pitch_bytes = sp * 4; break;
     case RC2DGI_RT_JUMP2: *dev = c->jump2; *pitch_bytes = sp * 4; break;
     case RC2DGI_RT_DIST: *dev = c->dist; *pitch_bytes = sp * 2; break;
-    case RC2DGI_RT_GI1: *dev = c->gi1; *pitch_bytes = cp * 16; break;
-    case RC2DGI_RT_GI2: *dev = c->gi2; *pitch_bytes = cp * 16; break;
+    case RC2DGI_RT_GI1: *dev = c->gi1; *pitch_bytes = cp * (int)gi_bytes(c); break;
+    case RC2DGI_RT_GI2: *dev = c->gi2; *pitch_bytes = cp * (int)gi_bytes(c); break;
     case RC2DGI_RT_BLUR: *dev = c->blur; *pitch_bytes = cp * 16; break;
     default: return fail(c, RC2DGI_E_ARG, "bad render texture id");
   }
@@ -1026,7 +1060,7 @@ int rc2dgi_set_keep_levels(rc2dgi_ctx *c, int enable) {
   c->keep_levels = enable != 0;
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
-    for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, (size_t)c->cd.pitch * c->CH * sizeof(float4)));
+    for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, (size_t)c->cd.pitch * c->CH * gi_bytes(c)));
   }
   return RC2DGI_OK;
 }
@@ -1041,6 +1075,14 @@ int rc2dgi_download_level(rc2dgi_ctx *c, int level, void *host, int pitch_bytes,
   if (pitch_bytes < row) return fail(c, RC2DGI_E_ARG, "pitch smaller than a row");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->cd.gi_f16) {
+    std::vector<float4> img((size_t)c->CW * c->CH);
+    int rc = fetch_gi(c, c->level_bufs[level], img);
+    if (rc != RC2DGI_OK) return rc;
+    for (int j = 0; j < c->CH; ++j)
+      std::memcpy(static_cast<char *>(host) + (size_t)j * pitch_bytes, img.data() + (size_t)j * c->CW, (size_t)row);
+    return RC2DGI_OK;
+  }
   HIPCHK(c, hipMemcpy2D(host, pitch_bytes, c->level_bufs[level], (size_t)c->cd.pitch * 16, row, c->CH,
                         hipMemcpyDeviceToHost));
   return RC2DGI_OK;
@@ -1071,13 +1113,13 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
     case RC2DGI_RT_COLOR: rc = fetch4(c->frame_done ? c->color_out : c->color_in); break;
     case RC2DGI_RT_EMISSIVE: rc = fetch4(c->emissive); break;
     case RC2DGI_RT_TEMP: rc = fetch4(c->temp); break;
-    case RC2DGI_RT_GI1: rc = fetch4(c->gi1); break;
+    case RC2DGI_RT_GI1: rc = c->cd.gi_f16 ? fetch_gi(c, c->gi1, img) : fetch4(c->gi1); break;
     case RC2DGI_RT_BLUR: rc = fetch4(c->blur); break;
     case RC2DGI_RT_GI2:
       if (n1) {  // giRT2 is never drawn with one cascade: ClearAllRTs content
         for (auto &p : img) p = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
       } else {
-        rc = fetch4(c->gi2);
+        rc = c->cd.gi_f16 ? fetch_gi(c, c->gi2, img) : fetch4(c->gi2);
       }
       break;
     case RC2DGI_RT_JUMP1:

@@ -71,6 +71,57 @@ __device__ __forceinline__ float4 ntload4(const float4 *p) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// ---- storage of the GI cascade textures giRT1 / giRT2 (and their stand-ins)
+// GiF32: RGBA32F (the parity referent).  GiF16: RGBA16F, the format RC2DGI.cs:105-106 names;
+// a store rounds toward zero (what the GL reference implementation, llvmpipe, does -- probed,
+// tests/golden), reads are exact.  v_cvt_pkrtz_f16_f32 is that rounding.
+struct GiF32 {
+  typedef float4 T;
+  static constexpr int kBytes = 16;
+  __device__ static float4 ld(const T *p) { return *p; }
+  __device__ static float4 ldnt(const T *p) {
+    const v4f_t v = __builtin_nontemporal_load(reinterpret_cast<const v4f_t *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  __device__ static void st(T *p, float4 v) { *p = v; }
+  __device__ static float4 round(float4 v) { return v; }
+};
+
+struct GiF16 {
+  typedef uint2 T;
+  static constexpr int kBytes = 8;
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  __device__ static float4 unpack(uint2 u) {
+    const h2_t a = __builtin_bit_cast(h2_t, u.x), b = __builtin_bit_cast(h2_t, u.y);
+    return make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
+  }
+  __device__ static uint2 pack(float4 v) {
+    return make_uint2(__builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v.x, v.y)),
+                      __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v.z, v.w)));
+  }
+  __device__ static float4 ld(const T *p) { return unpack(*p); }
+  __device__ static float4 ldnt(const T *p) {
+    typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
+    const v2u_t v = __builtin_nontemporal_load(reinterpret_cast<const v2u_t *>(p));
+    return unpack(make_uint2(v.x, v.y));
+  }
+  __device__ static void st(T *p, float4 v) { *p = pack(v); }
+  __device__ static float4 round(float4 v) { return unpack(pack(v)); }
+};
+
+// texture(T, (u, v)) with LINEAR filtering on a GI-format texture
+template <class GI>
+__device__ __forceinline__ float4 sample_bilinear_gi(const typename GI::T *__restrict__ T, int pitch, Axis ax, Axis ay,
+                                                     float u, float v) {
+  int x0, x1, y0, y1;
+  float wx, wy;
+  wrap_linear(u, ax, x0, x1, wx);
+  wrap_linear(v, ay, y0, y1, wy);
+  const float4 t00 = GI::ld(&T[(size_t)y0 * pitch + x0]), t10 = GI::ld(&T[(size_t)y0 * pitch + x1]);
+  const float4 t01 = GI::ld(&T[(size_t)y1 * pitch + x0]), t11 = GI::ld(&T[(size_t)y1 * pitch + x1]);
+  return lerp_gl(lerp_gl(t00, t10, wx), lerp_gl(t01, t11, wx), wy);
+}
+
 // blend-on-store (SRC_ALPHA, ONE_MINUS_SRC_ALPHA, FUNC_ADD on all four channels)
 __device__ __forceinline__ float4 blend(float4 src, float4 dst) {
   const float a = src.w, ia = 1.0f - a;

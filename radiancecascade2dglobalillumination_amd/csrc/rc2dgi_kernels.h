@@ -28,6 +28,7 @@ struct CascadeDims {
   int CW, CH;
   int pitch;
   int powW, powH;
+  int gi_f16;  // giRT1 / giRT2 (and their stand-ins) stored as RGBA16F (RC2DGI_STORAGE_F16)
 };
 
 // ScreenUV (shaders/ScreenUV.fs) as a 1-bit occupancy mask (row pitch mpitch 32-bit words)

@@ -330,9 +330,10 @@ __device__ __forceinline__ int cvt_floor(float x) {
 // rolled (1) the VALU-bound low levels (no SGPR spills, occupancy 8).
 // TILED: `dist` is the 8x8-tiled copy (k_dist_tile): one 128-byte line holds an 8x8 texel tile,
 // so the nearly parallel rays of a lane (and vertical-ish steps) share lines.
-template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, bool TILED>
-__global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *__restrict__ upper,
-                                                     float4 *__restrict__ out,
+// GI: storage of the cascade textures (GiF32 / GiF16, rc2dgi_device.h).
+template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, bool TILED, class GI>
+__global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
+                                                     typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
                                                      const float4 *__restrict__ color,
                                                      const float4 *__restrict__ emis,
@@ -359,8 +360,10 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
   // upper block of angleIndex a = 4*bi + r: (a mod 2b, a div 2b) in blocks of (bdx/2, bdy/2)
   const int ubx = P.bdx >> 1, uby = P.bdy >> 1;
   const int umask = 2 * P.bsc - 1, ushift = P.level + 1;
-  // staged texels as plain float components (HIP's float4 union defeats SROA -> scratch)
-  float stx[TOP ? 1 : PT], sty[TOP ? 1 : PT], stz[TOP ? 1 : PT], stw[TOP ? 1 : PT];
+  // staged texels as plain 32-bit components (HIP's vector unions defeat SROA -> scratch); raw
+  // storage bits, converted when written to LDS after the march
+  constexpr bool F16 = GI::kBytes == 8;
+  unsigned stx[TOP ? 1 : PT], sty[TOP ? 1 : PT], stz[(TOP || F16) ? 1 : PT], stw[(TOP || F16) ? 1 : PT];
   if (!TOP) {
 #pragma unroll
     for (int q = 0; q < PT; ++q) {
@@ -373,11 +376,16 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       int gy = (a >> ushift) * uby + (cy0 >> 1) - 1 + yy;
       gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
       gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
-      const float4 v = upper[(size_t)gy * P.c.pitch + gx];  // issued now, consumed after the march
-      stx[q] = v.x;
-      sty[q] = v.y;
-      stz[q] = v.z;
-      stw[q] = v.w;
+      const typename GI::T v = upper[(size_t)gy * P.c.pitch + gx];  // issued now, consumed after the march
+      if constexpr (F16) {
+        stx[q] = v.x;
+        sty[q] = v.y;
+      } else {
+        stx[q] = __float_as_uint(v.x);
+        sty[q] = __float_as_uint(v.y);
+        stz[q] = __float_as_uint(v.z);
+        stw[q] = __float_as_uint(v.w);
+      }
     }
   }
 
@@ -481,7 +489,13 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
 #pragma unroll
     for (int q = 0; q < PT; ++q) {
       const int k = (int)threadIdx.x + q * NT;
-      if (k < NSTAGE) s_up[k] = make_float4(stx[q], sty[q], stz[q], stw[q]);
+      if (k < NSTAGE) {
+        if constexpr (F16)
+          s_up[k] = GiF16::unpack(make_uint2(stx[q], sty[q]));
+        else
+          s_up[k] = make_float4(__uint_as_float(stx[q]), __uint_as_float(sty[q]), __uint_as_float(stz[q]),
+                                __uint_as_float(stw[q]));
+      }
     }
     __syncthreads();
   }
@@ -563,10 +577,10 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
               } else {
                 // rounding stepped outside the staged footprint: read HBM.  Non-temporal loads
                 // keep the compiler from fusing this path with the LDS path into flat loads.
-                t00 = ntload4(&upper[(size_t)y0 * P.c.pitch + x0]);
-                t10 = ntload4(&upper[(size_t)y0 * P.c.pitch + x1]);
-                t01 = ntload4(&upper[(size_t)y1 * P.c.pitch + x0]);
-                t11 = ntload4(&upper[(size_t)y1 * P.c.pitch + x1]);
+                t00 = GI::ldnt(&upper[(size_t)y0 * P.c.pitch + x0]);
+                t10 = GI::ldnt(&upper[(size_t)y0 * P.c.pitch + x1]);
+                t01 = GI::ldnt(&upper[(size_t)y1 * P.c.pitch + x0]);
+                t11 = GI::ldnt(&upper[(size_t)y1 * P.c.pitch + x1]);
               }
             }
             const float4 up = lerp_gl(lerp_gl(t00, t10, ux), lerp_gl(t01, t11, ux), uy);
@@ -588,7 +602,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const float4 *_
       }
       const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
       const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
-      out[(size_t)j * P.c.pitch + i] = blend_over_black(acc);
+      GI::st(&out[(size_t)j * P.c.pitch + i], blend_over_black(acc));
     }
   }
 }
@@ -607,7 +621,8 @@ __global__ __launch_bounds__(256) void k_dist_tile(const unsigned short *__restr
 }
 
 // ---------------------------------------------------------------- Blur + copy-back
-__global__ __launch_bounds__(256) void k_blur(const float4 *__restrict__ gi, float4 *__restrict__ blur_out,
+template <class GI>
+__global__ __launch_bounds__(256) void k_blur(const typename GI::T *__restrict__ gi, float4 *__restrict__ blur_out,
                                               CascadeDims c, float radius, int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
@@ -627,7 +642,7 @@ __global__ __launch_bounds__(256) void k_blur(const float4 *__restrict__ gi, flo
       sv = v + (ky[k] * tsy) * radius;
       w = k < 4 ? 0.0625f : 0.125f;
     }
-    const float4 t = sample_bilinear(gi, c.pitch, ax, ay, su, sv);
+    const float4 t = sample_bilinear_gi<GI>(gi, c.pitch, ax, ay, su, sv);
     res.x = res.x + t.x * w;
     res.y = res.y + t.y * w;
     res.z = res.z + t.z * w;
@@ -641,9 +656,10 @@ __global__ __launch_bounds__(256) void k_blur(const float4 *__restrict__ gi, flo
 // (x = (i+0.5)/n*n - 0.5 = i, weight 0: fma(0, b - a, a) = a), so each texel needs only its
 // own blur value.  G_0 is staged in LDS: a 64 x 16 core plus an H-texel halo covers every
 // bilinear tap of radius <= H - 2 (taps that ever fall outside are read from HBM).
-template <int H>
-__global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ gi_in, float4 *__restrict__ blur_out,
-                                                    float4 *__restrict__ gi_out, CascadeDims c, float radius,
+template <int H, class GI>
+__global__ __launch_bounds__(256) void k_blur_fused(const typename GI::T *__restrict__ gi_in,
+                                                    float4 *__restrict__ blur_out, typename GI::T *__restrict__ gi_out,
+                                                    CascadeDims c, float radius,
                                                     int tile0) {
   constexpr int TW = 64 + 2 * H, TH = 16 + 2 * H;
   __shared__ float4 tile[TH * TW];
@@ -652,7 +668,7 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ g
   for (int k = threadIdx.x; k < TW * TH; k += 256) {
     const int ty = k / TW, tx = k - ty * TW;
     const int gx = (x0 + tx) & (c.CW - 1), gy = (y0 + ty) & (c.CH - 1);
-    tile[k] = gi_in[(size_t)gy * c.pitch + gx];
+    tile[k] = GI::ld(&gi_in[(size_t)gy * c.pitch + gx]);
   }
   __syncthreads();
   const Axis ax{c.CW, 1}, ay{c.CH, 1};
@@ -703,7 +719,7 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ g
         t11 = tile[yb[qy] * TW + xb[qx]];
       } else {  // a tap beyond the staged halo: global coordinates are tile-local + origin
         auto g = [&](int ly, int lx) {
-          return ntload4(&gi_in[(size_t)((ly + y0) & (c.CH - 1)) * c.pitch + ((lx + x0) & (c.CW - 1))]);
+          return GI::ldnt(&gi_in[(size_t)((ly + y0) & (c.CH - 1)) * c.pitch + ((lx + x0) & (c.CW - 1))]);
         };
         t00 = g(ya[qy], xa[qx]);
         t10 = g(ya[qy], xb[qx]);
@@ -720,7 +736,7 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ g
     const float4 b = blend_over_black(res);  // cascadeBlurRT cleared to (0,0,0,1)
     const size_t o = (size_t)j * c.pitch + i;
     blur_out[o] = b;
-    gi_out[o] = blend(b, tile[(j - y0) * TW + (i - x0)]);  // copy-back onto finalGI, blended
+    GI::st(&gi_out[o], blend(b, tile[(j - y0) * TW + (i - x0)]));  // copy-back onto finalGI, blended
   }
 }
 
@@ -735,9 +751,10 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float4 *__restrict__ g
 // finite values (fma(0, b - a, a) = a) and are skipped.  With MERGE (screen == cascade size) the
 // merge's LINEAR sample of finalGI lands exactly on the texel as well (same argument), so
 // merge.fs runs on the blended GI value held in registers.
-template <int F, bool MERGE>
-__global__ __launch_bounds__(256) void k_blur_rows(const float4 *__restrict__ gi_in, float4 *__restrict__ blur_out,
-                                                   float4 *__restrict__ gi_out, CascadeDims c, BlurTaps bt,
+template <int F, bool MERGE, class GI>
+__global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restrict__ gi_in,
+                                                   float4 *__restrict__ blur_out, typename GI::T *__restrict__ gi_out,
+                                                   CascadeDims c, BlurTaps bt,
                                                    const float4 *__restrict__ color_in, float4 *__restrict__ temp,
                                                    float4 *__restrict__ color_out, int spitch, int tile0) {
   constexpr int HALO = F + 1, TW = 64 + 2 * HALO, TH = 32 + 2 * HALO, NR = 8 + 2 * HALO;
@@ -747,7 +764,7 @@ __global__ __launch_bounds__(256) void k_blur_rows(const float4 *__restrict__ gi
   for (int k = threadIdx.x; k < TW * TH; k += 256) {
     const int ty = k / TW, tx = k - ty * TW;
     const int gx = (x0 + tx) & (c.CW - 1), gy = (y0 + ty) & (c.CH - 1);
-    tile[k] = gi_in[(size_t)gy * c.pitch + gx];
+    tile[k] = GI::ld(&gi_in[(size_t)gy * c.pitch + gx]);
   }
   __syncthreads();
   const int lx = (threadIdx.x & 63) + HALO;  // tile column of this thread's texel
@@ -793,11 +810,11 @@ __global__ __launch_bounds__(256) void k_blur_rows(const float4 *__restrict__ gi
       res.w = res.w + tp.w * w;
     }
     const float4 b = blend_over_black(res);  // cascadeBlurRT cleared to (0,0,0,1)
-    const float4 g = blend(b, h[m][1]);      // copy-back onto finalGI, blended
+    const float4 g = GI::round(blend(b, h[m][1]));  // copy-back onto finalGI, blended (as stored)
     const int j = by * 32 + r0 + t;
     const size_t o = (size_t)j * c.pitch + i;
     blur_out[o] = b;
-    gi_out[o] = g;
+    GI::st(&gi_out[o], g);
     if constexpr (MERGE) {  // merge.fs:10-15 + tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
       const size_t so = (size_t)j * spitch + i;
       const float4 col = color_in[so];
@@ -810,7 +827,8 @@ __global__ __launch_bounds__(256) void k_blur_rows(const float4 *__restrict__ gi
   }
 }
 
-__global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict__ blur, float4 *__restrict__ gi,
+template <class GI>
+__global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict__ blur, typename GI::T *__restrict__ gi,
                                                        CascadeDims c, int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
@@ -818,11 +836,12 @@ __global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict_
   const float u = texcoord(i, Axis{c.CW, c.powW}), v = texcoord(j, Axis{c.CH, c.powH});
   const float4 s = sample_bilinear(blur, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
   const size_t o = (size_t)j * c.pitch + i;
-  gi[o] = blend(s, gi[o]);
+  GI::st(&gi[o], blend(s, GI::ld(&gi[o])));
 }
 
 // ---------------------------------------------------------------- Merge + copy-back
-__global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_in, const float4 *__restrict__ gi,
+template <class GI>
+__global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_in, const typename GI::T *__restrict__ gi,
                                                float4 *__restrict__ temp, float4 *__restrict__ color_out,
                                                ScreenDims s, CascadeDims c, int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -831,7 +850,7 @@ __global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_
   const float u = texcoord(i, Axis{s.W, s.powW}), v = texcoord(j, Axis{s.H, s.powH});
   const size_t o = (size_t)j * s.pitch + i;
   const float4 col = color_in[o];
-  const float4 g = sample_bilinear(gi, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
+  const float4 g = sample_bilinear_gi<GI>(gi, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
   const float4 src = make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
   const float4 t = blend_over_black(src);  // tempRT as cleared by ClearAllRTs
   temp[o] = t;
@@ -954,7 +973,7 @@ static const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles
   return e.dev;
 }
 
-template <int TX, int TY, int PY, int PD = 1, int UNR = 1, bool TILED = false>
+template <int TX, int TY, int PY, int PD = 1, int UNR = 1, bool TILED = false, class GI = GiF32>
 static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   P.tiles_x = ceil_div(P.bdx, TX);
   const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
@@ -974,8 +993,9 @@ static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t 
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
 #define RC2DGI_RC(TOPV, P2V)                                                                                      \
-  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, TILED>), dim3(nwg), dim3(TX * TY), 0, st, P,      \
-                     a.upper, a.out, TILED ? a.dist_tiled : a.dist, a.color, a.emissive, a.dirs, a.sky)
+  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, TILED, GI>), dim3(nwg), dim3(TX * TY), 0, st, P,  \
+                     reinterpret_cast<const typename GI::T *>(a.upper), reinterpret_cast<typename GI::T *>(a.out),   \
+                     TILED ? a.dist_tiled : a.dist, a.color, a.emissive, a.dirs, a.sky)
   const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
   const bool top = a.level == a.N - 1;
   if (top) {
@@ -1026,6 +1046,16 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.reflectivity = a.reflectivity;
   const int nblk = P.bsc * P.bsc;
   hipError_t e = hipSuccess;
+  if (c.gi_f16) {  // RGBA16F cascades: the 16x16x1 family only
+    switch (a.variant) {
+      case 13: e = launch_rc_tiles<16, 16, 1, 1, 32, false, GiF16>(a, P, st); break;
+      case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, true, GiF16>(a, P, st); break;
+      case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, true, GiF16>(a, P, st); break;
+      default: e = launch_rc_tiles<16, 16, 1, 1, 1, false, GiF16>(a, P, st); break;
+    }
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
+  }
   switch (a.variant) {
     case 1: e = launch_rc_tiles<16, 8, 2>(a, P, st); break;
     case 2: e = launch_rc_tiles<16, 16, 2>(a, P, st); break;
@@ -1057,7 +1087,12 @@ hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float 
                        int row1) {
   clamp_rows(c.CH, row0, row1);
   if (row0 >= row1) return hipSuccess;
-  hipLaunchKernelGGL(k_blur, grid2d(c.CW, row1 - row0), dim3(256), 0, st, gi, blur_out, c, radius, row0, row1);
+  if (c.gi_f16)
+    hipLaunchKernelGGL(k_blur<GiF16>, grid2d(c.CW, row1 - row0), dim3(256), 0, st,
+                       reinterpret_cast<const GiF16::T *>(gi), blur_out, c, radius, row0, row1);
+  else
+    hipLaunchKernelGGL(k_blur<GiF32>, grid2d(c.CW, row1 - row0), dim3(256), 0, st, gi, blur_out, c, radius, row0,
+                       row1);
   return hipGetLastError();
 }
 
@@ -1072,10 +1107,19 @@ bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Ca
   if (row0 >= row1) return true;
   const int t0 = row0 / 16, t1 = ceil_div(row1, 16);  // whole 16-row tiles
   const dim3 grid(ceil_div(c.CW, 64), t1 - t0);
-  if (radius <= 2.0f)
-    hipLaunchKernelGGL(k_blur_fused<4>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius, t0);
-  else if (radius <= 6.0f)
-    hipLaunchKernelGGL(k_blur_fused<8>, grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius, t0);
+  const auto *g16i = reinterpret_cast<const GiF16::T *>(gi_in);
+  auto *g16o = reinterpret_cast<GiF16::T *>(gi_out);
+  if (radius <= 2.0f) {
+    if (c.gi_f16)
+      hipLaunchKernelGGL((k_blur_fused<4, GiF16>), grid, dim3(256), 0, st, g16i, blur_out, g16o, c, radius, t0);
+    else
+      hipLaunchKernelGGL((k_blur_fused<4, GiF32>), grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius, t0);
+  } else if (radius <= 6.0f) {
+    if (c.gi_f16)
+      hipLaunchKernelGGL((k_blur_fused<8, GiF16>), grid, dim3(256), 0, st, g16i, blur_out, g16o, c, radius, t0);
+    else
+      hipLaunchKernelGGL((k_blur_fused<8, GiF32>), grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, radius, t0);
+  }
   else
     return false;
   return true;
@@ -1104,8 +1148,15 @@ bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Cas
   const int t0 = row0 / 32, t1 = ceil_div(row1, 32);  // whole 32-row tiles
   const dim3 grid(c.CW / 64, t1 - t0);
 #define RC2DGI_BLUR_ROWS(FV, MV)                                                                               \
-  hipLaunchKernelGGL((k_blur_rows<FV, MV>), grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, bt, color_in, \
-                     temp, color_out, s.pitch, t0)
+  do {                                                                                                         \
+    if (c.gi_f16)                                                                                              \
+      hipLaunchKernelGGL((k_blur_rows<FV, MV, GiF16>), grid, dim3(256), 0, st,                                 \
+                         reinterpret_cast<const GiF16::T *>(gi_in), blur_out, reinterpret_cast<GiF16::T *>(gi_out), \
+                         c, bt, color_in, temp, color_out, s.pitch, t0);                                        \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_blur_rows<FV, MV, GiF32>), grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, bt,  \
+                         color_in, temp, color_out, s.pitch, t0);                                               \
+  } while (0)
   if (merge) {
     if (F == 0) RC2DGI_BLUR_ROWS(0, true); else if (F == 1) RC2DGI_BLUR_ROWS(1, true); else RC2DGI_BLUR_ROWS(2, true);
   } else {
@@ -1118,7 +1169,11 @@ bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Cas
 hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st, int row0, int row1) {
   clamp_rows(c.CH, row0, row1);
   if (row0 >= row1) return hipSuccess;
-  hipLaunchKernelGGL(k_blur_copyback, grid2d(c.CW, row1 - row0), dim3(256), 0, st, blur, gi, c, row0, row1);
+  if (c.gi_f16)
+    hipLaunchKernelGGL(k_blur_copyback<GiF16>, grid2d(c.CW, row1 - row0), dim3(256), 0, st, blur,
+                       reinterpret_cast<GiF16::T *>(gi), c, row0, row1);
+  else
+    hipLaunchKernelGGL(k_blur_copyback<GiF32>, grid2d(c.CW, row1 - row0), dim3(256), 0, st, blur, gi, c, row0, row1);
   return hipGetLastError();
 }
 
@@ -1126,8 +1181,12 @@ hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, 
                         CascadeDims c, hipStream_t st, int row0, int row1) {
   clamp_rows(s.H, row0, row1);
   if (row0 >= row1) return hipSuccess;
-  hipLaunchKernelGGL(k_merge, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in, gi, temp, color_out, s, c,
-                     row0, row1);
+  if (c.gi_f16)
+    hipLaunchKernelGGL(k_merge<GiF16>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in,
+                       reinterpret_cast<const GiF16::T *>(gi), temp, color_out, s, c, row0, row1);
+  else
+    hipLaunchKernelGGL(k_merge<GiF32>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in, gi, temp, color_out, s,
+                       c, row0, row1);
   return hipGetLastError();
 }
 

@@ -127,9 +127,11 @@ class RC2DGI:
     """One GI context = the reference's render-texture set + DoRC2DGI() on one GPU."""
 
     def __init__(self, screen_width: int = 1200, screen_height: int = 900, cascade_count: int = 6,
-                 render_scale: float = 1.0, ray_range: float = 2.0, device: int = 0):
+                 render_scale: float = 1.0, ray_range: float = 2.0, device: int = 0, storage: str = "f32"):
+        """storage: "f32" (RGBA32F render textures) or "f16" (giRT1/2 as RGBA16F, RC2DGI.cs:105-106)."""
         self._L = load_library()
-        cfg = _Config(screen_width, screen_height, cascade_count, render_scale, ray_range, 0, device,
+        st = {"f32": 0, "rgba8": 1, "f16": 2}[storage]
+        cfg = _Config(screen_width, screen_height, cascade_count, render_scale, ray_range, st, device,
                       (ctypes.c_int * 5)())
         h = ctypes.c_void_p()
         rc = self._L.rc2dgi_create(ctypes.byref(cfg), ctypes.byref(h))
@@ -139,6 +141,7 @@ class RC2DGI:
         self.screen_width, self.screen_height = screen_width, screen_height
         self.render_scale = render_scale
         self.device = device
+        self.storage = storage
         self._N = cascade_count
 
     # ---------------------------------------------------------------- lifetime

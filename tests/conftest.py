@@ -32,7 +32,8 @@ def params_of(m: dict):
     return oracle.Params(W=m["W"], H=m["H"], N=m["N"], render_scale=m["render_scale"], ray_range=m["ray_range"],
                          sky_radiance=m["sky_radiance"], sky_color=tuple(m["sky_color"]),
                          sun_color=tuple(m["sun_color"]), sun_angle=m["sun_angle"],
-                         reflectivity=m["reflectivity"], blur_radius=m["blur_radius"])
+                         reflectivity=m["reflectivity"], blur_radius=m["blur_radius"],
+                         gi_f16=bool(m.get("gi_f16", False)))
 
 
 def rel_err(got: np.ndarray, want: np.ndarray, floor: float = 1e-3) -> np.ndarray:

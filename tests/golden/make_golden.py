@@ -46,6 +46,10 @@ FIXTURES = [
     ("rand96x64_n2_noblur", 96, 64, 2, 4.0, "rand:2", dict(blur_radius=0.0, sky_radiance=2.0), True),
     ("rand64x128_n4", 64, 128, 4, 2.0, "rand:3", dict(sky_color=(0.2, 0.9, 0.4), blur_radius=2.5), True),
     ("empty64_n3", 64, 64, 3, 2.0, "empty", {}, True),
+    # giRT1/2 as RGBA16F (RC2DGI.cs:105-106; rc2dgi RC2DGI_STORAGE_F16)
+    ("c0_demo_256_f16", 256, 256, 2, 8.0, "demo", dict(gi_f16=True), False),
+    ("rand128_n4_f16", 128, 128, 4, 2.0, "rand:4", dict(gi_f16=True, blur_radius=2.5), False),
+    ("rand96x64_n3_f16", 96, 64, 3, 4.0, "rand:5", dict(gi_f16=True), False),
 ]
 
 
@@ -62,6 +66,7 @@ def make_scene(spec: str, W: int, H: int):
 def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
     u = dict(DEFAULT_UNIFORMS)
     u.update(over)
+    gi_f16 = bool(u.pop("gi_f16", False))
     color, emis = make_scene(scene, W, H)
     with tempfile.TemporaryDirectory() as d:
         color.tofile(os.path.join(d, "c.f32"))
@@ -71,7 +76,8 @@ def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
                  "--reflectivity", str(u["reflectivity"]), "--blur-radius", str(u["blur_radius"])]
         base = ["--w", str(W), "--h", str(H), "--n", str(N), "--out", d]
         subprocess.run([GLREF, "--ref-shaders", shaders, "--ray-range", str(rr), "--in-color", d + "/c.f32",
-                        "--in-emissive", d + "/e.f32", "--dump", "all"] + base + uargs, check=True)
+                        "--in-emissive", d + "/e.f32", "--dump", "all"] + base + uargs + (["--gi-f16"] if gi_f16 else []),
+                       check=True)
         subprocess.run([GLREF, "--capture-tables"] + base + uargs, check=True)
         meta = json.load(open(os.path.join(d, "glref.json")))
         CW, CH = meta["CW"], meta["CH"]
@@ -94,7 +100,7 @@ def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
     entry = dict(name=name, W=W, H=H, N=N, ray_range=rr, render_scale=1.0, scene=scene, CW=CW, CH=CH,
                  jfa_steps=meta["jfa_steps"], final_gi=meta["final_gi"], renderer=meta["renderer"],
-                 gl_version=meta["version"], mode=meta["mode"], **u)
+                 gl_version=meta["version"], mode=meta["mode"], gi_f16=gi_f16, **u)
     entry["sky_color"] = list(u["sky_color"])
     entry["sun_color"] = list(u["sun_color"])
     return entry
@@ -103,10 +109,15 @@ def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref-shaders", default="/root/reference/shaders")
+    ap.add_argument("--only", nargs="*", help="regenerate these fixtures only (the manifest keeps the others)")
     a = ap.parse_args()
     if not os.path.exists(GLREF):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    manifest = [run(*f, shaders=a.ref_shaders) for f in FIXTURES]
+    old = {}
+    mpath = os.path.join(HERE, "manifest.json")
+    if a.only and os.path.exists(mpath):
+        old = {m["name"]: m for m in json.load(open(mpath))}
+    manifest = [run(*f, shaders=a.ref_shaders) if (not a.only or f[0] in a.only) else old[f[0]] for f in FIXTURES]
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     for m in manifest:

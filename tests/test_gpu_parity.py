@@ -44,7 +44,8 @@ def set_uniforms(ctx, p):
 
 
 def run_hip(RC2DGI, p, color, emis, dir_tabs=None, sky=None, keep_levels=False):
-    ctx = RC2DGI(p.W, p.H, cascade_count=p.N, render_scale=p.render_scale, ray_range=p.ray_range)
+    ctx = RC2DGI(p.W, p.H, cascade_count=p.N, render_scale=p.render_scale, ray_range=p.ray_range,
+                 storage="f16" if p.gi_f16 else "f32")
     set_uniforms(ctx, p)
     if dir_tabs is not None:
         off = 0
@@ -142,6 +143,10 @@ CONFIGS = [
     (128, 64, 4, 64.0, 1.0, dict(blur_radius=5.0, sun_angle=3.0), "rand:18"),
     (512, 512, 8, 64.0, 1.0, {}, "rand:19"),       # C2-style knobs, top levels start off-screen
     (300, 300, 6, 2.0, 1.0, dict(sky_radiance=0.0), "empty"),
+    # giRT1/2 as RGBA16F (RC2DGI_STORAGE_F16)
+    (256, 256, 5, 3.0, 1.0, dict(gi_f16=True), "demo"),
+    (333, 200, 4, 2.0, 0.5, dict(gi_f16=True, blur_radius=1.37), "rand:41"),
+    (128, 128, 3, 2.0, 1.0, dict(gi_f16=True, blur_radius=0.0, reflectivity=0.7), "rand:42"),
 ]
 
 
@@ -326,15 +331,18 @@ def test_timing_reports_passes(RC2DGI):
 
 @pytest.mark.parametrize("W,H,N,rr,scene", [(256, 192, 5, 2.0, "rand:40"), (333, 200, 4, 8.0, "demo"),
                                             (512, 512, 6, 2.0, "demo")])
-def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene):
+@pytest.mark.parametrize("storage", ["f32", "f16"])
+def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene, storage):
     """The tile-shape tuning knob changes the schedule only, never a result."""
     color, emis = make_scene(scene, W, H)
-    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr), color, emis, keep_levels=True)
-    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
+    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr, gi_f16=storage == "f16"), color, emis,
+                      keep_levels=True)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr, storage=storage)
     ctx.set_keep_levels(True)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
-    for v in range(ctx.get_tuning("rc_variant_count")):
+    variants = range(ctx.get_tuning("rc_variant_count")) if storage == "f32" else (0, 13, 14, 15)
+    for v in variants:
         ctx.set_tuning("rc_variant", v)
         ctx.do_rc2dgi()
         ctx.sync()
@@ -355,12 +363,13 @@ def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene):
     (256, 256, 0.5, 1.5),    # cascade 128^2 != screen: fixed taps, separate merge
     (200, 120, 1.0, 1.5),    # non-power-of-two: separate passes only
 ])
-def test_every_blur_path_matches_oracle(RC2DGI, W, H, rs, radius):
+@pytest.mark.parametrize("storage", ["f32", "f16"])
+def test_every_blur_path_matches_oracle(RC2DGI, W, H, rs, radius, storage):
     """blur_path 0 (fixed taps + fused merge), 1 (LDS tile), 2 (separate passes): same bits."""
-    p = oracle.Params(W=W, H=H, N=3, ray_range=4.0, render_scale=rs, blur_radius=radius)
+    p = oracle.Params(W=W, H=H, N=3, ray_range=4.0, render_scale=rs, blur_radius=radius, gi_f16=storage == "f16")
     color, emis = make_scene("rand:51", W, H)
     fr = oracle_dict(oracle.frame(p, color, emis))
-    ctx = RC2DGI(W, H, cascade_count=3, render_scale=rs, ray_range=4.0)
+    ctx = RC2DGI(W, H, cascade_count=3, render_scale=rs, ray_range=4.0, storage=storage)
     set_uniforms(ctx, p)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)

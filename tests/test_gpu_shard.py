@@ -123,3 +123,28 @@ def test_phase_api_matches_do(R):
     c.sync()
     assert np.array_equal(c.download("color"), want["color"])
     c.close()
+
+
+def test_group_shards_f16_storage(R):
+    """RGBA16F cascades (RC2DGI_STORAGE_F16) shard the same way, bit for bit."""
+    W, H, N = 512, 384, 5
+    color, emis = _scene("rand:26", W, H)
+    whole = R.RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage="f16")
+    whole.frame(color, emis)
+    whole.sync()
+    want = whole.download("color")
+    whole.close()
+    ctxs = []
+    for k in range(3):
+        c = R.RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage="f16")
+        c.set_shard(k, 3)
+        c.set_tuning("poison", 1)
+        c.upload("color", color)
+        c.upload("emissive", emis)
+        ctxs.append(c)
+    R.do_group(ctxs)
+    for c in ctxs:
+        c.sync()
+        y0, y1 = c.shard_rows()
+        assert np.array_equal(c.download("color")[y0:y1], want[y0:y1])
+        c.close()
