@@ -31,10 +31,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
-def b_rc(W, H, CW, CH, N):
+def b_rc(W, H, CW, CH, N, gi_bytes=16):
     """Algorithmic bytes of one RC pass: write G_L, read G_{L+1} once,
-    read the distance field once per level."""
-    return 16 * CW * CH * (2 * N - 1) + 4 * W * H * N
+    read the distance field once per level (gi_bytes = 8 with RGBA16F cascades)."""
+    return gi_bytes * CW * CH * (2 * N - 1) + 4 * W * H * N
 
 
 def cpu_baseline(W, H, N, rr, budget_s=12.0):
@@ -276,6 +276,8 @@ def main():
                     help="scenes per GPU, one context + stream each (BASELINE configs[4] batch mode)")
     ap.add_argument("--mode", default="replicas", choices=("replicas", "strips"),
                     help="strips: one frame split into row strips over the ranks (BASELINE configs[3])")
+    ap.add_argument("--storage", default="f32", choices=("f32", "f16"),
+                    help="f16: giRT1/2 as RGBA16F (RC2DGI.cs:105-106, SURVEY 8 f4)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="keep the default RC workgroup order (setup otherwise times the candidates per level)")
     ap.add_argument("--save-tuning", default="", help="write the chosen per-level rc_order / rc_variant (JSON)")
@@ -305,7 +307,7 @@ def main():
         color, emis = scenes.demo(W, H, t=3.0 + 0.25 * rank)  # one independent scene per rank
     else:
         color, emis = scenes.random_scene(W, H, seed=int(a.scene.split(":")[1]) + rank)
-    ctx = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local, storage=a.storage)
     CW, CH = ctx.cascade_resolution
     # inputs resident in HBM before the timed region
     ctx.upload("color", color)
@@ -349,7 +351,7 @@ def main():
     t_rc, t_tot, wall = rdist.max_over_ranks([sum(rc_ms), sum(tot_ms), wall], device="cuda")
     units = CW * CH * N * a.steps * world
     value = units / (t_rc / 1e3) / 1e6
-    bytes_launch = b_rc(W, H, CW, CH, N) / N
+    bytes_launch = b_rc(W, H, CW, CH, N, 8 if a.storage == "f16" else 16) / N
     avg_launch_s = (t_rc / 1e3) / (a.steps * N)
     achieved = bytes_launch / avg_launch_s / 1e9
     traffic = None
@@ -357,7 +359,7 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
-        if rec.get("config") == f"{W}x{H}_N{N}":
+        if rec.get("config") == f"{W}x{H}_N{N}" and a.storage == "f32":
             traffic = rec.get("hbm_bytes_per_launch")
     line = {
         "metric": (f"Mpixel*cascades/s (RC pass) at {W}^2, cascadeCount={N}" if W == H else
@@ -371,7 +373,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if a.storage == "f32" else "f32 (RGBA16F cascade storage)",
         "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
         "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}", "screen": [W, H],
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
