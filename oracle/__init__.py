@@ -35,6 +35,7 @@ class _Cfg(ctypes.Structure):
         ("sky_radiance", ctypes.c_float), ("sky_color", ctypes.c_float * 3),
         ("sun_color", ctypes.c_float * 3), ("sun_angle", ctypes.c_float),
         ("reflectivity", ctypes.c_float), ("blur_radius", ctypes.c_float), ("gi_f16", ctypes.c_int),
+        ("rgba8", ctypes.c_int),
     ]
 
 
@@ -83,6 +84,7 @@ def lib():
                                 _f32p]
         L.orc_set_rows.argtypes = [ctypes.c_int, ctypes.c_int]
         L.orc_set_gi_f16.argtypes = [ctypes.c_int]
+        L.orc_set_rgba8.argtypes = [ctypes.c_int]
         L.orc_half_rtz.argtypes = [ctypes.c_float]
         L.orc_half_rtz.restype = ctypes.c_float
         L.orc_num_threads.restype = ctypes.c_int
@@ -106,11 +108,26 @@ class Params:
     reflectivity: float = 0.0
     blur_radius: float = 1.5
     gi_f16: bool = False  # giRT1/2 stored as RGBA16F (RC2DGI.cs:105-106)
+    rgba8: bool = False   # every render texture RGBA8 (the literal app): texels k*(1/255)
 
     def c(self) -> _Cfg:
         return _Cfg(self.W, self.H, self.N, self.render_scale, self.ray_range, self.sky_radiance,
                     (ctypes.c_float * 3)(*self.sky_color), (ctypes.c_float * 3)(*self.sun_color),
-                    self.sun_angle, self.reflectivity, self.blur_radius, int(self.gi_f16))
+                    self.sun_angle, self.reflectivity, self.blur_radius, int(self.gi_f16),
+                    int(self.rgba8))
+
+
+INV255 = np.float32(1.0) / np.float32(255.0)
+
+
+def from_u8(a: np.ndarray) -> np.ndarray:
+    """RGBA8 texels -> the floats a unorm8 fetch returns on llvmpipe: k * (1/255) (f32 multiply)."""
+    return np.ascontiguousarray(np.asarray(a, np.uint8).astype(np.float32) * INV255)
+
+
+def to_u8(a: np.ndarray) -> np.ndarray:
+    """Floats k * (1/255) (an rgba8-mode frame's render textures) -> the texels k."""
+    return np.rint(np.asarray(a, np.float32) * np.float32(255.0)).astype(np.uint8)
 
 
 def _p(a):
@@ -165,6 +182,9 @@ def frame(p: Params, color: np.ndarray, emissive: np.ndarray, tc_screen=None, tc
     """One ClearAllRTs + DoRC2DGI() frame on the CPU restatement."""
     CW, CH, _ = dims(p)
     W, H = p.W, p.H
+    if p.rgba8:  # uint8 texels, or floats quantized the way a float upload to RGBA8 is
+        q = lambda a: a if a.dtype == np.uint8 else np.rint(np.clip(a, 0, 1) * 255).astype(np.uint8)  # noqa
+        color, emissive = from_u8(q(np.asarray(color))), from_u8(q(np.asarray(emissive)))
     color = np.ascontiguousarray(color, np.float32)
     emissive = np.ascontiguousarray(emissive, np.float32)
     assert color.shape == (H, W, 4) and emissive.shape == (H, W, 4)
@@ -198,6 +218,19 @@ def rc_level(p: Params, level: int, upper, color, emissive, dist, out, dir_table
 
 def _c(a):
     return np.ascontiguousarray(a, np.float32)
+
+
+class rgba8_textures:
+    """``with oracle.rgba8_textures():`` -- the per-pass functions below treat every render
+    texture as RGBA8 (8-bit blends, 8.8 fixed-point LINEAR filtering; texels k*(1/255))."""
+
+    def __enter__(self):
+        lib().orc_set_rgba8(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_rgba8(0)
+        return False
 
 
 def screen_uv(color, tc=None):

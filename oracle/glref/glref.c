@@ -358,8 +358,23 @@ static float *read_rt(RT rt) {
 }
 
 static const char *g_out = ".";
+static int g_dump_u8 = 0; /* --dump-u8: rgba8 render textures are dumped as raw bytes (<name>.u8) */
 
 static void dump_rt(RT rt, const char *name) {
+  if (g_dump_u8 && g_rgba8) {
+    unsigned char *b = (unsigned char *)malloc((size_t)rt.w * rt.h * 4);
+    p_glBindFramebuffer(GL_FRAMEBUFFER, rt.fbo);
+    p_glPixelStorei(GL_PACK_ALIGNMENT, 1);
+    p_glReadPixels(0, 0, rt.w, rt.h, GL_RGBA, GL_UNSIGNED_BYTE, b);
+    char p8[4096];
+    snprintf(p8, sizeof p8, "%s/%s.u8", g_out, name);
+    FILE *f8 = fopen(p8, "wb");
+    if (!f8) die("cannot write dump");
+    fwrite(b, 4, (size_t)rt.w * rt.h, f8);
+    fclose(f8);
+    free(b);
+    return;
+  }
   float *buf = read_rt(rt);
   char path[4096];
   snprintf(path, sizeof path, "%s/%s.f32", g_out, name);
@@ -447,12 +462,29 @@ static int run_probe(const char *fs_path, int W, int H, const char *in_path, int
   if (!src) die("cannot read probe fs");
   Program p = make_program(src, fs_path);
   RT in = make_rt(W, H, linear);
-  for (int i = 1; i < argc; ++i)
+  int out_f32 = 0;
+  for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--probe-out-f16")) g_next_f16 = 1;
+    if (!strcmp(argv[i], "--probe-out-f32")) out_f32 = 1;
+  }
+  const int keep8 = g_rgba8;
+  if (out_f32) g_rgba8 = 0;
   RT out = make_rt(W, H, 0);
+  g_rgba8 = keep8;
   float *img = load_f32(in_path, (size_t)W * H * 4);
   upload_rt(in, img);
   p_glDisable(GL_BLEND);
+  for (int i = 1; i < argc; ++i)
+    if (!strcmp(argv[i], "--probe-blend")) { /* blend onto a target cleared to (0,0,0,1), as the passes do */
+      float dc[4] = {0.f, 0.f, 0.f, 1.f};      /* or to --probe-dst r,g,b,a */
+      for (int k = 1; k + 1 < argc; ++k)
+        if (!strcmp(argv[k], "--probe-dst") && sscanf(argv[k + 1], "%f,%f,%f,%f", &dc[0], &dc[1], &dc[2], &dc[3]) != 4)
+          die("--probe-dst r,g,b,a");
+      clear_rt(out, dc[0], dc[1], dc[2], dc[3]);
+      p_glEnable(GL_BLEND);
+      p_glBlendFunc(GL_SRC_ALPHA, GL_ONE_MINUS_SRC_ALPHA);
+      p_glBlendEquation(GL_FUNC_ADD);
+    }
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--u") && i + 1 < argc) {
       char name[256];
@@ -557,7 +589,53 @@ static float *capture_pass(Program p, int w, int h) {
   return read_rt(out);
 }
 
+/* RGBA8 targets (--mode rgba8): llvmpipe interpolates fragTexCoord differently there (an ulp
+ * here and there), so the capture draws into an RGBA8 target too, one component per pass with
+ * its float bits packed into the four bytes (each byte/255 stores exactly). */
+static const char *kCapTexcoordBitsFS =
+    "#version 330 core\n"
+    "in vec2 fragTexCoord;\nout vec4 fragColor;\nuniform int _Comp;\n"
+    "void main() {\n"
+    "  uint b = floatBitsToUint(_Comp == 0 ? fragTexCoord.x : fragTexCoord.y);\n"
+    "  fragColor = vec4(float(b & 255u), float((b >> 8) & 255u), float((b >> 16) & 255u),\n"
+    "                   float(b >> 24)) / 255.0;\n"
+    "}\n";
+
+static void capture_texcoords_rgba8(int w, int h, const char *name) {
+  Program p = make_program(kCapTexcoordBitsFS, "capture_texcoord_bits.fs");
+  size_t n = (size_t)w * h;
+  float *tc = (float *)malloc(n * 2 * sizeof(float));
+  unsigned char *b = (unsigned char *)malloc(n * 4);
+  int save = g_rgba8;
+  g_rgba8 = 0;
+  RT dummy = make_rt(1, 1, 0);
+  g_rgba8 = 1;
+  RT out = make_rt(w, h, 0);
+  g_rgba8 = save;
+  p_glDisable(GL_BLEND);
+  for (int comp = 0; comp < 2; ++comp) {
+    u1i(p, "_Comp", comp);
+    draw(p, dummy, out);
+    p_glFinish();
+    p_glBindFramebuffer(GL_FRAMEBUFFER, out.fbo);
+    p_glPixelStorei(GL_PACK_ALIGNMENT, 1);
+    p_glReadPixels(0, 0, w, h, GL_RGBA, GL_UNSIGNED_BYTE, b);
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t bits = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+                      ((uint32_t)b[4 * i + 3] << 24);
+      memcpy(&tc[2 * i + comp], &bits, 4);
+    }
+  }
+  write_floats(name, tc, n * 2);
+  free(b);
+  free(tc);
+}
+
 static void capture_texcoords(int w, int h, const char *name) {
+  if (g_rgba8) {
+    capture_texcoords_rgba8(w, h, name);
+    return;
+  }
   Program p = make_program(kCapTexcoordFS, "capture_texcoord.fs");
   float *px = capture_pass(p, w, h);
   size_t n = (size_t)w * h;
@@ -761,6 +839,10 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "--linux-merge-fallback")) linux_merge = 1;
     else if (!strcmp(a, "--probe-linear")) probe_linear = 1;
     else if (!strcmp(a, "--probe-out-f16")) {}
+    else if (!strcmp(a, "--dump-u8")) g_dump_u8 = 1;
+    else if (!strcmp(a, "--probe-blend")) {}
+    else if (!strcmp(a, "--probe-dst")) ++i;
+    else if (!strcmp(a, "--probe-out-f32")) {}
     else if (!strcmp(a, "--gi-f16")) gi_f16 = 1; /* giRT1/2 as R16G16B16A16 (RC2DGI.cs:105-106) */
     else if (!strcmp(a, "--capture-tables")) capture = 1;
     else if (!strcmp(a, "--u") || !strcmp(a, "--ui")) ++i; /* probe-mode uniforms */

@@ -83,6 +83,34 @@ static inline void wrap_linear(float u, int n, int *i0, int *i1, float *w) {
 
 static inline float lerpf(float a, float b, float w) { return fmaf(w, b - a, a); }
 
+/* ---------------------------------------------------------------- RGBA8 render textures
+ * The literal app: every render texture RGBA8.  A texel k reads as k*(1/255)
+ * (llvmpipe's unorm8 fetch, probed), so RGBA8 textures are kept here as floats holding exactly
+ * those values; what changes is the store and the LINEAR filter (all probed on llvmpipe):
+ *   store  s8 = rint(f32(clamp(src, 0, 1) * 255)), a8 likewise from src.a;
+ *          dst8 = min(255, mul8(s8, a8) + mul8(dst8, 255 - a8)),              (SRC_ALPHA blend)
+ *          mul8(x, y) = (x * y * 257 + 32768) >> 16 -- each product rounded on its own
+ *          (glref --probe-blend --probe-dst: all 65536 (s8, a8) pairs x 7 destinations)
+ *   LINEAR X = rint(x * 256) in 8.8 fixed point; taps lerp x then y on bytes:
+ *          (a * 256 + (b - a) * w8 + 128) >> 8 */
+static int g_rgba8 = 0;
+static const float INV255 = 1.0f / 255.0f;
+static inline int to_byte(float v) { return (int)rintf(v * 255.0f); } /* exact for k*(1/255) */
+static inline int q8(float x) {
+  float c = x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
+  return (int)rintf(c * 255.0f);
+}
+static inline int mul8(int x, int y) { return (x * y * 257 + 32768) >> 16; } /* ~ x*y/255 */
+static inline void blend8(float *dst, const float src[4]) {
+  int a8 = q8(src[3]);
+  for (int k = 0; k < 4; ++k) {
+    int r = mul8(q8(src[k]), a8) + mul8(to_byte(dst[k]), 255 - a8);
+    dst[k] = (float)(r < 255 ? r : 255) * INV255;
+  }
+}
+static inline int lerp8(int a, int b, int w) { return (a * 256 + (b - a) * w + 128) >> 8; }
+void orc_set_rgba8(int on) { g_rgba8 = on; }
+
 /* texture(T, (u,v)) with LINEAR filtering, RGBA */
 static inline void sample_bilinear(const float *T, int w, int h, float u, float v, float out[4]) {
   int x0, x1, y0, y1;
@@ -91,6 +119,15 @@ static inline void sample_bilinear(const float *T, int w, int h, float u, float 
   wrap_linear(v, h, &y0, &y1, &wy);
   const float *t00 = T + ((size_t)y0 * w + x0) * 4, *t10 = T + ((size_t)y0 * w + x1) * 4;
   const float *t01 = T + ((size_t)y1 * w + x0) * 4, *t11 = T + ((size_t)y1 * w + x1) * 4;
+  if (g_rgba8) { /* rint(x*256) = floor(x)*256 + rint(w*256), w8 = 256 lands on the next tap */
+    int wx8 = (int)rintf(wx * 256.0f), wy8 = (int)rintf(wy * 256.0f);
+    for (int k = 0; k < 4; ++k) {
+      int l0 = lerp8(to_byte(t00[k]), to_byte(t10[k]), wx8);
+      int l1 = lerp8(to_byte(t01[k]), to_byte(t11[k]), wx8);
+      out[k] = (float)lerp8(l0, l1, wy8) * INV255;
+    }
+    return;
+  }
   for (int k = 0; k < 4; ++k) {
     float l0 = lerpf(t00[k], t10[k], wx);
     float l1 = lerpf(t01[k], t11[k], wx);
@@ -105,6 +142,10 @@ static inline const float *sample_nearest(const float *T, int w, int h, float u,
 
 /* blend-on-store: dst = src*src.a + dst*(1-src.a), all four channels (Appendix A.4) */
 static inline void blend_store(float *dst, const float src[4]) {
+  if (g_rgba8) {
+    blend8(dst, src);
+    return;
+  }
   float a = src[3], ia = 1.0f - a;
   for (int k = 0; k < 4; ++k) dst[k] = src[k] * a + dst[k] * ia;
 }
@@ -474,6 +515,7 @@ int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,
   float aspx = (float)c->W / (float)mx, aspy = (float)c->H / (float)mx;
 
   g_gi_f16 = c->gi_f16;
+  g_rgba8 = c->rgba8;
   /* 1. ScreenUV into jumpRT1 */
   orc_screen_uv(color_in, out->jump1, c->W, c->H, tcs);
   /* 2. jump flood ping-pong; jumpRT2 keeps its ClearAllRTs content until written */
@@ -542,5 +584,6 @@ int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,
   free(dirs);
   free(sky);
   g_gi_f16 = 0; /* the per-pass API defaults to RGBA32F again */
+  g_rgba8 = 0;
   return 0;
 }

@@ -36,6 +36,8 @@ typedef struct orc_cfg {
   float reflectivity;   /* _Reflectivity, RC2DGI.cs:41 */
   float blur_radius;    /* cascadeBlurRadius / _BlurRadius, RC2DGI.cs:34 */
   int gi_f16;           /* giRT1/2 as RGBA16F (RC2DGI.cs:105-106): stores round toward zero */
+  int rgba8;            /* every render texture RGBA8 (the literal app): texels hold
+                           k*(1/255); inputs must already be such values */
 } orc_cfg;
 
 /* Optional overrides used only to pin the restatement against llvmpipe goldens:
@@ -85,6 +87,8 @@ int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,
 
 /* float -> RGBA16F storage -> float: round toward zero (llvmpipe's half store, probed) */
 float orc_half_rtz(float x);
+/* RGBA8 render textures (the literal app): values k*(1/255), 8-bit blends and filtering */
+void orc_set_rgba8(int on);
 /* giRT stores of orc_blur_copyback round to half when set (orc_frame sets it from cfg) */
 void orc_set_gi_f16(int on);
 

@@ -4,7 +4,8 @@
 Each fixture is the output of the REFERENCE's own GLSL shaders (read at run time from
 ``--ref-shaders``, default /root/reference/shaders) executed by ``oracle/_ref/glref`` on
 Mesa llvmpipe, replaying DoRC2DGI() (RC2DGI.cs:267-406) with raylib's GL state, in the
-fp32 render-texture mode.  Stored per fixture (float32, GL row order):
+fp32 render-texture mode (``*_f16``: giRT1/2 RGBA16F; ``*_rgba8``: every render texture RGBA8,
+stored as uint8 texels).  Stored per fixture (float32 or uint8, GL row order):
 
 * inputs        color, emissive (the painted colorRT / emissiveRT)
 * llvmpipe data tc_screen, tc_cascade (interpolated fragTexCoord), dir_tables (cos/sin
@@ -50,6 +51,12 @@ FIXTURES = [
     ("c0_demo_256_f16", 256, 256, 2, 8.0, "demo", dict(gi_f16=True), False),
     ("rand128_n4_f16", 128, 128, 4, 2.0, "rand:4", dict(gi_f16=True, blur_radius=2.5), False),
     ("rand96x64_n3_f16", 96, 64, 3, 4.0, "rand:5", dict(gi_f16=True), False),
+    # every render texture RGBA8, the literal app (rc2dgi RC2DGI_STORAGE_RGBA8_COMPAT):
+    # render textures stored as the raw uint8 texels llvmpipe holds
+    ("c0_demo_256_rgba8", 256, 256, 3, 8.0, "demo", dict(rgba8=True), False),
+    ("rand128_n4_rgba8", 128, 128, 4, 2.0, "rand:6", dict(rgba8=True, blur_radius=2.5), True),
+    ("rand96x64_n3_rgba8", 96, 64, 3, 4.0, "rand:7", dict(rgba8=True, reflectivity=0.4), True),
+    ("rand128x64_n2_rgba8_noblur", 128, 64, 2, 4.0, "rand:8", dict(rgba8=True, blur_radius=0.0), True),
 ]
 
 
@@ -67,6 +74,7 @@ def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
     u = dict(DEFAULT_UNIFORMS)
     u.update(over)
     gi_f16 = bool(u.pop("gi_f16", False))
+    rgba8 = bool(u.pop("rgba8", False))
     color, emis = make_scene(scene, W, H)
     with tempfile.TemporaryDirectory() as d:
         color.tofile(os.path.join(d, "c.f32"))
@@ -76,31 +84,38 @@ def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
                  "--reflectivity", str(u["reflectivity"]), "--blur-radius", str(u["blur_radius"])]
         base = ["--w", str(W), "--h", str(H), "--n", str(N), "--out", d]
         subprocess.run([GLREF, "--ref-shaders", shaders, "--ray-range", str(rr), "--in-color", d + "/c.f32",
-                        "--in-emissive", d + "/e.f32", "--dump", "all"] + base + uargs + (["--gi-f16"] if gi_f16 else []),
+                        "--in-emissive", d + "/e.f32", "--dump", "all"] + base + uargs + (["--gi-f16"] if gi_f16 else [])
+                       + (["--mode", "rgba8", "--dump-u8"] if rgba8 else []),
                        check=True)
-        subprocess.run([GLREF, "--capture-tables"] + base + uargs, check=True)
+        subprocess.run([GLREF, "--capture-tables"] + base + uargs + (["--mode", "rgba8"] if rgba8 else []), check=True)
         meta = json.load(open(os.path.join(d, "glref.json")))
         CW, CH = meta["CW"], meta["CH"]
         ld = lambda n, w, h, c=4: np.fromfile(os.path.join(d, n + ".f32"), np.float32).reshape(h, w, c)  # noqa
+        if rgba8:  # render textures as the bytes llvmpipe stored; inputs as the bytes uploaded
+            ld_rt = lambda n, w, h: np.fromfile(os.path.join(d, n + ".u8"), np.uint8).reshape(h, w, 4)  # noqa
+            color = np.rint(np.clip(color, 0, 1) * 255).astype(np.uint8)
+            emis = np.rint(np.clip(emis, 0, 1) * 255).astype(np.uint8)
+        else:
+            ld_rt = ld
         arrs = dict(color=color, emissive=emis,
                     tc_screen=ld("tc_screen", W, H, 2), tc_cascade=ld("tc_cascade", CW, CH, 2),
                     dir_tables=np.fromfile(os.path.join(d, "dir_tables.f32"), np.float32).reshape(-1, 2),
                     sky_table=np.fromfile(os.path.join(d, "sky_table.f32"), np.float32).reshape(-1, 3))
         for n in ("jump1", "jump2", "dist", "temp", "color_out"):
-            arrs[n] = ld(n, W, H)
+            arrs[n] = ld_rt(n, W, H)
         for n in ("gi1", "gi2", "gi_final"):
-            arrs[n] = ld(n, CW, CH)
+            arrs[n] = ld_rt(n, CW, CH)
         if u["blur_radius"] > 0:
-            arrs["blur"] = ld("blur", CW, CH)
+            arrs["blur"] = ld_rt("blur", CW, CH)
         for L in range(N):
-            arrs[f"gi_L{L}"] = ld(f"gi_L{L}", CW, CH)
+            arrs[f"gi_L{L}"] = ld_rt(f"gi_L{L}", CW, CH)
         if keep_steps:
             for k in range(meta["jfa_steps"] + 1):
-                arrs[f"jump_s{k}"] = ld(f"jump_s{k}", W, H)
+                arrs[f"jump_s{k}"] = ld_rt(f"jump_s{k}", W, H)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
     entry = dict(name=name, W=W, H=H, N=N, ray_range=rr, render_scale=1.0, scene=scene, CW=CW, CH=CH,
                  jfa_steps=meta["jfa_steps"], final_gi=meta["final_gi"], renderer=meta["renderer"],
-                 gl_version=meta["version"], mode=meta["mode"], gi_f16=gi_f16, **u)
+                 gl_version=meta["version"], mode=meta["mode"], gi_f16=gi_f16, rgba8=rgba8, **u)
     entry["sky_color"] = list(u["sky_color"])
     entry["sun_color"] = list(u["sun_color"])
     return entry

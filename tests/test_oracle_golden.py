@@ -11,6 +11,17 @@ import pytest
 import oracle
 from conftest import load_fixture, manifest, params_of, rel_err
 
+import contextlib
+
+
+def _as_stored(m, arr):
+    """The oracle's floats as the fixture stores them (RGBA8 fixtures hold the texels)."""
+    return oracle.to_u8(arr) if m.get("rgba8") else arr
+
+
+def _mode(m):
+    return oracle.rgba8_textures() if m.get("rgba8") else contextlib.nullcontext()
+
 CASES = [m["name"] for m in manifest()]
 BY_NAME = {m["name"]: m for m in manifest()}
 
@@ -35,7 +46,8 @@ def test_bit_exact_frame_vs_llvmpipe(case):
         got[f"gi_L{L}"] = fr.gi_levels[L]
     for name, arr in got.items():
         want = fx[name]
-        assert arr.shape == want.shape, name
+        arr = _as_stored(m, arr)
+        assert arr.shape == want.shape and arr.dtype == want.dtype, name
         mism = np.count_nonzero(arr != want)
         assert mism == 0, f"{m['name']}:{name}: {mism} texels differ from llvmpipe"
 
@@ -48,14 +60,16 @@ def test_bit_exact_every_jfa_step(case):
     mx = max(W, H)
     aspx, aspy = np.float32(W) / np.float32(mx), np.float32(H) / np.float32(mx)
     tc = fx["tc_screen"]
-    j = oracle.screen_uv(fx["color"], tc)
-    assert np.array_equal(j, fx["jump_s0"])
-    step = np.float32(1.0)
-    for k in range(m["jfa_steps"]):
-        step = np.float32(step * np.float32(0.5))
-        j = oracle.jfa_step(j, float(step), float(aspx), float(aspy), tc)
-        assert np.array_equal(j, fx[f"jump_s{k + 1}"]), f"JFA step {k + 1}"
-    assert np.array_equal(oracle.distance_field(j, tc), fx["dist"])
+    color = oracle.from_u8(fx["color"]) if m.get("rgba8") else fx["color"]
+    with _mode(m):
+        j = oracle.screen_uv(color, tc)
+        assert np.array_equal(_as_stored(m, j), fx["jump_s0"])
+        step = np.float32(1.0)
+        for k in range(m["jfa_steps"]):
+            step = np.float32(step * np.float32(0.5))
+            j = oracle.jfa_step(j, float(step), float(aspx), float(aspy), tc)
+            assert np.array_equal(_as_stored(m, j), fx[f"jump_s{k + 1}"]), f"JFA step {k + 1}"
+        assert np.array_equal(_as_stored(m, oracle.distance_field(j, tc)), fx["dist"])
 
 
 def test_own_tables_close_to_llvmpipe(case):
@@ -67,7 +81,13 @@ def test_own_tables_close_to_llvmpipe(case):
     fr = oracle.frame(p, fx["color"], fx["emissive"])
     pow2 = (m["W"] & (m["W"] - 1)) == 0 and (m["H"] & (m["H"] - 1)) == 0
     if pow2:  # texture coordinates are exact: JFA / DF are bit-exact
-        assert np.array_equal(fr.jump1, fx["jump1"]) and np.array_equal(fr.dist, fx["dist"])
+        assert np.array_equal(_as_stored(m, fr.jump1), fx["jump1"])
+        assert np.array_equal(_as_stored(m, fr.dist), fx["dist"])
+    if m.get("rgba8"):  # cos/sin ulps move a value across a byte boundary now and then
+        for name, arr in (("gi_final", fr.gi_final), ("color_out", fr.color_out)):
+            d = np.abs(oracle.to_u8(arr).astype(int) - fx[name])
+            assert np.mean(d == 0) >= 0.995 and d.max() <= 2, f"{name}: {np.mean(d > 0):.4%} differ, max {d.max()}"
+        return
     for name, arr in (("gi_final", fr.gi_final), ("color_out", fr.color_out)):
         r = rel_err(arr, fx[name])
         assert np.mean(r <= 1e-4) >= 0.995, f"{name}: {np.mean(r > 1e-4):.4%} texels over 1e-4"
