@@ -29,8 +29,13 @@
  * Storage: f32 semantics (RGBA32F render textures, the reference's own commented intent,
  * RC2DGI.cs:100-107).  RC2DGI_STORAGE_F16 keeps that but stores giRT1 / giRT2 as RGBA16F,
  * the format RC2DGI.cs:105-106 names (stores round toward zero as the GL reference
- * implementation does; downloads convert exactly).  RC2DGI_STORAGE_RGBA8_COMPAT (the literal
- * 8-bit app) is reserved and currently returns RC2DGI_E_UNSUPPORTED.
+ * implementation does; downloads convert exactly).  RC2DGI_STORAGE_RGBA8_COMPAT is the literal
+ * app: every render texture RGBA8 (LoadRenderTexture's default, RC2DGI.cs:79-98) with the GL
+ * reference implementation's unorm8 arithmetic -- a texel k reads as k * (1/255), every pass
+ * output is blended in 8 bits, LINEAR fetches filter in 8.8 fixed point, the JFA seeds are
+ * quantized uv (an occluder whose u or v quantizes to 0 is no seed).  Float downloads return
+ * the values the shaders read (k * (1/255)); RGBA8 downloads the texels.  Float uploads are
+ * quantized as glTexSubImage into an RGBA8 texture does.
  */
 #ifndef RC2DGI_H
 #define RC2DGI_H

@@ -97,22 +97,40 @@ def _cover(P, W, H):
     return m
 
 
-def paint(W, H, prims, clear=None, base=None):
+def _blend8(src8, dst8):
+    """RGBA8 SRC_ALPHA blend as llvmpipe stores it (oracle/rc2dgi_oracle.c blend8): each product
+    rounded on its own, mul8(x, y) = (x*y*257 + 32768) >> 16, saturating sum."""
+    a8 = src8[..., 3:4].astype(np.int64)
+    m = lambda x, y: (x.astype(np.int64) * y * 257 + 32768) >> 16  # noqa: E731
+    return np.minimum(m(src8, a8) + m(dst8, 255 - a8), 255).astype(np.uint8)
+
+
+def paint(W, H, prims, clear=None, base=None, rgba8=False):
     """BeginTextureMode; ClearBackground(clear); draw prims; EndTextureMode -> (H, W, 4) float32
     in GL row order.  prims: (kind, x, y, w_or_radius, h, r, g, b, a) in raylib screen
-    coordinates; colours 0..255."""
-    img = np.zeros((H, W, 4), f32) if base is None else np.array(base, f32)
-    if clear is not None:
-        img[:] = np.array(clear, f32) / f32(255)
+    coordinates; colours 0..255.  rgba8: into an RGBA8 texture -> (H, W, 4) uint8 texels (base
+    given as texels too); the vertex colour reaches the blend as its own bytes."""
+    if rgba8:
+        img = np.zeros((H, W, 4), np.uint8) if base is None else np.array(base, np.uint8)
+        if clear is not None:
+            img[:] = np.array(clear, np.uint8)
+    else:
+        img = np.zeros((H, W, 4), f32) if base is None else np.array(base, f32)
+        if clear is not None:
+            img[:] = np.array(clear, f32) / f32(255)
     table = circle_table()
     inv = f32(f32(1) / f32(255))
     for pr in prims:
-        col = np.array(pr[5:9], f32) * inv
         cov = np.zeros((H, W), bool)
         for t in triangles(pr, W, H, table):
             m = _cover(t, W, H)
             if m is not None:
                 cov |= m
+        if rgba8:
+            src = np.broadcast_to(np.array(pr[5:9], np.uint8), img.shape)
+            img = np.where(cov[..., None], _blend8(src, img), img)
+            continue
+        col = np.array(pr[5:9], f32) * inv
         a = col[3]
         blended = (col[None, None, :] * a + img * (f32(1) - a)).astype(f32)
         img = np.where(cov[..., None], blended, img)

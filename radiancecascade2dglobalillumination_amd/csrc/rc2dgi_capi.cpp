@@ -124,7 +124,11 @@ struct rc2dgi_ctx {
 namespace {
 
 // giRT1 / giRT2 texel size of the context's storage
-size_t gi_bytes(const rc2dgi_ctx *c) { return c->storage == RC2DGI_STORAGE_F16 ? 8 : 16; }
+size_t gi_bytes(const rc2dgi_ctx *c) {
+  return c->storage == RC2DGI_STORAGE_F16 ? 8 : (c->storage == RC2DGI_STORAGE_RGBA8_COMPAT ? 4 : 16);
+}
+bool rgba8(const rc2dgi_ctx *c) { return c->storage == RC2DGI_STORAGE_RGBA8_COMPAT; }
+constexpr float kInv255h = 1.0f / 255.0f;  // an RGBA8 texel k reads as k * (1/255)
 
 int fail(rc2dgi_ctx *c, int code, const std::string &msg) {
   if (c) c->err = msg;
@@ -213,8 +217,8 @@ int allocate(rc2dgi_ctx *c) {
   free_buffers(c);
   derive_sizes(c->W, c->H, c->N, c->render_scale, c->CW, c->CH, c->S);
   const int sp = round_up(c->W, 64), cp = round_up(c->CW, 64);
-  c->sd = ScreenDims{c->W, c->H, sp, is_pow2(c->W), is_pow2(c->H)};
-  c->cd = CascadeDims{c->CW, c->CH, cp, is_pow2(c->CW), is_pow2(c->CH), c->storage == RC2DGI_STORAGE_F16};
+  c->sd = ScreenDims{c->W, c->H, sp, is_pow2(c->W), is_pow2(c->H), rgba8(c)};
+  c->cd = CascadeDims{c->CW, c->CH, cp, is_pow2(c->CW), is_pow2(c->CH), c->storage == RC2DGI_STORAGE_F16, rgba8(c)};
   const size_t ns = (size_t)sp * c->H, nc = (size_t)cp * c->CH;
   HIPCHK(c, alloc(&c->color_in, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->emissive, ns * sizeof(float4)));
@@ -322,12 +326,20 @@ float half_to_float(uint16_t h) {  // exact
   return s ? -v : v;
 }
 
-// a GI-format cascade texture -> float4 (CW x CH, tight)
-int fetch_gi(rc2dgi_ctx *c, const void *src, std::vector<float4> &img) {
-  const size_t gsz = gi_bytes(c);
+// a GI-format cascade texture -> float4 (CW x CH, tight); texels of RGBA8 storage read as k * (1/255)
+int fetch_gi(rc2dgi_ctx *c, const void *src, std::vector<float4> &img, size_t gsz) {
   if (gsz == 16) {
     HIPCHK(c, hipMemcpy2D(img.data(), (size_t)c->CW * 16, src, (size_t)c->cd.pitch * 16, (size_t)c->CW * 16, c->CH,
                           hipMemcpyDeviceToHost));
+    return RC2DGI_OK;
+  }
+  if (gsz == 4) {
+    std::vector<uint8_t> b((size_t)c->CW * c->CH * 4);
+    HIPCHK(c, hipMemcpy2D(b.data(), (size_t)c->CW * 4, src, (size_t)c->cd.pitch * 4, (size_t)c->CW * 4, c->CH,
+                          hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < img.size(); ++k)
+      img[k] = make_float4((float)b[4 * k] * kInv255h, (float)b[4 * k + 1] * kInv255h, (float)b[4 * k + 2] * kInv255h,
+                           (float)b[4 * k + 3] * kInv255h);
     return RC2DGI_OK;
   }
   std::vector<uint16_t> h((size_t)c->CW * c->CH * 4);
@@ -369,8 +381,9 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
     return RC2DGI_E_ARG;
   for (int r : cfg->reserved)
     if (r != 0) return RC2DGI_E_ARG;
-  if (cfg->storage == RC2DGI_STORAGE_RGBA8_COMPAT) return RC2DGI_E_UNSUPPORTED;
-  if (cfg->storage != RC2DGI_STORAGE_F32 && cfg->storage != RC2DGI_STORAGE_F16) return RC2DGI_E_ARG;
+  if (cfg->storage != RC2DGI_STORAGE_F32 && cfg->storage != RC2DGI_STORAGE_F16 &&
+      cfg->storage != RC2DGI_STORAGE_RGBA8_COMPAT)
+    return RC2DGI_E_ARG;
   rc2dgi_ctx *c = new (std::nothrow) rc2dgi_ctx();
   if (!c) return RC2DGI_E_OOM;
   c->device = cfg->device;
@@ -507,14 +520,18 @@ int rc2dgi_upload(rc2dgi_ctx *c, int which, const void *host, int pitch_bytes, i
   if (format == RC2DGI_FMT_RGBA32F) {
     HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)c->sd.pitch * 16, host, pitch_bytes, (size_t)W * 16, H,
                                hipMemcpyHostToDevice, c->stream));
+    if (rgba8(c)) HIPCHK(c, launch_quantize_u8(dst, c->sd.pitch, W, H, c->stream));  // into an RGBA8 texture
   } else {
     std::vector<float4> tmp((size_t)W * H);
     const unsigned char *src = static_cast<const unsigned char *>(host);
+    const bool u8 = rgba8(c);
     for (int j = 0; j < H; ++j)
       for (int i = 0; i < W; ++i) {
         const unsigned char *p = src + (size_t)j * pitch_bytes + 4 * (size_t)i;
-        tmp[(size_t)j * W + i] = make_float4((float)p[0] / 255.0f, (float)p[1] / 255.0f, (float)p[2] / 255.0f,
-                                             (float)p[3] / 255.0f);
+        tmp[(size_t)j * W + i] =
+            u8 ? make_float4((float)p[0] * kInv255h, (float)p[1] * kInv255h, (float)p[2] * kInv255h,
+                             (float)p[3] * kInv255h)
+               : make_float4((float)p[0] / 255.0f, (float)p[1] / 255.0f, (float)p[2] / 255.0f, (float)p[3] / 255.0f);
       }
     HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)c->sd.pitch * 16, tmp.data(), (size_t)W * 16, (size_t)W * 16, H,
                                hipMemcpyHostToDevice, c->stream));
@@ -545,7 +562,7 @@ int rc2dgi_paint(rc2dgi_ctx *c, int which, const unsigned char *clear_rgba, cons
   }
   HIPCHK(c, hipSetDevice(c->device));
   float4 *dst = which == RC2DGI_RT_COLOR ? c->color_in : c->emissive;
-  HIPCHK(c, paint_prims(dst, c->W, c->H, c->sd.pitch, clear_rgba, prims, n, c->paint_buf, c->stream));
+  HIPCHK(c, paint_prims(dst, c->W, c->H, c->sd.pitch, rgba8(c), clear_rgba, prims, n, c->paint_buf, c->stream));
   if (which == RC2DGI_RT_COLOR) c->frame_done = false;
   return RC2DGI_OK;
 }
@@ -564,9 +581,10 @@ int rc2dgi_upload_device(rc2dgi_ctx *c, int which, const void *dev, int pitch_by
   if (format == RC2DGI_FMT_RGBA32F) {
     HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)c->sd.pitch * 16, dev, pitch_bytes, (size_t)W * 16, H,
                                hipMemcpyDeviceToDevice, c->stream));
+    if (rgba8(c)) HIPCHK(c, launch_quantize_u8(dst, c->sd.pitch, W, H, c->stream));
   } else {
     HIPCHK(c, launch_unorm8_to_f32(static_cast<const unsigned char *>(dev), pitch_bytes, dst, c->sd.pitch, W, H,
-                                   c->stream));
+                                   c->stream, rgba8(c)));
   }
   if (which == RC2DGI_RT_COLOR) c->frame_done = false;
   return RC2DGI_OK;
@@ -1075,9 +1093,9 @@ int rc2dgi_download_level(rc2dgi_ctx *c, int level, void *host, int pitch_bytes,
   if (pitch_bytes < row) return fail(c, RC2DGI_E_ARG, "pitch smaller than a row");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (c->cd.gi_f16) {
+  if (gi_bytes(c) != 16) {
     std::vector<float4> img((size_t)c->CW * c->CH);
-    int rc = fetch_gi(c, c->level_bufs[level], img);
+    int rc = fetch_gi(c, c->level_bufs[level], img, gi_bytes(c));
     if (rc != RC2DGI_OK) return rc;
     for (int j = 0; j < c->CH; ++j)
       std::memcpy(static_cast<char *>(host) + (size_t)j * pitch_bytes, img.data() + (size_t)j * c->CW, (size_t)row);
@@ -1113,13 +1131,13 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
     case RC2DGI_RT_COLOR: rc = fetch4(c->frame_done ? c->color_out : c->color_in); break;
     case RC2DGI_RT_EMISSIVE: rc = fetch4(c->emissive); break;
     case RC2DGI_RT_TEMP: rc = fetch4(c->temp); break;
-    case RC2DGI_RT_GI1: rc = c->cd.gi_f16 ? fetch_gi(c, c->gi1, img) : fetch4(c->gi1); break;
-    case RC2DGI_RT_BLUR: rc = fetch4(c->blur); break;
+    case RC2DGI_RT_GI1: rc = fetch_gi(c, c->gi1, img, gi_bytes(c)); break;
+    case RC2DGI_RT_BLUR: rc = fetch_gi(c, c->blur, img, rgba8(c) ? 4 : 16); break;  // RGBA8 mode: bytes
     case RC2DGI_RT_GI2:
       if (n1) {  // giRT2 is never drawn with one cascade: ClearAllRTs content
         for (auto &p : img) p = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
       } else {
-        rc = c->cd.gi_f16 ? fetch_gi(c, c->gi2, img) : fetch4(c->gi2);
+        rc = fetch_gi(c, c->gi2, img, gi_bytes(c));
       }
       break;
     case RC2DGI_RT_JUMP1:
@@ -1128,7 +1146,9 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
       HIPCHK(c, hipMemcpy2D(s.data(), (size_t)w * 4, which == RC2DGI_RT_JUMP1 ? c->jump1 : c->jump2,
                             (size_t)pitch * 4, (size_t)w * 4, h, hipMemcpyDeviceToHost));
       for (size_t k = 0; k < s.size(); ++k) {
-        if (s[k] == 0x80008000u) {  // kNoSeed
+        if (rgba8(c)) {  // the unorm8 seed uv (kv << 16 | ku) itself
+          img[k] = make_float4((float)(s[k] & 0xFFFFu) * kInv255h, (float)(s[k] >> 16) * kInv255h, 0.0f, 1.0f);
+        } else if (s[k] == 0x80008000u) {  // kNoSeed
           img[k] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
         } else {
           const int si = (int)(s[k] & 0xFFFFu), sj = (int)(s[k] >> 16);
@@ -1142,8 +1162,9 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
       HIPCHK(c, hipMemcpy2D(d.data(), (size_t)w * 2, c->dist, (size_t)pitch * 2, (size_t)w * 2, h,
                             hipMemcpyDeviceToHost));
       for (size_t k = 0; k < d.size(); ++k) {  // DistanceField.fs packUNorm16 encoding of q
-        const unsigned q = d[k];
-        img[k] = make_float4((float)((q >> 8) & 255u) / 255.0f, (float)(q & 255u) / 255.0f, 0.0f, 1.0f);
+        const float hi = (float)((d[k] >> 8) & 255u), lo = (float)(d[k] & 255u);
+        img[k] = rgba8(c) ? make_float4(hi * kInv255h, lo * kInv255h, 0.0f, 1.0f)  // RGBA8 texel k: k * (1/255)
+                          : make_float4(hi / 255.0f, lo / 255.0f, 0.0f, 1.0f);
       }
       break;
     }

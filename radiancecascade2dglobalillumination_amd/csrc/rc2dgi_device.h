@@ -71,12 +71,37 @@ __device__ __forceinline__ float4 ntload4(const float4 *p) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// ---- storage of the GI cascade textures giRT1 / giRT2 (and their stand-ins)
+// blend-on-store (SRC_ALPHA, ONE_MINUS_SRC_ALPHA, FUNC_ADD on all four channels)
+__device__ __forceinline__ float4 blend(float4 src, float4 dst) {
+  const float a = src.w, ia = 1.0f - a;
+  return make_float4(src.x * a + dst.x * ia, src.y * a + dst.y * ia, src.z * a + dst.z * ia, src.w * a + dst.w * ia);
+}
+
+// blend over a target cleared to ClearBackground(Black) = (0,0,0,1)
+__device__ __forceinline__ float4 blend_over_black(float4 src) {
+  const float a = src.w, ia = 1.0f - a;
+  return make_float4(src.x * a + 0.0f * ia, src.y * a + 0.0f * ia, src.z * a + 0.0f * ia, src.w * a + 1.0f * ia);
+}
+
+// ---- render-texture storage policies
+// GI textures giRT1 / giRT2 (and their stand-ins) are stored per policy; RT names the policy of
+// the other render textures of the same mode (cascadeBlurRT, tempRT, colorRT).  A policy gives:
+//   T         stored texel;  S  texel as staged in LDS / fed to bilerp
+//   ld / ldnt texel -> float4 (the value a NEAREST fetch returns);  st  float4 -> texel
+//   ld_stage / ld_stage_nt, stage(words)  texel -> S
+//   bilerp    LINEAR filter of four S taps;  blend / blend_black  the blended store
 // GiF32: RGBA32F (the parity referent).  GiF16: RGBA16F, the format RC2DGI.cs:105-106 names;
 // a store rounds toward zero (what the GL reference implementation, llvmpipe, does -- probed,
 // tests/golden), reads are exact.  v_cvt_pkrtz_f16_f32 is that rounding.
+// GiU8: RGBA8, the literal app's format for every render texture, with
+// llvmpipe's unorm8 arithmetic (probed, tests/golden/*_rgba8): a texel k reads as k*(1/255);
+// a store blends in 8 bits, min(255, mul8(s8, a8) + mul8(d8, 255 - a8)) with
+// s8 = rint(clamp(src) * 255) and mul8(x, y) = (x*y*257 + 32768) >> 16; LINEAR filters the bytes in
+// 8.8 fixed point, (a*256 + (b-a)*w8 + 128) >> 8 with w8 = rint(w * 256), x then y.
 struct GiF32 {
   typedef float4 T;
+  typedef float4 S;
+  typedef GiF32 RT;
   static constexpr int kBytes = 16;
   __device__ static float4 ld(const T *p) { return *p; }
   __device__ static float4 ldnt(const T *p) {
@@ -85,10 +110,22 @@ struct GiF32 {
   }
   __device__ static void st(T *p, float4 v) { *p = v; }
   __device__ static float4 round(float4 v) { return v; }
+  __device__ static S ld_stage(const T *p) { return *p; }
+  __device__ static S ld_stage_nt(const T *p) { return ldnt(p); }
+  __device__ static S stage(unsigned x, unsigned y, unsigned z, unsigned w) {
+    return make_float4(__uint_as_float(x), __uint_as_float(y), __uint_as_float(z), __uint_as_float(w));
+  }
+  __device__ static float4 bilerp(S t00, S t10, S t01, S t11, float wx, float wy) {
+    return lerp_gl(lerp_gl(t00, t10, wx), lerp_gl(t01, t11, wx), wy);
+  }
+  __device__ static float4 blend(float4 src, float4 dst) { return rc2dgi::blend(src, dst); }
+  __device__ static float4 blend_black(float4 src) { return blend_over_black(src); }
 };
 
-struct GiF16 {
+struct GiF16 : GiF32 {
   typedef uint2 T;
+  typedef float4 S;
+  typedef GiF32 RT;  // cascadeBlurRT / tempRT stay RGBA32F
   static constexpr int kBytes = 8;
   typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
   __device__ static float4 unpack(uint2 u) {
@@ -107,9 +144,63 @@ struct GiF16 {
   }
   __device__ static void st(T *p, float4 v) { *p = pack(v); }
   __device__ static float4 round(float4 v) { return unpack(pack(v)); }
+  __device__ static S ld_stage(const T *p) { return ld(p); }
+  __device__ static S ld_stage_nt(const T *p) { return ldnt(p); }
+  __device__ static S stage(unsigned x, unsigned y, unsigned, unsigned) { return unpack(make_uint2(x, y)); }
 };
 
-// texture(T, (u, v)) with LINEAR filtering on a GI-format texture
+constexpr float kInv255 = 1.0f / 255.0f;  // llvmpipe's unorm8 fetch: k * (1/255), one f32 multiply
+
+__device__ __forceinline__ unsigned q8(float x) {  // fragment output -> unorm8 (NaN -> 0)
+  return (unsigned)rintf(fminf(fmaxf(x, 0.0f), 1.0f) * 255.0f);
+}
+__device__ __forceinline__ unsigned mul8(unsigned x, unsigned y) { return (x * y * 257u + 32768u) >> 16; }
+__device__ __forceinline__ unsigned lerp8(unsigned a, unsigned b, int w) {  // >= 0 for w in [0, 256]
+  return (unsigned)((int)(a * 256u) + ((int)b - (int)a) * w + 128) >> 8;
+}
+
+struct GiU8 {
+  typedef unsigned T;  // r | g << 8 | b << 16 | a << 24
+  typedef unsigned S;
+  typedef GiU8 RT;
+  static constexpr int kBytes = 4;
+  __device__ static float4 unpack(unsigned u) {
+    return make_float4((float)(u & 255u) * kInv255, (float)((u >> 8) & 255u) * kInv255,
+                       (float)((u >> 16) & 255u) * kInv255, (float)(u >> 24) * kInv255);
+  }
+  __device__ static unsigned pack(float4 v) { return q8(v.x) | (q8(v.y) << 8) | (q8(v.z) << 16) | (q8(v.w) << 24); }
+  __device__ static float4 ld(const T *p) { return unpack(*p); }
+  __device__ static float4 ldnt(const T *p) { return unpack(__builtin_nontemporal_load(p)); }
+  __device__ static void st(T *p, float4 v) { *p = pack(v); }  // v: values k * (1/255) (exact)
+  __device__ static float4 round(float4 v) { return unpack(pack(v)); }
+  __device__ static S ld_stage(const T *p) { return *p; }
+  __device__ static S ld_stage_nt(const T *p) { return __builtin_nontemporal_load(p); }
+  __device__ static S stage(unsigned x, unsigned, unsigned, unsigned) { return x; }
+  __device__ static float4 bilerp(S t00, S t10, S t01, S t11, float wx, float wy) {
+    const int w8x = (int)rintf(wx * 256.0f), w8y = (int)rintf(wy * 256.0f);
+    float r[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int sh = 8 * c;
+      const unsigned l0 = lerp8((t00 >> sh) & 255u, (t10 >> sh) & 255u, w8x);
+      const unsigned l1 = lerp8((t01 >> sh) & 255u, (t11 >> sh) & 255u, w8x);
+      r[c] = (float)lerp8(l0, l1, w8y) * kInv255;
+    }
+    return make_float4(r[0], r[1], r[2], r[3]);
+  }
+  __device__ static float blend1(float s, float d, unsigned a8) {
+    const unsigned v = mul8(q8(s), a8) + mul8(q8(d), 255u - a8);
+    return (float)(v < 255u ? v : 255u) * kInv255;
+  }
+  __device__ static float4 blend(float4 src, float4 dst) {
+    const unsigned a8 = q8(src.w);
+    return make_float4(blend1(src.x, dst.x, a8), blend1(src.y, dst.y, a8), blend1(src.z, dst.z, a8),
+                       blend1(src.w, dst.w, a8));
+  }
+  __device__ static float4 blend_black(float4 src) { return blend(src, make_float4(0.0f, 0.0f, 0.0f, 1.0f)); }
+};
+
+// texture(T, (u, v)) with LINEAR filtering on a policy-format texture
 template <class GI>
 __device__ __forceinline__ float4 sample_bilinear_gi(const typename GI::T *__restrict__ T, int pitch, Axis ax, Axis ay,
                                                      float u, float v) {
@@ -117,21 +208,8 @@ __device__ __forceinline__ float4 sample_bilinear_gi(const typename GI::T *__res
   float wx, wy;
   wrap_linear(u, ax, x0, x1, wx);
   wrap_linear(v, ay, y0, y1, wy);
-  const float4 t00 = GI::ld(&T[(size_t)y0 * pitch + x0]), t10 = GI::ld(&T[(size_t)y0 * pitch + x1]);
-  const float4 t01 = GI::ld(&T[(size_t)y1 * pitch + x0]), t11 = GI::ld(&T[(size_t)y1 * pitch + x1]);
-  return lerp_gl(lerp_gl(t00, t10, wx), lerp_gl(t01, t11, wx), wy);
-}
-
-// blend-on-store (SRC_ALPHA, ONE_MINUS_SRC_ALPHA, FUNC_ADD on all four channels)
-__device__ __forceinline__ float4 blend(float4 src, float4 dst) {
-  const float a = src.w, ia = 1.0f - a;
-  return make_float4(src.x * a + dst.x * ia, src.y * a + dst.y * ia, src.z * a + dst.z * ia, src.w * a + dst.w * ia);
-}
-
-// blend over a target cleared to ClearBackground(Black) = (0,0,0,1)
-__device__ __forceinline__ float4 blend_over_black(float4 src) {
-  const float a = src.w, ia = 1.0f - a;
-  return make_float4(src.x * a + 0.0f * ia, src.y * a + 0.0f * ia, src.z * a + 0.0f * ia, src.w * a + 1.0f * ia);
+  return GI::bilerp(GI::ld_stage(&T[(size_t)y0 * pitch + x0]), GI::ld_stage(&T[(size_t)y0 * pitch + x1]),
+                    GI::ld_stage(&T[(size_t)y1 * pitch + x0]), GI::ld_stage(&T[(size_t)y1 * pitch + x1]), wx, wy);
 }
 
 }  // namespace rc2dgi

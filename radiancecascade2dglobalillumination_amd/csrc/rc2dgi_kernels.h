@@ -10,6 +10,7 @@ struct ScreenDims {
   int W, H;        // screen texels
   int pitch;       // row pitch in texels (all screen-size buffers share it)
   int powW, powH;  // power-of-two flags (GL wrap arithmetic differs)
+  int u8;          // RGBA8 render textures (RC2DGI_STORAGE_RGBA8_COMPAT): seeds are unorm8 (u, v)
 };
 
 // fixed bilinear taps of Blur.fs for a dyadic radius (see k_blur_rows)
@@ -29,6 +30,8 @@ struct CascadeDims {
   int pitch;
   int powW, powH;
   int gi_f16;  // giRT1 / giRT2 (and their stand-ins) stored as RGBA16F (RC2DGI_STORAGE_F16)
+  int gi_u8;   // every render texture RGBA8 (RC2DGI_STORAGE_RGBA8_COMPAT): giRT1/2 and
+               // cascadeBlurRT as bytes, 8-bit blends and filtering
 };
 
 // ScreenUV (shaders/ScreenUV.fs) as a 1-bit occupancy mask (row pitch mpitch 32-bit words)
@@ -36,7 +39,8 @@ hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, Scr
 // the ScreenUV seed texture J0 (packed seeds) from the mask
 hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *seeds, ScreenDims s, hipStream_t st);
 
-// one JumpFlood step (shaders/JumpFlood.fs) over packed seeds (sj<<16 | si, 0x80008000 = none).
+// one JumpFlood step (shaders/JumpFlood.fs) over packed seeds (sj<<16 | si, 0x80008000 = none;
+// with s.u8 the stored unorm8 seed uv, kv<<16 | ku, none when ku or kv is 0).
 // first: src is the occupancy mask (pitch in words), else packed seeds (pitch in texels).
 // off_x/off_y = vec2(k,k)*_Aspect.yx*_StepSize for k = -1,0,1 (host-computed).
 // dist != nullptr fuses DistanceField.fs: stores the 16-bit q of packUNorm16.
@@ -109,8 +113,11 @@ hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, 
                         CascadeDims c, hipStream_t st, int row0 = 0,
                         int row1 = -1);
 
-// format conversion for uploads from device memory: RGBA8 unorm -> float4 (k/255)
+// format conversion for uploads from device memory: RGBA8 unorm -> float4 (k/255; u8: k*(1/255),
+// the value an RGBA8 texture fetch returns)
 hipError_t launch_unorm8_to_f32(const unsigned char *src, int src_pitch_bytes, float4 *dst, int dst_pitch, int W,
-                                int H, hipStream_t st);
+                                int H, hipStream_t st, bool u8 = false);
+// a float upload into an RGBA8 texture: v -> rint(clamp(v) * 255) * (1/255), in place
+hipError_t launch_quantize_u8(float4 *buf, int pitch, int W, int H, hipStream_t st);
 
 }  // namespace rc2dgi

@@ -16,7 +16,10 @@
 //   ScreenUV seeds (J0)                    1 bit   occupancy mask read by the first JFA step
 //   distRT                                 uint16  q = packUNorm16(d) (DistanceField.fs:12-19);
 //                                                  RadianceCascades.fs:30-33 reads q / 65535
-//   giRT1/2, cascadeBlurRT                 float4
+//   giRT1/2, cascadeBlurRT                 float4 (f16 mode: giRT1/2 as RGBA16F)
+// RGBA8 mode (RC2DGI_STORAGE_RGBA8_COMPAT, every render texture RGBA8 as in the literal app):
+//   jumpRT1/2 hold the unorm8 seed uv (kv<<16 | ku), giRT1/2 and cascadeBlurRT are RGBA8 bytes,
+//   the float4 textures hold exactly k * (1/255); stores blend and LINEAR filters in 8 bits.
 // The floating-point arithmetic follows the shader expressions operation by operation
 // (compiled with -ffp-contract=off), so results are reproducible against the CPU oracle.
 #include "rc2dgi_device.h"
@@ -34,6 +37,14 @@ static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 constexpr unsigned kNoSeed = 0x80008000u;  // si = sj = 32768: never a texel (W, H <= 32768)
 
 __device__ __forceinline__ unsigned pack_seed(int si, int sj) { return ((unsigned)sj << 16) | (unsigned)si; }
+
+// RGBA8 jumpRT (ScreenDims::u8): a texel holds the unorm8 seed uv, packed kv << 16 | ku; it reads
+// back as (ku, kv) * (1/255).  ScreenUV.fs stores the seed texel's fragTexCoord, quantized; the
+// JumpFlood.fs test `peek.x != 0 && peek.y != 0` then rejects every ku == 0 or kv == 0 (no seed = 0).
+__device__ __forceinline__ unsigned pack_seed_u8(int si, int sj, Axis ax, Axis ay) {
+  return (q8(texcoord(sj, ay)) << 16) | q8(texcoord(si, ax));
+}
+__device__ __forceinline__ bool seed_u8_ok(unsigned sd) { return (sd & 0xFFFFu) != 0u && (sd >> 16) != 0u; }
 
 // ScreenUV.fs:19 `any(greaterThan(color.rgb, 0))` as a 1-bit occupancy mask (one 64-texel ballot
 // per wave; mask row pitch s.mpitch words).  The seed texture J0 itself is never observable when
@@ -69,7 +80,10 @@ __global__ __launch_bounds__(256) void k_seeds_from_mask(const unsigned *__restr
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= s.H) return;
   const bool occ = (mask[(size_t)j * mpitch + (i >> 5)] >> (i & 31)) & 1u;
-  seeds[(size_t)j * s.pitch + i] = occ ? pack_seed(i, j) : kNoSeed;
+  if (s.u8)
+    seeds[(size_t)j * s.pitch + i] = occ ? pack_seed_u8(i, j, Axis{s.W, s.powW}, Axis{s.H, s.powH}) : 0u;
+  else
+    seeds[(size_t)j * s.pitch + i] = occ ? pack_seed(i, j) : kNoSeed;
 }
 
 // ---------------------------------------------------------------- JumpFlood (+ DistanceField)
@@ -79,11 +93,12 @@ struct JfaOffsets {
 
 
 // One JumpFlood.fs step.  FIRST: taps read the occupancy mask (the ScreenUV seeds); otherwise the
-// packed seeds of the previous step.  dist != nullptr fuses DistanceField.fs.
+// packed seeds of the previous step.  dist != nullptr fuses DistanceField.fs.  U8: RGBA8 jumpRT
+// (quantized seed uv, pack_seed_u8).
 // A 256-thread workgroup covers 64 x (4*JT) texels; each lane owns JT texels 4 rows apart and issues all 9*JT tap loads before the first compare (latency-bound gathers).
 constexpr int JT = 4;
 
-template <bool FIRST>
+template <bool FIRST, bool U8>
 __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ src, int src_pitch,
                                                   unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                   ScreenDims s, JfaOffsets o, int row0, int row1) {
@@ -107,7 +122,10 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
       for (int x = 0; x < 3; ++x) {
         if (FIRST) {
           const bool occ = (src[(size_t)tj * src_pitch + (ti[x] >> 5)] >> (ti[x] & 31)) & 1u;
-          seed[t][y * 3 + x] = occ ? pack_seed(ti[x], tj) : kNoSeed;
+          if constexpr (U8)
+            seed[t][y * 3 + x] = occ ? pack_seed_u8(ti[x], tj, ax, ay) : 0u;
+          else
+            seed[t][y * 3 + x] = occ ? pack_seed(ti[x], tj) : kNoSeed;
         } else {
           seed[t][y * 3 + x] = src[(size_t)tj * src_pitch + ti[x]];
         }
@@ -120,12 +138,13 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
     if (j >= row1) break;
     const float v = texcoord(j, ay);
     float minDist = 1.0f, bx = 0.0f, by = 0.0f;
-    unsigned best = kNoSeed;
+    unsigned best = U8 ? 0u : kNoSeed;
 #pragma unroll
     for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
       const unsigned sd = seed[t][k];
-      if (sd != kNoSeed) {  // peek.x != 0 && peek.y != 0 (a seed's uv is never 0)
-        const float px = texcoord((int)(sd & 0xFFFFu), ax), py = texcoord((int)(sd >> 16), ay);
+      if (U8 ? seed_u8_ok(sd) : sd != kNoSeed) {  // peek.x != 0 && peek.y != 0 (f32: a seed's uv is never 0)
+        const float px = U8 ? (float)(sd & 0xFFFFu) * kInv255 : texcoord((int)(sd & 0xFFFFu), ax);
+        const float py = U8 ? (float)(sd >> 16) * kInv255 : texcoord((int)(sd >> 16), ay);
         const float dx = px - u, dy = py - v;
         const float d = dx * dx + dy * dy;
         if (d < minDist) {
@@ -330,7 +349,7 @@ __device__ __forceinline__ int cvt_floor(float x) {
 // rolled (1) the VALU-bound low levels (no SGPR spills, occupancy 8).
 // TILED: `dist` is the 8x8-tiled copy (k_dist_tile): one 128-byte line holds an 8x8 texel tile,
 // so the nearly parallel rays of a lane (and vertical-ish steps) share lines.
-// GI: storage of the cascade textures (GiF32 / GiF16, rc2dgi_device.h).
+// GI: storage of the cascade textures (GiF32 / GiF16 / GiU8, rc2dgi_device.h).
 template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, bool TILED, class GI>
 __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
@@ -344,7 +363,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
   constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
   constexpr int NSTAGE = ND * RH * RW;
   constexpr int PT = (NSTAGE + NT - 1) / NT;
-  __shared__ float4 s_up[TOP ? 1 : NSTAGE];
+  __shared__ typename GI::S s_up[TOP ? 1 : NSTAGE];
 
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
   // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
@@ -362,8 +381,9 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
   const int umask = 2 * P.bsc - 1, ushift = P.level + 1;
   // staged texels as plain 32-bit components (HIP's vector unions defeat SROA -> scratch); raw
   // storage bits, converted when written to LDS after the march
-  constexpr bool F16 = GI::kBytes == 8;
-  unsigned stx[TOP ? 1 : PT], sty[TOP ? 1 : PT], stz[(TOP || F16) ? 1 : PT], stw[(TOP || F16) ? 1 : PT];
+  constexpr int NWD = GI::kBytes / 4;  // 32-bit words per texel
+  unsigned stx[TOP ? 1 : PT], sty[(TOP || NWD < 2) ? 1 : PT], stz[(TOP || NWD < 4) ? 1 : PT],
+      stw[(TOP || NWD < 4) ? 1 : PT];
   if (!TOP) {
 #pragma unroll
     for (int q = 0; q < PT; ++q) {
@@ -377,7 +397,9 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
       gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
       gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
       const typename GI::T v = upper[(size_t)gy * P.c.pitch + gx];  // issued now, consumed after the march
-      if constexpr (F16) {
+      if constexpr (NWD == 1) {
+        stx[q] = v;
+      } else if constexpr (NWD == 2) {
         stx[q] = v.x;
         sty[q] = v.y;
       } else {
@@ -490,11 +512,12 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
     for (int q = 0; q < PT; ++q) {
       const int k = (int)threadIdx.x + q * NT;
       if (k < NSTAGE) {
-        if constexpr (F16)
-          s_up[k] = GiF16::unpack(make_uint2(stx[q], sty[q]));
+        if constexpr (NWD == 1)
+          s_up[k] = GI::stage(stx[q], 0u, 0u, 0u);
+        else if constexpr (NWD == 2)
+          s_up[k] = GI::stage(stx[q], sty[q], 0u, 0u);
         else
-          s_up[k] = make_float4(__uint_as_float(stx[q]), __uint_as_float(sty[q]), __uint_as_float(stz[q]),
-                                __uint_as_float(stw[q]));
+          s_up[k] = GI::stage(stx[q], sty[q], stz[q], stw[q]);
       }
     }
     __syncthreads();
@@ -544,10 +567,10 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
         const int ai = bi * 4 + r4;  // angleIndex
         if (rad.w != 0.0f) {
           if (!TOP) {
-            float4 t00, t10, t01, t11;
+            typename GI::S t00, t10, t01, t11;
             float ux = wx, uy = wy;
             if (pow2c) {
-              const float4 *sr = s_up + r * RH * RW;
+              const typename GI::S *sr = s_up + r * RH * RW;
               t00 = sr[ly0 * RW + lx0];
               t10 = sr[ly0 * RW + lx0 + 1];
               t01 = sr[(ly0 + 1) * RW + lx0];
@@ -569,7 +592,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
               const int b0 = rel(y0, ry0, P.c.CH), b1 = rel(y1, ry0, P.c.CH);
               if ((unsigned)a0 < (unsigned)RW && (unsigned)a1 < (unsigned)RW && (unsigned)b0 < (unsigned)RH &&
                   (unsigned)b1 < (unsigned)RH) {
-                const float4 *sr = s_up + r * RH * RW;
+                const typename GI::S *sr = s_up + r * RH * RW;
                 t00 = sr[b0 * RW + a0];
                 t10 = sr[b0 * RW + a1];
                 t01 = sr[b1 * RW + a0];
@@ -577,13 +600,13 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
               } else {
                 // rounding stepped outside the staged footprint: read HBM.  Non-temporal loads
                 // keep the compiler from fusing this path with the LDS path into flat loads.
-                t00 = GI::ldnt(&upper[(size_t)y0 * P.c.pitch + x0]);
-                t10 = GI::ldnt(&upper[(size_t)y0 * P.c.pitch + x1]);
-                t01 = GI::ldnt(&upper[(size_t)y1 * P.c.pitch + x0]);
-                t11 = GI::ldnt(&upper[(size_t)y1 * P.c.pitch + x1]);
+                t00 = GI::ld_stage_nt(&upper[(size_t)y0 * P.c.pitch + x0]);
+                t10 = GI::ld_stage_nt(&upper[(size_t)y0 * P.c.pitch + x1]);
+                t01 = GI::ld_stage_nt(&upper[(size_t)y1 * P.c.pitch + x0]);
+                t11 = GI::ld_stage_nt(&upper[(size_t)y1 * P.c.pitch + x1]);
               }
             }
-            const float4 up = lerp_gl(lerp_gl(t00, t10, ux), lerp_gl(t01, t11, ux), uy);
+            const float4 up = GI::bilerp(t00, t10, t01, t11, ux, uy);
             rad.x = rad.x + up.x * rad.w;
             rad.y = rad.y + up.y * rad.w;
             rad.z = rad.z + up.z * rad.w;
@@ -602,7 +625,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
       }
       const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
       const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
-      GI::st(&out[(size_t)j * P.c.pitch + i], blend_over_black(acc));
+      GI::st(&out[(size_t)j * P.c.pitch + i], GI::blend_black(acc));
     }
   }
 }
@@ -622,8 +645,9 @@ __global__ __launch_bounds__(256) void k_dist_tile(const unsigned short *__restr
 
 // ---------------------------------------------------------------- Blur + copy-back
 template <class GI>
-__global__ __launch_bounds__(256) void k_blur(const typename GI::T *__restrict__ gi, float4 *__restrict__ blur_out,
-                                              CascadeDims c, float radius, int row0, int row1) {
+__global__ __launch_bounds__(256) void k_blur(const typename GI::T *__restrict__ gi,
+                                              typename GI::RT::T *__restrict__ blur_out, CascadeDims c, float radius,
+                                              int row0, int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= c.CW || j >= row1) return;
@@ -648,7 +672,7 @@ __global__ __launch_bounds__(256) void k_blur(const typename GI::T *__restrict__
     res.z = res.z + t.z * w;
     res.w = res.w + t.w * w;
   }
-  blur_out[(size_t)j * c.pitch + i] = blend_over_black(res);
+  GI::RT::st(&blur_out[(size_t)j * c.pitch + i], GI::RT::blend_black(res));  // cascadeBlurRT cleared to (0,0,0,1)
 }
 
 // Blur.fs + its blended copy-back in one pass, for power-of-two cascade sizes.  There the
@@ -828,15 +852,16 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
 }
 
 template <class GI>
-__global__ __launch_bounds__(256) void k_blur_copyback(const float4 *__restrict__ blur, typename GI::T *__restrict__ gi,
-                                                       CascadeDims c, int row0, int row1) {
+__global__ __launch_bounds__(256) void k_blur_copyback(const typename GI::RT::T *__restrict__ blur,
+                                                       typename GI::T *__restrict__ gi, CascadeDims c, int row0,
+                                                       int row1) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= c.CW || j >= row1) return;
   const float u = texcoord(i, Axis{c.CW, c.powW}), v = texcoord(j, Axis{c.CH, c.powH});
-  const float4 s = sample_bilinear(blur, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
+  const float4 s = sample_bilinear_gi<typename GI::RT>(blur, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
   const size_t o = (size_t)j * c.pitch + i;
-  GI::st(&gi[o], blend(s, GI::ld(&gi[o])));
+  GI::st(&gi[o], GI::blend(s, GI::ld(&gi[o])));
 }
 
 // ---------------------------------------------------------------- Merge + copy-back
@@ -852,19 +877,29 @@ __global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_
   const float4 col = color_in[o];
   const float4 g = sample_bilinear_gi<GI>(gi, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
   const float4 src = make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
-  const float4 t = blend_over_black(src);  // tempRT as cleared by ClearAllRTs
+  const float4 t = GI::RT::blend_black(src);  // tempRT as cleared by ClearAllRTs
   temp[o] = t;
-  color_out[o] = blend(t, col);            // tempRT -> colorRT, default shader, blended
+  color_out[o] = GI::RT::blend(t, col);       // tempRT -> colorRT, default shader, blended
 }
 
 __global__ __launch_bounds__(256) void k_unorm8_to_f32(const unsigned char *__restrict__ src, int src_pitch,
-                                                       float4 *__restrict__ dst, int dst_pitch, int W, int H) {
+                                                       float4 *__restrict__ dst, int dst_pitch, int W, int H,
+                                                       int u8) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= W || j >= H) return;
   const uchar4 b = *reinterpret_cast<const uchar4 *>(src + (size_t)j * src_pitch + 4 * (size_t)i);
   dst[(size_t)j * dst_pitch + i] =
-      make_float4((float)b.x / 255.0f, (float)b.y / 255.0f, (float)b.z / 255.0f, (float)b.w / 255.0f);
+      u8 ? make_float4((float)b.x * kInv255, (float)b.y * kInv255, (float)b.z * kInv255, (float)b.w * kInv255)
+         : make_float4((float)b.x / 255.0f, (float)b.y / 255.0f, (float)b.z / 255.0f, (float)b.w / 255.0f);
+}
+
+__global__ __launch_bounds__(256) void k_quantize_u8(float4 *__restrict__ buf, int pitch, int W, int H) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= W || j >= H) return;
+  float4 &v = buf[(size_t)j * pitch + i];
+  v = GiU8::unpack(GiU8::pack(v));
 }
 
 // ---------------------------------------------------------------- launchers
@@ -922,7 +957,13 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   }
   const dim3 grid(ceil_div(s.W, 64), ceil_div(row1 - row0, 4 * JT));
   JfaTaps tp;
-  if (jfa_p2_taps(s, off_x, off_y, &tp)) {
+  if (s.u8) {  // RGBA8 jumpRT: quantized seed uv, the float path
+    if (first)
+      hipLaunchKernelGGL((k_jfa_step<true, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
+    else
+      hipLaunchKernelGGL((k_jfa_step<false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
+                         row1);
+  } else if (jfa_p2_taps(s, off_x, off_y, &tp)) {
     const bool ikey = s.W == s.H && s.W <= 4096;
 #define RC2DGI_JFA(F, K) \
   hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1)
@@ -933,9 +974,10 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     }
 #undef RC2DGI_JFA
   } else if (first) {
-    hipLaunchKernelGGL(k_jfa_step<true>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
+    hipLaunchKernelGGL((k_jfa_step<true, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
   } else {
-    hipLaunchKernelGGL(k_jfa_step<false>, grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
+    hipLaunchKernelGGL((k_jfa_step<false, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
+                       row1);
   }
   return hipGetLastError();
 }
@@ -1046,6 +1088,16 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.reflectivity = a.reflectivity;
   const int nblk = P.bsc * P.bsc;
   hipError_t e = hipSuccess;
+  if (c.gi_u8) {  // RGBA8 cascades: the 16x16x1 family only
+    switch (a.variant) {
+      case 13: e = launch_rc_tiles<16, 16, 1, 1, 32, false, GiU8>(a, P, st); break;
+      case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, true, GiU8>(a, P, st); break;
+      case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, true, GiU8>(a, P, st); break;
+      default: e = launch_rc_tiles<16, 16, 1, 1, 1, false, GiU8>(a, P, st); break;
+    }
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
+  }
   if (c.gi_f16) {  // RGBA16F cascades: the 16x16x1 family only
     switch (a.variant) {
       case 13: e = launch_rc_tiles<16, 16, 1, 1, 32, false, GiF16>(a, P, st); break;
@@ -1087,7 +1139,11 @@ hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float 
                        int row1) {
   clamp_rows(c.CH, row0, row1);
   if (row0 >= row1) return hipSuccess;
-  if (c.gi_f16)
+  if (c.gi_u8)
+    hipLaunchKernelGGL(k_blur<GiU8>, grid2d(c.CW, row1 - row0), dim3(256), 0, st,
+                       reinterpret_cast<const GiU8::T *>(gi), reinterpret_cast<GiU8::T *>(blur_out), c, radius, row0,
+                       row1);
+  else if (c.gi_f16)
     hipLaunchKernelGGL(k_blur<GiF16>, grid2d(c.CW, row1 - row0), dim3(256), 0, st,
                        reinterpret_cast<const GiF16::T *>(gi), blur_out, c, radius, row0, row1);
   else
@@ -1097,7 +1153,7 @@ hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float 
 }
 
 bool blur_fused_ok(CascadeDims c, float radius) {
-  return c.powW && c.powH && c.CW >= 64 && c.CH >= 16 && radius <= 6.0f;
+  return !c.gi_u8 && c.powW && c.powH && c.CW >= 64 && c.CH >= 16 && radius <= 6.0f;
 }
 
 bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
@@ -1126,7 +1182,7 @@ bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Ca
 }
 
 int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt) {
-  if (!(c.powW && c.powH) || c.CW < 64 || c.CH < 32 || c.CW > 16384 || c.CH > 16384) return -1;
+  if (c.gi_u8 || !(c.powW && c.powH) || c.CW < 64 || c.CH < 32 || c.CW > 16384 || c.CH > 16384) return -1;
   if (!(radius > 0.0f) || !(radius < 3.0f) || radius * 256.0f != floorf(radius * 256.0f)) return -1;
   // x = i - radius and i + radius are exact: floor / fraction do not depend on i
   const float lo = -radius, hi = radius;
@@ -1169,7 +1225,10 @@ bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Cas
 hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, hipStream_t st, int row0, int row1) {
   clamp_rows(c.CH, row0, row1);
   if (row0 >= row1) return hipSuccess;
-  if (c.gi_f16)
+  if (c.gi_u8)
+    hipLaunchKernelGGL(k_blur_copyback<GiU8>, grid2d(c.CW, row1 - row0), dim3(256), 0, st,
+                       reinterpret_cast<const GiU8::T *>(blur), reinterpret_cast<GiU8::T *>(gi), c, row0, row1);
+  else if (c.gi_f16)
     hipLaunchKernelGGL(k_blur_copyback<GiF16>, grid2d(c.CW, row1 - row0), dim3(256), 0, st, blur,
                        reinterpret_cast<GiF16::T *>(gi), c, row0, row1);
   else
@@ -1181,7 +1240,10 @@ hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, 
                         CascadeDims c, hipStream_t st, int row0, int row1) {
   clamp_rows(s.H, row0, row1);
   if (row0 >= row1) return hipSuccess;
-  if (c.gi_f16)
+  if (c.gi_u8)
+    hipLaunchKernelGGL(k_merge<GiU8>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in,
+                       reinterpret_cast<const GiU8::T *>(gi), temp, color_out, s, c, row0, row1);
+  else if (c.gi_f16)
     hipLaunchKernelGGL(k_merge<GiF16>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in,
                        reinterpret_cast<const GiF16::T *>(gi), temp, color_out, s, c, row0, row1);
   else
@@ -1199,8 +1261,14 @@ hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned shor
 }
 
 hipError_t launch_unorm8_to_f32(const unsigned char *src, int src_pitch_bytes, float4 *dst, int dst_pitch, int W,
-                                int H, hipStream_t st) {
-  hipLaunchKernelGGL(k_unorm8_to_f32, grid2d(W, H), dim3(256), 0, st, src, src_pitch_bytes, dst, dst_pitch, W, H);
+                                int H, hipStream_t st, bool u8) {
+  hipLaunchKernelGGL(k_unorm8_to_f32, grid2d(W, H), dim3(256), 0, st, src, src_pitch_bytes, dst, dst_pitch, W, H,
+                     (int)u8);
+  return hipGetLastError();
+}
+
+hipError_t launch_quantize_u8(float4 *buf, int pitch, int W, int H, hipStream_t st) {
+  hipLaunchKernelGGL(k_quantize_u8, grid2d(W, H), dim3(256), 0, st, buf, pitch, W, H);
   return hipGetLastError();
 }
 

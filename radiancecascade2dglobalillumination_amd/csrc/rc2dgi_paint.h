@@ -20,9 +20,10 @@ struct PaintBuffers {
 };
 
 // BeginTextureMode(dst); [ClearBackground(clear)]; draw prims[0..n); EndTextureMode.
-// dst: W x H float4 render texture (pitch in texels), GL row order.  Synchronous w.r.t. the
-// host arrays (they are copied before returning); the raster runs on `st`.
-hipError_t paint_prims(float4 *dst, int W, int H, int pitch, const unsigned char *clear, const rc2dgi_prim *prims,
-                       int n, PaintBuffers &buf, hipStream_t st);
+// dst: W x H float4 render texture (pitch in texels), GL row order; u8: an RGBA8 texture (values
+// k * (1/255), 8-bit blends).  Synchronous w.r.t. the host arrays (they are copied before
+// returning); the raster runs on `st`.
+hipError_t paint_prims(float4 *dst, int W, int H, int pitch, bool u8, const unsigned char *clear,
+                       const rc2dgi_prim *prims, int n, PaintBuffers &buf, hipStream_t st);
 
 }  // namespace rc2dgi

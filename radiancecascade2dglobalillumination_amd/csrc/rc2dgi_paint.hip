@@ -16,6 +16,7 @@
 // A workgroup owns a 64 x 4 pixel tile: it first compacts (in order) the primitives whose
 // bounding box meets the tile into LDS, then each pixel walks that short list.
 #include "rc2dgi_paint.h"
+#include "rc2dgi_device.h"
 
 #include <algorithm>
 #include <climits>
@@ -47,7 +48,7 @@ constexpr int kPaintChunk = 1024;  // primitives compacted per pass of a workgro
 
 __global__ __launch_bounds__(256) void k_paint(float4 *__restrict__ dst, int W, int H, int pitch, int clear_on,
                                                float4 clear, const PaintPrim *__restrict__ prims, int n,
-                                               const PaintTri *__restrict__ tris) {
+                                               const PaintTri *__restrict__ tris, int u8) {
   __shared__ unsigned char flag[kPaintChunk];
   __shared__ int list[kPaintChunk];
   __shared__ int count;
@@ -92,11 +93,8 @@ __global__ __launch_bounds__(256) void k_paint(float4 *__restrict__ dst, int W, 
         }
         cov = ok;
       }
-      if (cov) {  // SRC_ALPHA, ONE_MINUS_SRC_ALPHA on all four channels (unfused)
-        const float a = p.color.w, ia = 1.0f - a;
-        v = make_float4(p.color.x * a + v.x * ia, p.color.y * a + v.y * ia, p.color.z * a + v.z * ia,
-                        p.color.w * a + v.w * ia);
-      }
+      if (cov)  // SRC_ALPHA, ONE_MINUS_SRC_ALPHA on all four channels (unfused; RGBA8: in 8 bits)
+        v = u8 ? GiU8::blend(p.color, v) : GiF32::blend(p.color, v);
     }
     __syncthreads();  // flag / list are rewritten by the next chunk
   }
@@ -149,7 +147,7 @@ void PaintBuffers::release() {
   prim_cap = tri_cap = 0;
 }
 
-hipError_t paint_prims(float4 *dst, int W, int H, int pitch, const unsigned char *clear, const rc2dgi_prim *in,
+hipError_t paint_prims(float4 *dst, int W, int H, int pitch, bool u8, const unsigned char *clear, const rc2dgi_prim *in,
                        int n, PaintBuffers &buf, hipStream_t st) {
   static const CircleTable tab;
   std::vector<PaintPrim> hp;
@@ -229,12 +227,15 @@ hipError_t paint_prims(float4 *dst, int W, int H, int pitch, const unsigned char
     e = hipMemcpyAsync(buf.edges, ht.data(), ht.size() * sizeof(PaintTri), hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return e;
   float4 cl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (clear)  // ClearBackground: rlClearColor(c / 255)
+  if (clear && u8)  // ClearBackground into RGBA8: the texel is c itself, read as c * (1/255)
+    cl = make_float4((float)clear[0] * kInv255, (float)clear[1] * kInv255, (float)clear[2] * kInv255,
+                     (float)clear[3] * kInv255);
+  else if (clear)  // ClearBackground: rlClearColor(c / 255)
     cl = make_float4((float)clear[0] / 255.0f, (float)clear[1] / 255.0f, (float)clear[2] / 255.0f,
                      (float)clear[3] / 255.0f);
   hipLaunchKernelGGL(k_paint, dim3((W + 63) / 64, (H + 3) / 4), dim3(256), 0, st, dst, W, H, pitch, clear ? 1 : 0,
                      cl, static_cast<const PaintPrim *>(buf.prims), (int)hp.size(),
-                     static_cast<const PaintTri *>(buf.edges));
+                     static_cast<const PaintTri *>(buf.edges), (int)u8);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   return hipStreamSynchronize(st);  // pageable host sources

@@ -128,7 +128,8 @@ class RC2DGI:
 
     def __init__(self, screen_width: int = 1200, screen_height: int = 900, cascade_count: int = 6,
                  render_scale: float = 1.0, ray_range: float = 2.0, device: int = 0, storage: str = "f32"):
-        """storage: "f32" (RGBA32F render textures) or "f16" (giRT1/2 as RGBA16F, RC2DGI.cs:105-106)."""
+        """storage: "f32" (RGBA32F render textures), "f16" (giRT1/2 as RGBA16F, RC2DGI.cs:105-106) or
+        "rgba8" (every render texture RGBA8 with GL unorm8 arithmetic -- the literal app)."""
         self._L = load_library()
         st = {"f32": 0, "rgba8": 1, "f16": 2}[storage]
         cfg = _Config(screen_width, screen_height, cascade_count, render_scale, ray_range, st, device,

@@ -4,7 +4,8 @@ DoRC2DGI: RenderScene RC2DGI.cs:224-264, RedrawSceneToRTs :528-545) rasterized b
 reference implementation available here (Mesa llvmpipe, oracle/_ref/glref --paint).
 
 Per case: W, H, clear colour (or none), primitive list (kind, x, y, w|radius, h, r, g, b, a) and
-the painted render texture (float32, GL row order).  Re-run: python tests/golden/make_paint_golden.py
+the painted render texture (float32, GL row order; ``__image_u8``: the same draws into an RGBA8
+texture, as texels).  Re-run: python tests/golden/make_paint_golden.py
 """
 from __future__ import annotations
 
@@ -71,6 +72,10 @@ def main():
                 f.write("\n".join(lines) + "\n")
             subprocess.run([GLREF, "--paint", cmd, "--w", str(W), "--h", str(H), "--out", d], check=True)
             img = np.fromfile(os.path.join(d, "paint.f32"), np.float32).reshape(H, W, 4)
+            # the same draws into an RGBA8 render texture (the literal app), as texels
+            subprocess.run([GLREF, "--paint", cmd, "--w", str(W), "--h", str(H), "--out", d, "--mode", "rgba8",
+                            "--dump-u8"], check=True)
+            data[name + "__image_u8"] = np.fromfile(os.path.join(d, "paint.u8"), np.uint8).reshape(H, W, 4)
             names.append(name)
             data[name + "__size"] = np.array([W, H], np.int32)
             data[name + "__clear"] = np.array(clear if clear is not None else (-1, -1, -1, -1), np.int32)

@@ -51,7 +51,7 @@ def _cfg(**kw):
 
 @pytest.mark.parametrize("kw,code", [
     (dict(screen_width=0), -1), (dict(screen_height=-3), -1), (dict(cascade_count=0), -1),
-    (dict(cascade_count=16), -1), (dict(render_scale=0.0), -1), (dict(storage=1), -5), (dict(storage=7), -1),
+    (dict(cascade_count=16), -1), (dict(render_scale=0.0), -1), (dict(storage=-1), -1), (dict(storage=7), -1),
 ])
 def test_create_validates_config_before_touching_the_device(lib, kw, code):
     h = ctypes.c_void_p()

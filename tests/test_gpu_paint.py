@@ -19,13 +19,17 @@ def R():
     return rc2dgi
 
 
+@pytest.mark.parametrize("storage", ["f32", "rgba8"])
 @pytest.mark.parametrize("case", list(paint_cases()), ids=lambda c: c[0])
-def test_paint_matches_llvmpipe(R, case):
-    name, W, H, clear, prims, want = case
-    ctx = R.RC2DGI(W, H, cascade_count=2)
+def test_paint_matches_llvmpipe(R, case, storage):
+    name, W, H, clear, prims, want, want_u8 = case
+    ctx = R.RC2DGI(W, H, cascade_count=2, storage=storage)
     ctx.upload("emissive", np.zeros((H, W, 4), np.float32))  # a fresh (zero) render texture
     ctx.paint("emissive", prims, clear)
-    got = ctx.download("emissive")
+    if storage == "rgba8":  # an RGBA8 render texture: compare the texels
+        got, want = ctx.download("emissive", np.uint8), want_u8
+    else:
+        got = ctx.download("emissive")
     assert np.array_equal(got, want), f"{name}: {np.count_nonzero(np.any(got != want, axis=-1))} texels differ"
     ctx.close()
 
@@ -51,19 +55,41 @@ def test_paint_random_and_many_prims(R):
     ctx.close()
 
 
-def test_painted_frame_equals_uploaded_frame(R):
+def test_paint_many_prims_rgba8(R):
+    """Translucent overlaps into RGBA8 textures: the 8-bit blend chain, against the restatement."""
+    rng = np.random.default_rng(12)
+    W, H = 200, 150
+    prims = []
+    for _ in range(600):
+        col = tuple(int(v) for v in rng.integers(0, 256, 4))
+        if rng.random() < 0.5:
+            prims.append((1, float(rng.uniform(0, W)), float(rng.uniform(0, H)), float(rng.uniform(0, 20)), 0.0) + col)
+        else:
+            prims.append((0, float(rng.uniform(-10, W)), float(rng.uniform(-10, H)), float(rng.uniform(0, 30)),
+                          float(rng.uniform(0, 30))) + col)
+    ctx = R.RC2DGI(W, H, cascade_count=3, storage="rgba8")
+    ctx.paint("color", prims, (3, 4, 5, 255))
+    got = ctx.download("color", np.uint8)
+    want = paint_ref.paint(W, H, prims, (3, 4, 5, 255), rgba8=True)
+    assert np.array_equal(got, want), np.count_nonzero(np.any(got != want, axis=-1))
+    ctx.close()
+
+
+@pytest.mark.parametrize("storage", ["f32", "rgba8"])
+def test_painted_frame_equals_uploaded_frame(R, storage):
     """Painting the demo scene on the device and uploading the same pixels give the same frame."""
     from radiancecascade2dglobalillumination_amd import scenes
 
     W = H = 512
     cc, cp, ec, ep = scenes.demo_prims(W, H)
-    a = R.RC2DGI(W, H, cascade_count=5, ray_range=2.0)
+    a = R.RC2DGI(W, H, cascade_count=5, ray_range=2.0, storage=storage)
     a.paint("color", cp, cc)
     a.paint("emissive", ep, ec)
     a.do_rc2dgi()
     a.sync()
-    b = R.RC2DGI(W, H, cascade_count=5, ray_range=2.0)
-    b.frame(paint_ref.paint(W, H, cp, cc), paint_ref.paint(W, H, ep, ec))
+    b = R.RC2DGI(W, H, cascade_count=5, ray_range=2.0, storage=storage)
+    u8 = storage == "rgba8"
+    b.frame(paint_ref.paint(W, H, cp, cc, rgba8=u8), paint_ref.paint(W, H, ep, ec, rgba8=u8))
     b.sync()
     assert np.array_equal(a.download("color"), b.download("color"))
     a.close()

@@ -43,9 +43,18 @@ def set_uniforms(ctx, p):
     ctx.set_shader_value("_BlurRadius", p.blur_radius)
 
 
+def storage_of(p):
+    return "rgba8" if p.rgba8 else ("f16" if p.gi_f16 else "f32")
+
+
+def mode_params(storage):
+    """oracle.Params keywords of a storage mode"""
+    return dict(gi_f16=storage == "f16", rgba8=storage == "rgba8")
+
+
 def run_hip(RC2DGI, p, color, emis, dir_tabs=None, sky=None, keep_levels=False):
     ctx = RC2DGI(p.W, p.H, cascade_count=p.N, render_scale=p.render_scale, ray_range=p.ray_range,
-                 storage="f16" if p.gi_f16 else "f32")
+                 storage=storage_of(p))
     set_uniforms(ctx, p)
     if dir_tabs is not None:
         off = 0
@@ -101,9 +110,14 @@ def test_fixture_with_reference_tables(RC2DGI, name):
         names.append("blur")
     pow2 = (p.W & (p.W - 1)) == 0 and (p.H & (p.H - 1)) == 0
     if pow2:
-        # the reference shaders' own outputs, bit for bit
+        # the reference shaders' own outputs, bit for bit (RGBA8 fixtures: the texels)
         alias = {"color": "color_out", "final_gi": "gi_final"}
         want = {k: fx[alias.get(k, k)] for k in names}
+        if p.rgba8:
+            got = {k: oracle.to_u8(got[k]) for k in names}
+            for k in names:
+                assert np.array_equal(got[k], want[k]), f"{name} vs llvmpipe:{k}: {np.count_nonzero(got[k] != want[k])}"
+            return
         assert_parity(got, want, names, exact=True, what=name + " vs llvmpipe")
     else:
         # llvmpipe interpolates fragTexCoord to within 1 ulp of (i+0.5)/n here; compare with the
@@ -123,6 +137,11 @@ def test_fixture_own_tables_vs_oracle(RC2DGI, name):
     names = ["color", "jump1", "jump2", "dist", "temp", "gi1", "gi2", "final_gi"] + [f"gi_L{L}" for L in range(p.N)]
     assert_parity(got, oracle_dict(fr), names, exact=True, what=name)
     # and the product stays within the reference's own branch-flip noise
+    if p.rgba8:  # in bytes: an ulp of cos/sin occasionally crosses a byte boundary
+        for n, g in (("final_gi", "gi_final"), ("color", "color_out")):
+            d = np.abs(oracle.to_u8(got[n]).astype(int) - fx[g])
+            assert np.mean(d == 0) >= 0.995 and d.max() <= 2, n
+        return
     for n, g in (("final_gi", "gi_final"), ("color", "color_out")):
         r = rel_err(got[n], fx[g])
         assert np.mean(r <= TOL) >= 0.995 and np.abs(got[n] - fx[g]).max() <= 5e-3, n
@@ -147,6 +166,14 @@ CONFIGS = [
     (256, 256, 5, 3.0, 1.0, dict(gi_f16=True), "demo"),
     (333, 200, 4, 2.0, 0.5, dict(gi_f16=True, blur_radius=1.37), "rand:41"),
     (128, 128, 3, 2.0, 1.0, dict(gi_f16=True, blur_radius=0.0, reflectivity=0.7), "rand:42"),
+    # every render texture RGBA8 (RC2DGI_STORAGE_RGBA8_COMPAT): float inputs quantized on upload
+    (256, 256, 5, 3.0, 1.0, dict(rgba8=True), "demo"),
+    (333, 200, 4, 2.0, 0.5, dict(rgba8=True, blur_radius=1.37), "rand:61"),
+    (128, 128, 3, 2.0, 1.0, dict(rgba8=True, blur_radius=0.0, reflectivity=0.7), "rand:62"),
+    (17, 5, 2, 2.0, 1.0, dict(rgba8=True), "rand:63"),
+    (1, 1, 1, 2.0, 1.0, dict(rgba8=True), "rand:64"),
+    (512, 512, 8, 64.0, 1.0, dict(rgba8=True, blur_radius=2.5), "rand:65"),
+    (1200, 900, 6, 2.0, 1.0, dict(rgba8=True), "demo"),  # the reference app itself (C1 knobs)
 ]
 
 
@@ -331,11 +358,11 @@ def test_timing_reports_passes(RC2DGI):
 
 @pytest.mark.parametrize("W,H,N,rr,scene", [(256, 192, 5, 2.0, "rand:40"), (333, 200, 4, 8.0, "demo"),
                                             (512, 512, 6, 2.0, "demo")])
-@pytest.mark.parametrize("storage", ["f32", "f16"])
+@pytest.mark.parametrize("storage", ["f32", "f16", "rgba8"])
 def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene, storage):
     """The tile-shape tuning knob changes the schedule only, never a result."""
     color, emis = make_scene(scene, W, H)
-    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr, gi_f16=storage == "f16"), color, emis,
+    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr, **mode_params(storage)), color, emis,
                       keep_levels=True)
     ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr, storage=storage)
     ctx.set_keep_levels(True)
@@ -363,10 +390,11 @@ def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene, storage):
     (256, 256, 0.5, 1.5),    # cascade 128^2 != screen: fixed taps, separate merge
     (200, 120, 1.0, 1.5),    # non-power-of-two: separate passes only
 ])
-@pytest.mark.parametrize("storage", ["f32", "f16"])
+@pytest.mark.parametrize("storage", ["f32", "f16", "rgba8"])
 def test_every_blur_path_matches_oracle(RC2DGI, W, H, rs, radius, storage):
-    """blur_path 0 (fixed taps + fused merge), 1 (LDS tile), 2 (separate passes): same bits."""
-    p = oracle.Params(W=W, H=H, N=3, ray_range=4.0, render_scale=rs, blur_radius=radius, gi_f16=storage == "f16")
+    """blur_path 0 (fixed taps + fused merge), 1 (LDS tile), 2 (separate passes): same bits
+    (RGBA8 runs the separate passes whatever the knob says)."""
+    p = oracle.Params(W=W, H=H, N=3, ray_range=4.0, render_scale=rs, blur_radius=radius, **mode_params(storage))
     color, emis = make_scene("rand:51", W, H)
     fr = oracle_dict(oracle.frame(p, color, emis))
     ctx = RC2DGI(W, H, cascade_count=3, render_scale=rs, ray_range=4.0, storage=storage)

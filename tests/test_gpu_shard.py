@@ -125,18 +125,20 @@ def test_phase_api_matches_do(R):
     c.close()
 
 
-def test_group_shards_f16_storage(R):
-    """RGBA16F cascades (RC2DGI_STORAGE_F16) shard the same way, bit for bit."""
+@pytest.mark.parametrize("storage", ["f16", "rgba8"])
+def test_group_shards_other_storage(R, storage):
+    """RGBA16F cascades (RC2DGI_STORAGE_F16) and RGBA8 render textures (RC2DGI_STORAGE_RGBA8_COMPAT)
+    shard the same way, bit for bit."""
     W, H, N = 512, 384, 5
     color, emis = _scene("rand:26", W, H)
-    whole = R.RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage="f16")
+    whole = R.RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
     whole.frame(color, emis)
     whole.sync()
     want = whole.download("color")
     whole.close()
     ctxs = []
     for k in range(3):
-        c = R.RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage="f16")
+        c = R.RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
         c.set_shard(k, 3)
         c.set_tuning("poison", 1)
         c.upload("color", color)
