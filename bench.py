@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 def b_rc(W, H, CW, CH, N, gi_bytes=16):
     """Algorithmic bytes of one RC pass: write G_L, read G_{L+1} once,
-    read the distance field once per level (gi_bytes = 8 with RGBA16F cascades)."""
+    read the distance field once per level (gi_bytes = 8 with RGBA16F cascades, 4 with RGBA8)."""
     return gi_bytes * CW * CH * (2 * N - 1) + 4 * W * H * N
 
 
@@ -276,8 +276,9 @@ def main():
                     help="scenes per GPU, one context + stream each (BASELINE configs[4] batch mode)")
     ap.add_argument("--mode", default="replicas", choices=("replicas", "strips"),
                     help="strips: one frame split into row strips over the ranks (BASELINE configs[3])")
-    ap.add_argument("--storage", default="f32", choices=("f32", "f16"),
-                    help="f16: giRT1/2 as RGBA16F (RC2DGI.cs:105-106, SURVEY 8 f4)")
+    ap.add_argument("--storage", default="f32", choices=("f32", "f16", "rgba8"),
+                    help="f16: giRT1/2 as RGBA16F (RC2DGI.cs:105-106, SURVEY 8 f4); rgba8: every render texture "
+                         "RGBA8 with GL unorm8 arithmetic, the literal app (SURVEY 8 f3)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="keep the default RC workgroup order (setup otherwise times the candidates per level)")
     ap.add_argument("--save-tuning", default="", help="write the chosen per-level rc_order / rc_variant (JSON)")
@@ -351,7 +352,7 @@ def main():
     t_rc, t_tot, wall = rdist.max_over_ranks([sum(rc_ms), sum(tot_ms), wall], device="cuda")
     units = CW * CH * N * a.steps * world
     value = units / (t_rc / 1e3) / 1e6
-    bytes_launch = b_rc(W, H, CW, CH, N, 8 if a.storage == "f16" else 16) / N
+    bytes_launch = b_rc(W, H, CW, CH, N, {"f32": 16, "f16": 8, "rgba8": 4}[a.storage]) / N
     avg_launch_s = (t_rc / 1e3) / (a.steps * N)
     achieved = bytes_launch / avg_launch_s / 1e9
     traffic = None
@@ -373,7 +374,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if a.storage == "f32" else "f32 (RGBA16F cascade storage)",
+        "dtype": {"f32": "f32", "f16": "f32 (RGBA16F cascade storage)",
+                  "rgba8": "f32 arithmetic, RGBA8 render textures (8-bit blends / filtering)"}[a.storage],
         "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
         "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}", "screen": [W, H],
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,

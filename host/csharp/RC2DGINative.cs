@@ -17,6 +17,7 @@ static unsafe class RC2DGINative
     public const int OK = 0;
     public enum RT { Color = 0, Emissive = 1, Jump1 = 2, Jump2 = 3, Dist = 4, GI1 = 5, GI2 = 6, Temp = 7, Blur = 8, FinalGI = 9 }
     public enum Format { RGBA8 = 0, RGBA32F = 1 }
+    public enum Storage { F32 = 0, RGBA8Compat = 1, F16 = 2 }  // RGBA8Compat: the shipped app's RGBA8 textures, byte-exact
 
     [StructLayout(LayoutKind.Sequential)]
     public struct Config
