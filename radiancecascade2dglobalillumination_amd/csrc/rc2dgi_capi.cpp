@@ -90,6 +90,7 @@ struct rc2dgi_ctx {
   int mpitch = 0;                               // mask row pitch (words)
   unsigned short *dist = nullptr;  // packUNorm16 q
   unsigned short *dist_t = nullptr;  // 8x8-tiled copy for the "t" RC variants
+  uint4 *dist_p = nullptr;           // packed copy for the "p" RC variants (k_dist_pack)
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
@@ -178,13 +179,14 @@ void free_buffers(rc2dgi_ctx *c) {
   c->rc_maps.clear();
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
-                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t};
+                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   c->color_in = c->emissive = c->temp = c->color_out = nullptr;
   c->jump1 = c->jump2 = nullptr;
   c->occ = nullptr;
   c->dist = c->dist_t = nullptr;
+  c->dist_p = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
   c->sky = nullptr;
@@ -230,6 +232,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->occ, (size_t)c->mpitch * c->H * sizeof(unsigned)));
   HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
+  HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
   const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
   HIPCHK(c, alloc(&c->gi1, nc * gsz));
   HIPCHK(c, alloc(&c->gi2, nc * gsz));
@@ -640,15 +643,21 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
   const bool T = c->timing;
-  // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362); the "t" variants read an 8x8-tiled copy
-  bool tiled = false;
-  for (int v : c->rc_variant) tiled |= rc_variant_tiled(v);
+  // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362).  The "t" / "p" / "o" variants read re-laid-out
+  // copies of distRT; building them is timed with the top level (it is RC work, not DistanceField's)
+  if (T) HIPCHK(c, hipEventRecord(c->ev_level[c->N], st));
+  bool tiled = false, packed = false;
+  for (int v : c->rc_variant) {
+    tiled |= rc_variant_tiled(v);
+    packed |= rc_variant_packed(v);
+  }
   if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
+  if (packed) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
     float4 *dstGI = gi1final ? c->gi2 : c->gi1;
-    if (T) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
+    if (T && L + 1 < c->N) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
     RcLevelArgs a;
     a.upper = (L == c->N - 1) ? nullptr : srcGI;
     a.out = dstGI;
@@ -667,6 +676,8 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.order_dg = c->rc_order[L] >> 16;
     a.map_cache = &c->rc_maps;
     a.dist_tiled = c->dist_t;
+    a.dist_packed = c->dist_p;
+
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
       a.p1 = r.second;
@@ -767,7 +778,8 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   const bool timing = c->timing;
   c->timing = true;
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
-  const int kVariants[] = {0, 13, 14, 15};  // march rolled / unrolled, linear / tiled distance field
+  // march rolled / unrolled x linear / 8x8-tiled / packed distance field; 32x8 tiles (x2 probes per lane)
+  const int kVariants[] = {0, 3, 6, 13, 14, 15, 16};
   const int nv = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
   std::vector<float> best(c->N, 1e30f);
   std::vector<int> pick(c->rc_order), pickv(c->rc_variant);

@@ -77,6 +77,7 @@ struct RcLevelArgs {
   int order_px = 0, order_py = 0, order_dg = 0;  // workgroup order (0: tile-major, direction-minor)
   RcMapCache *map_cache = nullptr;  // where the launch finds / builds its workgroup map
   const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
+  const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
 };
 
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
@@ -86,6 +87,12 @@ hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned shor
 int rc_variant_count();
 const char *rc_variant_name(int v);
 bool rc_variant_tiled(int v);  // reads the 8x8-tiled distance field
+bool rc_variant_packed(int v);  // reads the packed distance field
+
+// distRT -> packed 14-texel packets (16 B each: the minimum q + one excess byte per texel)
+size_t dist_packed_bytes(int W, int H);
+hipError_t launch_dist_pack(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st);
+
 
 // one RadianceCascades.fs level
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);

@@ -350,15 +350,59 @@ __device__ __forceinline__ int cvt_floor(float x) {
 // TILED: `dist` is the 8x8-tiled copy (k_dist_tile): one 128-byte line holds an 8x8 texel tile,
 // so the nearly parallel rays of a lane (and vertical-ish steps) share lines.
 // GI: storage of the cascade textures (GiF32 / GiF16 / GiU8, rc2dgi_device.h).
-template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, bool TILED, class GI>
+// the 16-bit distance q at byte offset `off` (32-bit offsets from the scalar base)
+__device__ __forceinline__ unsigned ld_dist(const unsigned short *dist, unsigned off) {
+  return *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + off);
+}
+
+// Packed distance field (DL = 2, k_dist_pack): one 16-byte packet per 14 texels of a row.  Bytes
+// 0-1 hold the packet's minimum q, byte 2 + t the excess q - min of texel t, or 255 (escape: read
+// the 16-bit field).  A distance field changes by at most 65535 / max(W, H) per texel plus the
+// jump flood's rare wrong seeds, so at 4096^2 the 13-texel span stays within 254 (measured: max
+// 234 over the demo and random scenes).  The 1.14 B/texel layout puts 112 texels of a row in one
+// 128-byte line instead of 64, and the field (19 MB at 4096^2 instead of 32 MB) fits the L2s better.
+constexpr int kPackTexels = 14;
+__host__ __device__ __forceinline__ int pack_per_row(int W) { return (W + kPackTexels - 1) / kPackTexels; }
+// ix / 14 for 0 <= ix < 16384 (37450 / 2^19 overestimates 1/14 by 2.3e-5: never crosses an integer)
+__device__ __forceinline__ unsigned pack_div14(unsigned ix) { return __umul24(ix, 37450u) >> 19; }
+__device__ __forceinline__ unsigned pack_byte(uint4 v, unsigned b) {  // byte b (0..15) of the packet
+  const unsigned long long h = b < 8u ? ((unsigned long long)v.y << 32 | v.x) : ((unsigned long long)v.w << 32 | v.z);
+  return (unsigned)(h >> ((b & 7u) * 8u)) & 0xFFu;
+}
+
+// one distance sample (q) of texel (ix, iy) = linear index idx, in layout DL
+template <int DL>
+__device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const uint4 *dpk, int tpr, int ix, int iy,
+                                            int idx) {
+  if constexpr (DL == 1) {
+    const unsigned t = ((__umul24((unsigned)iy >> 3, (unsigned)tpr) + ((unsigned)ix >> 3)) << 6) |
+                       (((unsigned)iy & 7u) << 3) | ((unsigned)ix & 7u);
+    return ld_dist(dist, t << 1);
+  } else if constexpr (DL == 2) {
+    const unsigned pk = pack_div14((unsigned)ix);
+    const uint4 v = dpk[__umul24((unsigned)iy, (unsigned)tpr) + pk];
+    const unsigned e = pack_byte(v, (unsigned)ix - pk * (unsigned)kPackTexels + 2u);
+    return e == 255u ? ld_dist(dist, (unsigned)idx << 1) : (v.x & 0xFFFFu) + e;
+  } else {
+    return ld_dist(dist, (unsigned)idx << 1);
+  }
+}
+
+// DL: distance-field layout the march reads: 0 pitch-linear uint16, 1 8x8-tiled (TILED), 2 packed
+// 14-texel row packets (`dpk`, see kPackTexels; power-of-two screens <= 16384).
+// Z0: level 0 on a power-of-two screen (t0 = 0): the first march iteration is shared by a probe's rays
+template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false>
 __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
                                                      const float4 *__restrict__ color,
                                                      const float4 *__restrict__ emis,
                                                      const float2 *__restrict__ dirs,
-                                                     const float4 *__restrict__ sky) {
+                                                     const float4 *__restrict__ sky,
+                                                     const uint4 *__restrict__ dpk) {
   constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
+  constexpr bool TILED = DL == 1, PACKED = DL == 2;
+  static_assert(!PACKED || P2S, "packed distance field: power-of-two screens only");
   // staged footprint: taps of c in [c0, c0+T) lie in [c0/2 - 1, c0/2 + T/2]
   constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
   constexpr int NSTAGE = ND * RH * RW;
@@ -438,7 +482,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
   for (int k = 0; k < NR; ++k) {
     t[k] = P.t0;
     hit_idx[k] = -1;
-    act[k] = pok[k / ND];
+    act[k] = pok[k / ND] && !(P.t0 > P.t1);  // act: the ray takes another sample (t <= t1 folded in)
   }
 #ifndef RC2DGI_DIAG_MAX_ITERS
 #define RC2DGI_DIAG_MAX_ITERS 32  // RadianceCascades.fs:64 (diagnostic builds may cap it; never shipped)
@@ -446,10 +490,42 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
 #ifdef RC2DGI_DIAG_STATS
   unsigned diag_slots = 0, diag_samples = 0;
 #endif
+  constexpr int it0 = Z0 ? 1 : 0;
+  if constexpr (Z0) {
+    // level 0 (t0 = 0): every ray of a probe starts at the probe centre, x = o + (0*dir)*asp = o
+    // exactly, so the first iteration is one shared sample per probe instead of one per ray
+#pragma unroll
+    for (int p = 0; p < PY; ++p) {
+      const bool live = act[p * ND] && __float_as_uint(ox) <= 0x3f800000u && __float_as_uint(oy[p]) <= 0x3f800000u;
+      int ix = cvt_floor(ox * P.sWf) & (P.s.W - 1);
+      int iy = cvt_floor(oy[p] * P.sHf) & (P.s.H - 1);
+      if (!live) ix = iy = 0;
+      const int idx = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
+      const float d = decode_dist(fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx));
+      const bool hit = live && d < 0.001f;
+#pragma unroll
+      for (int r = 0; r < ND; ++r) {
+        const int k = p * ND + r;
+        hit_idx[k] = hit ? idx : -1;
+        t[k] = live && !hit ? P.t0 + d : P.t0;
+        act[k] = live && !hit && !(t[k] > P.t1);
+      }
+#ifdef RC2DGI_DIAG_STATS
+      diag_samples += live ? (unsigned)ND : 0u;
+#endif
+    }
+#ifdef RC2DGI_DIAG_STATS
+    diag_slots += NR;
+#endif
+  }
+  bool more = false;  // a ray of this lane still marches
+#pragma unroll
+  for (int k = 0; k < NR; ++k) more |= act[k];
 #pragma unroll UNR
-  for (int it = 0; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
+  for (int it = it0; more && it < RC2DGI_DIAG_MAX_ITERS; ++it) {
     int idx[NR];
-    unsigned didx[NR];  // distance-field index (tiled or linear)
+    unsigned didx[NR];  // distance-field index (tiled or linear) or packet (packed)
+    unsigned psub[PACKED ? NR : 1];  // packed: byte of the texel in its packet
     bool live[NR];
     bool any_live = false;
 #pragma unroll
@@ -459,22 +535,26 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
       const float py = oy[p] + (t[k] * rdy[r]) * P.aspx;
       int ix, iy;
       if constexpr (P2S) {
-        live[k] = act[k] && !(t[k] > P.t1) && __float_as_uint(px) <= 0x3f800000u &&
-                  __float_as_uint(py) <= 0x3f800000u;
+        live[k] = act[k] && __float_as_uint(px) <= 0x3f800000u && __float_as_uint(py) <= 0x3f800000u;
         ix = cvt_floor(px * P.sWf) & (P.s.W - 1);
         iy = cvt_floor(py * P.sHf) & (P.s.H - 1);
       } else {
-        live[k] = act[k] && !(t[k] > P.t1 || px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+        live[k] = act[k] && !(px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
         ix = wrap_nearest(px, sax);
         iy = wrap_nearest(py, say);
       }
       if (!live[k]) ix = iy = 0;
       idx[k] = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;  // < 2^24 operands
-      if constexpr (TILED)
+      if constexpr (TILED) {
         didx[k] = ((__umul24((unsigned)iy >> 3, (unsigned)P.tpr) + ((unsigned)ix >> 3)) << 6) |
                   (((unsigned)iy & 7u) << 3) | ((unsigned)ix & 7u);
-      else
+      } else if constexpr (PACKED) {
+        const unsigned pk = pack_div14((unsigned)ix);
+        didx[k] = __umul24((unsigned)iy, (unsigned)P.tpr) + pk;  // packet
+        psub[k] = (unsigned)ix - pk * (unsigned)kPackTexels + 2u;  // its byte
+      } else {
         didx[k] = (unsigned)idx[k];
+      }
       act[k] = live[k];
       any_live |= live[k];
     }
@@ -484,17 +564,36 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
     for (int k = 0; k < NR; ++k) diag_samples += live[k] ? 1u : 0u;
 #endif
     unsigned q[NR];
+    if constexpr (PACKED) {
+      uint4 pv[NR];
 #pragma unroll
-    for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
-      q[k] = *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + (didx[k] << 1));
+      for (int k = 0; k < NR; ++k)  // dead rays re-read packet 0
+        pv[k] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(dpk) + (didx[k] << 4));
+      bool esc = false;
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        const unsigned e = pack_byte(pv[k], psub[k]);
+        q[k] = (pv[k].x & 0xFFFFu) + e;
+        esc |= e == 255u;
+      }
+      if (esc) {  // rare: some texel's excess did not fit a byte
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+          if (pack_byte(pv[k], psub[k]) == 255u) q[k] = ld_dist(dist, (unsigned)idx[k] << 1);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
+        q[k] = ld_dist(dist, didx[k] << 1);
+    }
     bool any = false;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {  // branch-free: selects, no exec-mask juggling
       const float d = decode_dist(q[k]);
       const bool hit = live[k] && d < 0.001f;
       hit_idx[k] = hit ? idx[k] : hit_idx[k];
-      act[k] = live[k] && !hit;
-      t[k] = act[k] ? t[k] + d : t[k];
+      t[k] = live[k] && !hit ? t[k] + d : t[k];
+      act[k] = live[k] && !hit && !(t[k] > P.t1);  // the next iteration's interval test, done now
       any |= act[k];
     }
     if (!any) break;
@@ -641,6 +740,39 @@ __global__ __launch_bounds__(256) void k_dist_tile(const unsigned short *__restr
   const uint4 v = *reinterpret_cast<const uint4 *>(dist + (size_t)j * pitch + seg * 8);
   *reinterpret_cast<uint4 *>(tiled + (((size_t)(j >> 3) * tpr + seg) << 6) + ((j & 7) << 3)) = v;
   (void)W;
+}
+
+// dist (pitch-linear) -> packed 14-texel packets (kPackTexels); one thread per packet, rows of ppr
+// packets.  Texel t of packet k is column 14k + t; columns past W repeat the packet's minimum.
+__global__ __launch_bounds__(256) void k_dist_pack(const unsigned short *__restrict__ dist, int pitch,
+                                                   uint4 *__restrict__ packed, int ppr, int W, int H) {
+  const int k = blockIdx.x * 256 + (int)threadIdx.x, j = blockIdx.y;
+  if (k >= ppr || j >= H) return;
+  const int x0 = k * kPackTexels;
+  // 14 texels = 7 aligned dwords (the row starts 128-byte aligned, a packet at 28k bytes)
+  const unsigned *src = reinterpret_cast<const unsigned *>(dist + (size_t)j * pitch + x0);
+  unsigned q[kPackTexels];
+#pragma unroll
+  for (int w = 0; w < kPackTexels / 2; ++w) {
+    const unsigned v = x0 + 2 * w < W ? src[w] : 0xFFFFFFFFu;
+    q[2 * w] = v & 0xFFFFu;
+    q[2 * w + 1] = v >> 16;
+  }
+  unsigned lo = q[0];
+#pragma unroll
+  for (int t = 1; t < kPackTexels; ++t)
+    if (x0 + t < W) lo = min(lo, q[t]);
+  unsigned b[16];
+  b[0] = lo & 0xFFu;
+  b[1] = lo >> 8;
+#pragma unroll
+  for (int t = 0; t < kPackTexels; ++t) b[2 + t] = x0 + t < W ? min(q[t] - lo, 255u) : 0u;
+  uint4 o;
+  o.x = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+  o.y = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+  o.z = b[8] | b[9] << 8 | b[10] << 16 | b[11] << 24;
+  o.w = b[12] | b[13] << 8 | b[14] << 16 | b[15] << 24;
+  packed[(size_t)j * ppr + k] = o;
 }
 
 // ---------------------------------------------------------------- Blur + copy-back
@@ -1015,8 +1147,13 @@ static const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles
   return e.dev;
 }
 
-template <int TX, int TY, int PY, int PD = 1, int UNR = 1, bool TILED = false, class GI = GiF32>
+template <int TX, int TY, int PY, int PD = 1, int UNR = 1, int DL = 0, class GI = GiF32>
 static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
+  const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
+  if constexpr (DL == 2) {  // packed field: power-of-two screens up to 16384 wide; same bits either way
+    if (!p2s || P.s.W > 16384) return launch_rc_tiles<TX, TY, PY, PD, UNR, 0, GI>(a, P, st);
+    if (!a.dist_packed) return hipErrorInvalidValue;
+  }
   P.tiles_x = ceil_div(P.bdx, TX);
   const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
   P.tiles_per_block = P.tiles_x * tiles_y;
@@ -1030,20 +1167,23 @@ static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t 
   // tile coordinates fit the map's 16-bit fields (<= 32768 probes per axis)
   P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, P.opx, P.opy, P.odg);
   if (!P.wg_map) return hipErrorOutOfMemory;
-  P.tpr = (P.s.W + 7) / 8;
-  if (TILED && !a.dist_tiled) return hipErrorInvalidValue;
+  P.tpr = DL == 2 ? pack_per_row(P.s.W) : (P.s.W + 7) / 8;
+  if (DL == 1 && !a.dist_tiled) return hipErrorInvalidValue;
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
-#define RC2DGI_RC(TOPV, P2V)                                                                                      \
-  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, TILED, GI>), dim3(nwg), dim3(TX * TY), 0, st, P,  \
-                     reinterpret_cast<const typename GI::T *>(a.upper), reinterpret_cast<typename GI::T *>(a.out),   \
-                     TILED ? a.dist_tiled : a.dist, a.color, a.emissive, a.dirs, a.sky)
-  const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
+#define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \
+  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL == 2 ? 0 : DL)), GI, Z0V>), \
+                     dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),   \
+                     reinterpret_cast<typename GI::T *>(a.out), DL == 1 ? a.dist_tiled : a.dist, a.color,     \
+                     a.emissive, a.dirs, a.sky, a.dist_packed)
   const bool top = a.level == a.N - 1;
   if (top) {
-    if (p2s) RC2DGI_RC(true, true); else RC2DGI_RC(true, false);
+    if (p2s) RC2DGI_RC(true, true, false); else RC2DGI_RC(true, false, false);
+  } else if (p2s) {
+    // level 0: t0 = CalculateRayRange's start 0 -> the shared first sample
+    if (a.level == 0 && P.t0 == 0.0f) RC2DGI_RC(false, true, true); else RC2DGI_RC(false, true, false);
   } else {
-    if (p2s) RC2DGI_RC(false, true); else RC2DGI_RC(false, false);
+    RC2DGI_RC(false, false, false);
   }
 #undef RC2DGI_RC
   return hipGetLastError();
@@ -1051,12 +1191,15 @@ static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t 
 
 // RC tile variants (tuning knob "rc_variant"): TXxTYxPY probes per workgroup, "dD" = D direction
 // blocks per workgroup (needs 4^level >= D; falls back to d1 below that)
-// ("u": march loop fully unrolled, "t": 8x8-tiled distance field)
+// ("u": march loop fully unrolled, "t": 8x8-tiled distance field, "p": packed distance field; the rolled
+// packed march was dropped: its GiF16 build gave run-to-run different results on gfx950)
 static const char *kRcVariantNames[] = {"16x16x1", "16x8x2",   "16x16x2",  "32x8x1",   "64x4x1",
                                         "8x8x1",   "32x8x2",   "16x16x1d2", "16x16x1d4", "16x8x1d2",
-                                        "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t"};
+                                        "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t",
+                                        "16x16x1up"};
 int rc_variant_count() { return (int)(sizeof(kRcVariantNames) / sizeof(kRcVariantNames[0])); }
 bool rc_variant_tiled(int v) { return v == 14 || v == 15; }
+bool rc_variant_packed(int v) { return v == 16; }
 const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
@@ -1090,20 +1233,22 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   hipError_t e = hipSuccess;
   if (c.gi_u8) {  // RGBA8 cascades: the 16x16x1 family only
     switch (a.variant) {
-      case 13: e = launch_rc_tiles<16, 16, 1, 1, 32, false, GiU8>(a, P, st); break;
-      case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, true, GiU8>(a, P, st); break;
-      case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, true, GiU8>(a, P, st); break;
-      default: e = launch_rc_tiles<16, 16, 1, 1, 1, false, GiU8>(a, P, st); break;
+      case 13: e = launch_rc_tiles<16, 16, 1, 1, 32, 0, GiU8>(a, P, st); break;
+      case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, 1, GiU8>(a, P, st); break;
+      case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, 1, GiU8>(a, P, st); break;
+      case 16: e = launch_rc_tiles<16, 16, 1, 1, 32, 2, GiU8>(a, P, st); break;
+      default: e = launch_rc_tiles<16, 16, 1, 1, 1, 0, GiU8>(a, P, st); break;
     }
     if (e != hipSuccess) return e;
     return hipGetLastError();
   }
   if (c.gi_f16) {  // RGBA16F cascades: the 16x16x1 family only
     switch (a.variant) {
-      case 13: e = launch_rc_tiles<16, 16, 1, 1, 32, false, GiF16>(a, P, st); break;
-      case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, true, GiF16>(a, P, st); break;
-      case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, true, GiF16>(a, P, st); break;
-      default: e = launch_rc_tiles<16, 16, 1, 1, 1, false, GiF16>(a, P, st); break;
+      case 13: e = launch_rc_tiles<16, 16, 1, 1, 32, 0, GiF16>(a, P, st); break;
+      case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, 1, GiF16>(a, P, st); break;
+      case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, 1, GiF16>(a, P, st); break;
+      case 16: e = launch_rc_tiles<16, 16, 1, 1, 32, 2, GiF16>(a, P, st); break;
+      default: e = launch_rc_tiles<16, 16, 1, 1, 1, 0, GiF16>(a, P, st); break;
     }
     if (e != hipSuccess) return e;
     return hipGetLastError();
@@ -1122,8 +1267,9 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
     case 11: e = nblk >= 4 ? launch_rc_tiles<16, 8, 1, 4>(a, P, st) : launch_rc_tiles<16, 8, 1>(a, P, st); break;
     case 12: e = nblk >= 4 ? launch_rc_tiles<8, 8, 1, 4>(a, P, st) : launch_rc_tiles<8, 8, 1>(a, P, st); break;
     case 13: e = launch_rc_tiles<16, 16, 1, 1, 32>(a, P, st); break;
-    case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, true>(a, P, st); break;
-    case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, true>(a, P, st); break;
+    case 14: e = launch_rc_tiles<16, 16, 1, 1, 32, 1>(a, P, st); break;
+    case 15: e = launch_rc_tiles<16, 16, 1, 1, 1, 1>(a, P, st); break;
+    case 16: e = launch_rc_tiles<16, 16, 1, 1, 32, 2>(a, P, st); break;
     default: e = launch_rc_tiles<16, 16, 1>(a, P, st); break;
   }
   if (e != hipSuccess) return e;
@@ -1257,6 +1403,15 @@ hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned shor
   const int tpr = (W + 7) / 8;
   hipLaunchKernelGGL(k_dist_tile, dim3(ceil_div(tpr, 64), ceil_div(H, 4)), dim3(256), 0, st, dist, pitch, tiled, tpr,
                      W, H);
+  return hipGetLastError();
+}
+
+size_t dist_packed_bytes(int W, int H) { return (size_t)pack_per_row(W) * H * sizeof(uint4); }
+
+
+hipError_t launch_dist_pack(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st) {
+  const int ppr = pack_per_row(W);
+  hipLaunchKernelGGL(k_dist_pack, dim3(ceil_div(ppr, 256), H), dim3(256), 0, st, dist, pitch, packed, ppr, W, H);
   return hipGetLastError();
 }
 
