@@ -645,6 +645,27 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
       lx0 = (int)fx - ((cx0 >> 1) - 1);
       ly0 = (int)fy - ((cy0 >> 1) - 1);
     }
+    // hit shading of the probe's rays (RadianceCascades.fs:79-86): every emissive load is issued
+    // before the first one is used, then the albedo loads of the non-emissive hits likewise (one
+    // round trip each instead of two per hit ray)
+    float4 hr[ND];
+#pragma unroll
+    for (int r = 0; r < ND; ++r) {
+      const int k = p * ND + r;
+      hr[r] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+      if (hit_idx[k] >= 0) {
+        const float4 e = emis[hit_idx[k]];
+        hr[r] = make_float4(e.x, e.y, e.z, 1.0f);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < ND; ++r) {
+      const int k = p * ND + r;
+      if (hit_idx[k] >= 0 && !(sqrtf(hr[r].x * hr[r].x + hr[r].y * hr[r].y + hr[r].z * hr[r].z) > 0.0f)) {
+        const float4 c = color[hit_idx[k]];
+        hr[r] = make_float4(c.x, c.y, c.z, P.reflectivity);
+      }
+    }
 #pragma unroll
     for (int dblk = 0; dblk < PD; ++dblk) {
       const int bi = bi0 + dblk;
@@ -652,17 +673,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
         const int r = dblk * 4 + r4;  // index into the 4*PD directions
-        const int k = p * ND + r;
-        float4 rad = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-        if (hit_idx[k] >= 0) {
-          const float4 e = emis[hit_idx[k]];
-          if (sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f) {
-            rad = make_float4(e.x, e.y, e.z, 1.0f);
-          } else {
-            const float4 c = color[hit_idx[k]];
-            rad = make_float4(c.x, c.y, c.z, P.reflectivity);
-          }
-        }
+        float4 rad = hr[r];
         const int ai = bi * 4 + r4;  // angleIndex
         if (rad.w != 0.0f) {
           if (!TOP) {
