@@ -392,7 +392,7 @@ def main():
                      "avg_launch_ms": round(avg_launch_s * 1e3, 5)},
     }
     line["inputs"] = input_costs(ctx, W, H, color, emis)
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the CPU leg: rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(W, H, N, a.ray_range, a.cpu_budget)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -61,6 +61,9 @@ if __name__ == "__main__":
         n = sys.argv[2] if len(sys.argv) > 2 else "6"
         print(build(force=True, verbose=True, extra=[f"-DRC2DGI_DIAG_MAX_ITERS={n}"],
                     out=os.path.join(HERE, f"librc2dgi_diag{n}.so")))
+    elif len(sys.argv) > 1 and sys.argv[1] == "nomerge":
+        # timing-only ablation build: RC levels without the upper-cascade staging and merge (WRONG results)
+        print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_NOMERGE"], out=os.path.join(HERE, "librc2dgi_nomerge.so")))
     elif len(sys.argv) > 1 and sys.argv[1] == "stats":
         # diagnostic build: march statistics per level (rc2dgi_diag_stats; atomics, slower)
         print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_STATS"], out=os.path.join(HERE, "librc2dgi_stats.so")))

@@ -406,8 +406,17 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
   // staged footprint: taps of c in [c0, c0+T) lie in [c0/2 - 1, c0/2 + T/2]
   constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
   constexpr int NSTAGE = ND * RH * RW;
-  constexpr int PT = (NSTAGE + NT - 1) / NT;
-  __shared__ typename GI::S s_up[TOP ? 1 : NSTAGE];
+  // staging assignment: wave w stages directions w, w + NW, ...; a lane the texels lane + 64 q of
+  // each, so the direction (and its footprint origin) is wave-uniform scalar arithmetic
+  constexpr int NW = NT / 64, DPW = ND / NW, FP = RH * RW, QPD = (FP + 63) / 64;
+  static_assert(NT % 64 == 0 && ND % NW == 0, "whole waves, whole directions per wave");
+  constexpr int PT = DPW * QPD;
+#ifdef RC2DGI_DIAG_NOMERGE
+  constexpr bool STG = false;  // timing-only ablation build: no upper staging, no merge (WRONG results)
+#else
+  constexpr bool STG = !TOP;  // stage and merge the level-(L+1) cascade
+#endif
+  __shared__ typename GI::S s_up[STG ? NSTAGE : 1];
 
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
   // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
@@ -426,31 +435,51 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
   // staged texels as plain 32-bit components (HIP's vector unions defeat SROA -> scratch); raw
   // storage bits, converted when written to LDS after the march
   constexpr int NWD = GI::kBytes / 4;  // 32-bit words per texel
-  unsigned stx[TOP ? 1 : PT], sty[(TOP || NWD < 2) ? 1 : PT], stz[(TOP || NWD < 4) ? 1 : PT],
-      stw[(TOP || NWD < 4) ? 1 : PT];
-  if (!TOP) {
+  unsigned stx[!STG ? 1 : PT], sty[(!STG || NWD < 2) ? 1 : PT], stz[(!STG || NWD < 4) ? 1 : PT],
+      stw[(!STG || NWD < 4) ? 1 : PT];
+  const int lane = (int)threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int yy0 = lane / RW, xx0 = lane - (lane / RW) * RW;
+  if (STG) {
 #pragma unroll
-    for (int q = 0; q < PT; ++q) {
-      // unconditional (clamped) loads keep the staging arrays in registers
-      const int k = min((int)threadIdx.x + q * NT, NSTAGE - 1);
-      const int r = k / (RH * RW), rem = k - r * (RH * RW);  // r indexes the 4*PD directions
-      const int yy = rem / RW, xx = rem - yy * RW;
+    for (int j = 0; j < DPW; ++j) {
+      const int r = wv + j * NW;  // direction (of the 4*PD) this wave stages
       const int a = bi0 * 4 + r;
-      int gx = (a & umask) * ubx + (cx0 >> 1) - 1 + xx;
-      int gy = (a >> ushift) * uby + (cy0 >> 1) - 1 + yy;
-      gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
-      gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
-      const typename GI::T v = upper[(size_t)gy * P.c.pitch + gx];  // issued now, consumed after the march
-      if constexpr (NWD == 1) {
-        stx[q] = v;
-      } else if constexpr (NWD == 2) {
-        stx[q] = v.x;
-        sty[q] = v.y;
-      } else {
-        stx[q] = __float_as_uint(v.x);
-        sty[q] = __float_as_uint(v.y);
-        stz[q] = __float_as_uint(v.z);
-        stw[q] = __float_as_uint(v.w);
+      const int bx = (a & umask) * ubx + (cx0 >> 1) - 1, by = (a >> ushift) * uby + (cy0 >> 1) - 1;
+      // REPEAT wrap only where the footprint crosses a texture edge (a wave-uniform branch)
+      const bool wrap = bx < 0 || bx + RW > P.c.CW || by < 0 || by + RH > P.c.CH;
+#pragma unroll
+      for (int q = 0; q < QPD; ++q) {
+        // texel e = lane + 64 q of the footprint: (yy, xx) from the lane's (yy0, xx0), clamped to
+        // the footprint (unconditional loads keep the staging arrays in registers)
+        int xx = xx0 + (64 * q) % RW, yy = yy0 + (64 * q) / RW;
+        if (xx >= RW) {
+          xx -= RW;
+          ++yy;
+        }
+        if (yy >= RH) {
+          yy = RH - 1;
+          xx = RW - 1;
+        }
+        int gx = bx + xx, gy = by + yy;
+        if (wrap) {
+          gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
+          gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
+        }
+        const unsigned off = __umul24((unsigned)gy, (unsigned)P.c.pitch) + (unsigned)gx;
+        const typename GI::T v = upper[off];  // issued now, consumed after the march
+        const int t = j * QPD + q;
+        if constexpr (NWD == 1) {
+          stx[t] = v;
+        } else if constexpr (NWD == 2) {
+          stx[t] = v.x;
+          sty[t] = v.y;
+        } else {
+          stx[t] = __float_as_uint(v.x);
+          sty[t] = __float_as_uint(v.y);
+          stz[t] = __float_as_uint(v.z);
+          stw[t] = __float_as_uint(v.w);
+        }
       }
     }
   }
@@ -606,17 +635,21 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
   }
 #endif
 
-  if (!TOP) {
+  if (STG) {
 #pragma unroll
-    for (int q = 0; q < PT; ++q) {
-      const int k = (int)threadIdx.x + q * NT;
-      if (k < NSTAGE) {
-        if constexpr (NWD == 1)
-          s_up[k] = GI::stage(stx[q], 0u, 0u, 0u);
-        else if constexpr (NWD == 2)
-          s_up[k] = GI::stage(stx[q], sty[q], 0u, 0u);
-        else
-          s_up[k] = GI::stage(stx[q], sty[q], stz[q], stw[q]);
+    for (int j = 0; j < DPW; ++j) {
+#pragma unroll
+      for (int q = 0; q < QPD; ++q) {
+        const int e = lane + 64 * q, t = j * QPD + q;
+        const int k = (wv + j * NW) * FP + e;
+        if (64 * (q + 1) <= FP || e < FP) {
+          if constexpr (NWD == 1)
+            s_up[k] = GI::stage(stx[t], 0u, 0u, 0u);
+          else if constexpr (NWD == 2)
+            s_up[k] = GI::stage(stx[t], sty[t], 0u, 0u);
+          else
+            s_up[k] = GI::stage(stx[t], sty[t], stz[t], stw[t]);
+        }
       }
     }
     __syncthreads();
@@ -675,7 +708,7 @@ __global__ __launch_bounds__(TX *TY) void k_rc_level(RcParams P, const typename 
         const int r = dblk * 4 + r4;  // index into the 4*PD directions
         float4 rad = hr[r];
         const int ai = bi * 4 + r4;  // angleIndex
-        if (rad.w != 0.0f) {
+        if (rad.w != 0.0f && (STG || TOP)) {
           if (!TOP) {
             typename GI::S t00, t10, t01, t11;
             float ux = wx, uy = wy;
