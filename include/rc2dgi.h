@@ -220,6 +220,12 @@ enum { RC2DGI_PLAN_JFA = 0, RC2DGI_PLAN_LEVEL = 1000, RC2DGI_PLAN_BLUR = 2000, R
 int rc2dgi_plan_rows(const rc2dgi_config *cfg, float blur_radius, int rank, int world, int pass, int *intervals,
                      int max_intervals);
 
+/* Schedule introspection (no GPU): the RC workgroup order `code` (tuning key rc_order_L<n>:
+ * px | py << 8 | dg << 16 | oriented << 24) over a grid of tiles_x x tiles_y probe tiles and ngrp
+ * direction groups.  Writes, for logical workgroups 0..n-1, the probe tile and direction group
+ * each one traces; returns 0, or a negative status for bad arguments. */
+int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int ngrp, int *tiles, int *groups, int n);
+
 #ifdef __cplusplus
 }
 #endif

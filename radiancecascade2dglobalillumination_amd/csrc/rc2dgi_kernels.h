@@ -55,6 +55,7 @@ bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTa
 struct RcMapCache {
   struct Entry {
     int nwg, tiles_x, tiles_y, ngrp, opx, opy, odg;
+    bool oriented;
     uint2 *dev;
   };
   std::vector<Entry> entries;
@@ -75,6 +76,7 @@ struct RcLevelArgs {
   int variant;           // tile shape (rc_variant_name)
   int p0 = 0, p1 = -1;   // probe rows [p0, p1) of every direction block (-1 = all)
   int order_px = 0, order_py = 0, order_dg = 0;  // workgroup order (0: tile-major, direction-minor)
+  bool order_oriented = false;                   // patches laid along the direction chunk's mean ray
   RcMapCache *map_cache = nullptr;  // where the launch finds / builds its workgroup map
   const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
@@ -83,6 +85,9 @@ struct RcLevelArgs {
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,
                             hipStream_t st);
+
+// rc_order code (px | py << 8 | dg << 16 | oriented << 24): logical workgroup -> (tile, group)
+int rc_order_logical_map(int code, int tiles_x, int tiles_y, int ngrp, int logical, int *tile, int *group);
 
 int rc_variant_count();
 const char *rc_variant_name(int v);

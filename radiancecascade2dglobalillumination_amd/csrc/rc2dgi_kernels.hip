@@ -294,8 +294,41 @@ __host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
 // workgroups an XCD runs together trace a few neighbouring tiles in a narrow fan of directions.
 // Patches of opx x opy tiles cover the tile grid row by row; the last patch row / column may be
 // partial (w x h tiles), which keeps the map a bijection for any grid.
+// Oriented orders (`oriented`, order code bit 24): for chunk of odg direction groups: for patch:
+// for tile in patch: for group in chunk.  A patch is opx tiles along the chunk's mean ray
+// direction and opy across it (axis-aligned: opx wide for directions within 45 degrees of the x
+// axis, opx tall otherwise), so the rays of an XCD's resident workgroups sweep a band along
+// their own direction and their distance samples share that XCD's L2.
+__host__ __device__ __forceinline__ void rc_order_map_oriented(int logical, int tiles_x, int tiles_y, int ngrp,
+                                                               int opx, int opy, int odg, int &tile, int &dgi) {
+  const int per_chunk = tiles_x * tiles_y * odg;
+  const int ch = logical / per_chunk;
+  const int rk = logical - ch * per_chunk;
+  const int tr = rk / odg, gi = rk - tr * odg;  // tile rank in the chunk, group in the chunk
+  // mean direction of the chunk: group g covers angles 2 pi [g, g+1) / ngrp
+  const float th = 6.28318530718f * ((float)ch * (float)odg + 0.5f * (float)odg) / (float)ngrp;
+  const bool along_x = fabsf(cosf(th)) >= fabsf(sinf(th));
+  const int px = along_x ? opx : opy, py = along_x ? opy : opx;
+  const int prow = tiles_x * py;  // tiles in a full patch row
+  const int pr = tr / prow;
+  int r = tr - pr * prow;
+  const int h = min(py, tiles_y - pr * py);
+  int pc = r / (px * h);
+  const int nfull = tiles_x / px;
+  if (pc > nfull) pc = nfull;  // the partial last column
+  r -= pc * px * h;
+  const int w = min(px, tiles_x - pc * px);
+  const int iy = r / w, ix = r - iy * w;
+  tile = (pr * py + iy) * tiles_x + pc * px + ix;
+  dgi = ch * odg + gi;
+}
+
 __host__ __device__ __forceinline__ void rc_order_map(int logical, int tiles_x, int tiles_y, int ngrp, int opx,
-                                                      int opy, int odg, int &tile, int &dgi) {
+                                                      int opy, int odg, int &tile, int &dgi, bool oriented = false) {
+  if (odg > 0 && oriented) {
+    rc_order_map_oriented(logical, tiles_x, tiles_y, ngrp, opx, opy, odg, tile, dgi);
+    return;
+  }
   if (odg <= 0) {
     tile = logical / ngrp;
     dgi = logical - tile * ngrp;
@@ -1169,20 +1202,20 @@ void RcMapCache::clear() {
 
 // the host-built workgroup map for one launch geometry (built once, then reused)
 static const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int ngrp, int opx, int opy,
-                              int odg) {
+                              int odg, bool oriented) {
   if (!cache) return nullptr;
   for (auto &e : cache->entries)
     if (e.nwg == nwg && e.tiles_x == tiles_x && e.tiles_y == tiles_y && e.ngrp == ngrp && e.opx == opx &&
-        e.opy == opy && e.odg == odg)
+        e.opy == opy && e.odg == odg && e.oriented == oriented)
       return e.dev;
   std::vector<uint2> m(nwg);
   for (int p = 0; p < nwg; ++p) {
     int tile, dgi;
-    rc_order_map(xcd_logical_id(p, nwg), tiles_x, tiles_y, ngrp, opx, opy, odg, tile, dgi);
+    rc_order_map(xcd_logical_id(p, nwg), tiles_x, tiles_y, ngrp, opx, opy, odg, tile, dgi, oriented);
     const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
     m[p] = make_uint2((unsigned)tx | ((unsigned)ty << 16), (unsigned)dgi);
   }
-  RcMapCache::Entry e{nwg, tiles_x, tiles_y, ngrp, opx, opy, odg, nullptr};
+  RcMapCache::Entry e{nwg, tiles_x, tiles_y, ngrp, opx, opy, odg, oriented, nullptr};
   if (hipMalloc(reinterpret_cast<void **>(&e.dev), (size_t)nwg * sizeof(uint2)) != hipSuccess) return nullptr;
   if (hipMemcpy(e.dev, m.data(), (size_t)nwg * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipFree(e.dev);
@@ -1210,7 +1243,7 @@ static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t 
   const int ngrp = P.bsc * P.bsc / PD;
   if (P.odg <= 0 || P.opx <= 0 || P.opy <= 0 || ngrp % P.odg) P.opx = P.opy = P.odg = 0;
   // tile coordinates fit the map's 16-bit fields (<= 32768 probes per axis)
-  P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, P.opx, P.opy, P.odg);
+  P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, P.opx, P.opy, P.odg, a.order_oriented && P.odg > 0);
   if (!P.wg_map) return hipErrorOutOfMemory;
   P.tpr = DL == 2 ? pack_per_row(P.s.W) : (P.s.W + 7) / 8;
   if (DL == 1 && !a.dist_tiled) return hipErrorInvalidValue;
@@ -1449,6 +1482,14 @@ hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned shor
   hipLaunchKernelGGL(k_dist_tile, dim3(ceil_div(tpr, 64), ceil_div(H, 4)), dim3(256), 0, st, dist, pitch, tiled, tpr,
                      W, H);
   return hipGetLastError();
+}
+
+int rc_order_logical_map(int code, int tiles_x, int tiles_y, int ngrp, int logical, int *tile, int *group) {
+  int opx = code & 0xFF, opy = (code >> 8) & 0xFF, odg = (code >> 16) & 0xFF;
+  const bool oriented = (code >> 24) & 1;
+  if (odg <= 0 || opx <= 0 || opy <= 0 || ngrp % odg) opx = opy = odg = 0;
+  rc_order_map(logical, tiles_x, tiles_y, ngrp, opx, opy, odg, *tile, *group, oriented && odg > 0);
+  return 0;
 }
 
 size_t dist_packed_bytes(int W, int H) { return (size_t)pack_per_row(W) * H * sizeof(uint4); }
