@@ -322,7 +322,7 @@ def main():
             ctx.set_tuning(f"rc_variant_L{L}", tun["rc_variant"][L])
         orders = tun["rc_order"]
     else:
-        orders = None if a.no_autotune else ctx.autotune(2)  # setup: schedule choice, results identical
+        orders = None if a.no_autotune else ctx.autotune(3)  # setup: schedule choice, results identical
     variants = [ctx.get_tuning(f"rc_variant_L{L}") for L in range(N)]
     orders = [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)] if orders else None
     if a.save_tuning and rank == 0:

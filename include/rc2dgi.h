@@ -221,10 +221,12 @@ int rc2dgi_plan_rows(const rc2dgi_config *cfg, float blur_radius, int rank, int 
                      int max_intervals);
 
 /* Schedule introspection (no GPU): the RC workgroup order `code` (tuning key rc_order_L<n>:
- * px | py << 8 | dg << 16 | oriented << 24) over a grid of tiles_x x tiles_y probe tiles and ngrp
- * direction groups.  Writes, for logical workgroups 0..n-1, the probe tile and direction group
- * each one traces; returns 0, or a negative status for bad arguments. */
-int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int ngrp, int *tiles, int *groups, int n);
+ * px | py << 8 | dg << 16 | mode << 24, mode 0 patches, 1 oriented patches, 2 bands along the
+ * rays) over a grid of tiles_x x tiles_y probe tiles of tile_w x tile_h probes and ngrp direction
+ * groups.  Writes, for logical workgroups 0..n-1, the probe tile and direction group each one
+ * traces; returns 0, or a negative status for bad arguments. */
+int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
+                      int n);
 
 #ifdef __cplusplus
 }

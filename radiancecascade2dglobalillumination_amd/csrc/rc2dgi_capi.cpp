@@ -201,7 +201,8 @@ hipError_t alloc(T **p, size_t bytes) {
 // gather-bound levels prefer the fully unrolled march ("16x16x1u")
 int default_rc_variant(int level) { return level >= 3 ? 13 : 0; }
 
-inline int order_code(int px, int py, int dg, int oriented = 0) { return px | (py << 8) | (dg << 16) | (oriented << 24); }
+// mode: 0 patches, 1 oriented patches, 2 bands along the rays (rc_logical_order)
+inline int order_code(int px, int py, int dg, int mode = 0) { return px | (py << 8) | (dg << 16) | (mode << 24); }
 
 // default workgroup order per level (scripts/sweep_rc_order.py, profiles/r01/rc_order_*.json):
 // from level 3 up, patches of 2 x 2 tiles x 8 direction blocks keep the distance-field
@@ -210,12 +211,16 @@ int default_rc_order(int level) { return level >= 3 ? order_code(2, 2, 8) : 0; }
 
 // rc2dgi_autotune candidates (px, py, dg); the library falls back to tile-major per level where
 // a candidate does not tile the grid
-// (oriented candidates, 4th field 1: px tiles along the chunk's mean ray direction, py across)
+// (4th field: 1 oriented patches, px tiles along the chunk's mean ray direction, py across;
+// 2 bands py tiles wide along the chunk's mean ray direction, rc_logical_order)
 const int kOrderCandidates[][4] = {{0, 0, 0, 0},  {2, 2, 8, 0},  {4, 4, 4, 0},   {2, 4, 4, 0},  {2, 8, 8, 0},
                                    {2, 16, 16, 0}, {1, 16, 16, 0}, {1, 16, 32, 0}, {1, 32, 16, 0}, {1, 4, 64, 0},
                                    {2, 8, 16, 0},  {4, 8, 4, 0},   {1, 8, 8, 0},   {2, 2, 16, 0},  {4, 2, 32, 0},
                                    {1, 4, 16, 0},  {16, 1, 16, 1}, {16, 2, 8, 1},  {8, 2, 16, 1},  {16, 1, 32, 1},
-                                   {8, 1, 32, 1},  {32, 1, 8, 1},  {8, 4, 8, 1},   {4, 2, 32, 1}};
+                                   {8, 1, 32, 1},  {32, 1, 8, 1},  {8, 4, 8, 1},   {4, 2, 32, 1},  {1, 1, 16, 2},
+                                   {1, 1, 32, 2},  {1, 2, 8, 2},   {1, 2, 16, 2},  {1, 4, 4, 2},   {1, 4, 8, 2},
+                                   {1, 1, 8, 2},   {1, 2, 32, 2},  {1, 1, 4, 2},   {1, 2, 4, 2},   {1, 4, 2, 2},
+                                   {1, 8, 4, 2},   {1, 1, 64, 2},  {1, 2, 64, 2},  {1, 1, 128, 2}, {1, 8, 8, 2}};
 
 // (re)allocate every render texture for the current W, H, N (RC2DGI.cs:79-98)
 int allocate(rc2dgi_ctx *c) {
@@ -674,10 +679,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.ray_range = c->ray_range;
     a.reflectivity = c->reflectivity;
     a.variant = c->rc_variant[L];
-    a.order_px = c->rc_order[L] & 0xFF;
-    a.order_py = (c->rc_order[L] >> 8) & 0xFF;
-    a.order_dg = (c->rc_order[L] >> 16) & 0xFF;
-    a.order_oriented = (c->rc_order[L] >> 24) & 1;
+    a.order_code = c->rc_order[L];
     a.map_cache = &c->rc_maps;
     a.dist_tiled = c->dist_t;
     a.dist_packed = c->dist_p;
@@ -930,11 +932,12 @@ int rc2dgi_device_buffer(rc2dgi_ctx *c, int which, void **dev, int *pitch_bytes)
   return RC2DGI_OK;
 }
 
-int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int ngrp, int *tiles, int *groups, int n) {
-  if (tiles_x <= 0 || tiles_y <= 0 || ngrp <= 0 || n < 0 || n > tiles_x * tiles_y * ngrp || (n && (!tiles || !groups)))
+int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
+                      int n) {
+  if (tiles_x <= 0 || tiles_y <= 0 || tile_w <= 0 || tile_h <= 0 || ngrp <= 0 || n < 0 ||
+      n > tiles_x * tiles_y * ngrp || (n && (!tiles || !groups)))
     return RC2DGI_E_ARG;
-  for (int q = 0; q < n; ++q) rc_order_logical_map(code, tiles_x, tiles_y, ngrp, q, &tiles[q], &groups[q]);
-  return RC2DGI_OK;
+  return rc_order_plan(code, tiles_x, tiles_y, tile_w, tile_h, ngrp, tiles, groups, n);
 }
 
 int rc2dgi_plan_rows(const rc2dgi_config *cfg, float blur_radius, int rank, int world, int pass, int *intervals,

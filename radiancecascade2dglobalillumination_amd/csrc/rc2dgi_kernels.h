@@ -54,8 +54,7 @@ bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTa
 // device copies of the host-built workgroup maps of k_rc_level, one per launch geometry
 struct RcMapCache {
   struct Entry {
-    int nwg, tiles_x, tiles_y, ngrp, opx, opy, odg;
-    bool oriented;
+    int nwg, tiles_x, tiles_y, ngrp, code, tile_w, tile_h;
     uint2 *dev;
   };
   std::vector<Entry> entries;
@@ -75,8 +74,7 @@ struct RcLevelArgs {
   float ray_range, reflectivity;
   int variant;           // tile shape (rc_variant_name)
   int p0 = 0, p1 = -1;   // probe rows [p0, p1) of every direction block (-1 = all)
-  int order_px = 0, order_py = 0, order_dg = 0;  // workgroup order (0: tile-major, direction-minor)
-  bool order_oriented = false;                   // patches laid along the direction chunk's mean ray
+  int order_code = 0;  // workgroup order, tuning rc_order_L<n> (0: tile-major, direction-minor)
   RcMapCache *map_cache = nullptr;  // where the launch finds / builds its workgroup map
   const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
@@ -86,8 +84,10 @@ struct RcLevelArgs {
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,
                             hipStream_t st);
 
-// rc_order code (px | py << 8 | dg << 16 | oriented << 24): logical workgroup -> (tile, group)
-int rc_order_logical_map(int code, int tiles_x, int tiles_y, int ngrp, int logical, int *tile, int *group);
+// rc_order code (px | py << 8 | dg << 16 | oriented << 24 | banded << 25): logical workgroups
+// 0..n-1 -> (tile, direction group), tiles of tile_w x tile_h probes
+int rc_order_plan(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
+                  int n);
 
 int rc_variant_count();
 const char *rc_variant_name(int v);

@@ -25,6 +25,8 @@
 #include "rc2dgi_device.h"
 #include "rc2dgi_kernels.h"
 
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 namespace rc2dgi {
@@ -1200,22 +1202,63 @@ void RcMapCache::clear() {
   entries.clear();
 }
 
-// the host-built workgroup map for one launch geometry (built once, then reused)
-static const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int ngrp, int opx, int opy,
-                              int odg, bool oriented) {
+// Logical workgroup order of one launch geometry: (tile, direction group) per logical id.
+// code = px | py << 8 | dg << 16 | oriented << 24 | banded << 25 (an invalid patch or group size
+// falls back to tile-major).  Banded orders (bit 25): for chunk of dg direction groups: tiles
+// sorted by (band across the chunk's mean ray direction, position along it), bands py tile
+// widths wide -- the rays of consecutive workgroups sweep one band along their own direction,
+// at any angle.  tile_w x tile_h: a tile's size in probes (the bands are isotropic in probes).
+static std::vector<uint2> rc_logical_order(int code, int tiles_x, int tiles_y, int ngrp, int tile_w, int tile_h) {
+  int opx = code & 0xFF, opy = (code >> 8) & 0xFF, odg = (code >> 16) & 0xFF;
+  const bool oriented = (code >> 24) & 1, banded = (code >> 25) & 1;
+  if (odg <= 0 || opx <= 0 || opy <= 0 || ngrp % odg) opx = opy = odg = 0;
+  const int ntiles = tiles_x * tiles_y, n = ntiles * ngrp;
+  std::vector<uint2> out(n);
+  if (odg > 0 && banded) {
+    const double band = (double)opy * std::sqrt((double)tile_w * (double)tile_h);
+    std::vector<std::pair<std::pair<long long, double>, int>> key(ntiles);
+    int q = 0;
+    for (int ch = 0; ch < ngrp / odg; ++ch) {
+      const double th = 6.283185307179586 * ((double)ch * odg + 0.5 * odg) / (double)ngrp;
+      const double c = std::cos(th), sn = std::sin(th);
+      for (int t = 0; t < ntiles; ++t) {
+        const int ty = t / tiles_x, tx = t - ty * tiles_x;
+        const double x = (tx + 0.5) * tile_w, y = (ty + 0.5) * tile_h;
+        const double u = x * c + y * sn, v = -x * sn + y * c;
+        key[t] = {{(long long)std::floor(v / band), u}, t};
+      }
+      std::sort(key.begin(), key.end());
+      for (int t = 0; t < ntiles; ++t)
+        for (int gi = 0; gi < odg; ++gi) out[q++] = make_uint2((unsigned)key[t].second, (unsigned)(ch * odg + gi));
+    }
+    return out;
+  }
+  for (int l = 0; l < n; ++l) {
+    int tile, dgi;
+    rc_order_map(l, tiles_x, tiles_y, ngrp, opx, opy, odg, tile, dgi, oriented && odg > 0);
+    out[l] = make_uint2((unsigned)tile, (unsigned)dgi);
+  }
+  return out;
+}
+
+// the host-built workgroup map for one launch geometry (built once, then reused): physical
+// workgroup -> XCD chunk of the logical order (xcd_logical_id) -> (tile x | y << 16, group)
+static const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int ngrp, int code, int tile_w,
+                              int tile_h) {
   if (!cache) return nullptr;
   for (auto &e : cache->entries)
-    if (e.nwg == nwg && e.tiles_x == tiles_x && e.tiles_y == tiles_y && e.ngrp == ngrp && e.opx == opx &&
-        e.opy == opy && e.odg == odg && e.oriented == oriented)
+    if (e.nwg == nwg && e.tiles_x == tiles_x && e.tiles_y == tiles_y && e.ngrp == ngrp && e.code == code &&
+        e.tile_w == tile_w && e.tile_h == tile_h)
       return e.dev;
+  const std::vector<uint2> lo = rc_logical_order(code, tiles_x, tiles_y, ngrp, tile_w, tile_h);
+  if ((int)lo.size() != nwg) return nullptr;
   std::vector<uint2> m(nwg);
   for (int p = 0; p < nwg; ++p) {
-    int tile, dgi;
-    rc_order_map(xcd_logical_id(p, nwg), tiles_x, tiles_y, ngrp, opx, opy, odg, tile, dgi, oriented);
-    const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-    m[p] = make_uint2((unsigned)tx | ((unsigned)ty << 16), (unsigned)dgi);
+    const uint2 v = lo[xcd_logical_id(p, nwg)];
+    const int ty = (int)v.x / tiles_x, tx = (int)v.x - ty * tiles_x;
+    m[p] = make_uint2((unsigned)tx | ((unsigned)ty << 16), v.y);
   }
-  RcMapCache::Entry e{nwg, tiles_x, tiles_y, ngrp, opx, opy, odg, oriented, nullptr};
+  RcMapCache::Entry e{nwg, tiles_x, tiles_y, ngrp, code, tile_w, tile_h, nullptr};
   if (hipMalloc(reinterpret_cast<void **>(&e.dev), (size_t)nwg * sizeof(uint2)) != hipSuccess) return nullptr;
   if (hipMemcpy(e.dev, m.data(), (size_t)nwg * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipFree(e.dev);
@@ -1236,14 +1279,10 @@ static hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t 
   const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
   P.tiles_per_block = P.tiles_x * tiles_y;
   const int nwg = P.tiles_per_block * P.bsc * P.bsc / PD;
-  // workgroup order (tuning "rc_order"): only when patches and groups tile the grid exactly
-  P.opx = a.order_px;
-  P.opy = a.order_py;
-  P.odg = a.order_dg;
+  // workgroup order (tuning "rc_order", rc_logical_order); tile coordinates fit the map's
+  // 16-bit fields (<= 32768 probes per axis)
   const int ngrp = P.bsc * P.bsc / PD;
-  if (P.odg <= 0 || P.opx <= 0 || P.opy <= 0 || ngrp % P.odg) P.opx = P.opy = P.odg = 0;
-  // tile coordinates fit the map's 16-bit fields (<= 32768 probes per axis)
-  P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, P.opx, P.opy, P.odg, a.order_oriented && P.odg > 0);
+  P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, a.order_code, TX, TY * PY);
   if (!P.wg_map) return hipErrorOutOfMemory;
   P.tpr = DL == 2 ? pack_per_row(P.s.W) : (P.s.W + 7) / 8;
   if (DL == 1 && !a.dist_tiled) return hipErrorInvalidValue;
@@ -1484,11 +1523,13 @@ hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned shor
   return hipGetLastError();
 }
 
-int rc_order_logical_map(int code, int tiles_x, int tiles_y, int ngrp, int logical, int *tile, int *group) {
-  int opx = code & 0xFF, opy = (code >> 8) & 0xFF, odg = (code >> 16) & 0xFF;
-  const bool oriented = (code >> 24) & 1;
-  if (odg <= 0 || opx <= 0 || opy <= 0 || ngrp % odg) opx = opy = odg = 0;
-  rc_order_map(logical, tiles_x, tiles_y, ngrp, opx, opy, odg, *tile, *group, oriented && odg > 0);
+int rc_order_plan(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
+                  int n) {
+  const std::vector<uint2> lo = rc_logical_order(code, tiles_x, tiles_y, ngrp, tile_w, tile_h);
+  for (int q = 0; q < n && q < (int)lo.size(); ++q) {
+    tiles[q] = (int)lo[q].x;
+    groups[q] = (int)lo[q].y;
+  }
   return 0;
 }
 

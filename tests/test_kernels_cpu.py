@@ -96,19 +96,19 @@ def test_jfa_scaled_float_key_matches_shader_distance():
         assert np.array_equal(got, want), (W, H)
 
 
-def _plan_order(lib, code, tx, ty, ng):
+def _plan_order(lib, code, tx, ty, ng, tw=16, th=16):
     import ctypes
 
     n = tx * ty * ng
     tiles, groups = (ctypes.c_int * n)(), (ctypes.c_int * n)()
-    assert lib.rc2dgi_plan_order(code, tx, ty, ng, tiles, groups, n) == 0
+    assert lib.rc2dgi_plan_order(code, tx, ty, tw, th, ng, tiles, groups, n) == 0
     return list(zip(tiles, groups))
 
 
 def test_rc_workgroup_order_is_a_bijection():
     """Every (tile, direction group) is visited exactly once for any grid, partial patches
     included (row-strip shards give tile grids the patches do not divide), for the plain and
-    the direction-oriented orders (the library's own host map, rc2dgi_plan_order)."""
+    the direction-oriented / banded orders (the library's own host map, rc2dgi_plan_order)."""
     import itertools
 
     from radiancecascade2dglobalillumination_amd import _build, load_library
@@ -116,7 +116,7 @@ def test_rc_workgroup_order_is_a_bijection():
     _build.build()
     lib = load_library()
     for tx, ty, ng, px, py, dg, ori in itertools.product([1, 3, 5, 16], [1, 2, 5, 7, 16], [1, 4, 16],
-                                                         [1, 2, 3, 4, 16], [1, 2, 4, 5], [1, 2, 4, 16], [0, 1]):
+                                                         [1, 2, 3, 4, 16], [1, 2, 4, 5], [1, 2, 4, 16], [0, 1, 2]):
         if ng % dg:
             continue
         code = px | py << 8 | dg << 16 | ori << 24
@@ -138,3 +138,26 @@ def test_oriented_order_lays_patches_along_the_rays():
     q = 2 * 256  # chunk 1, mean angle 2 pi * 3/16 (67.5 deg)
     second = [t for t, _ in m[q:q + 16 * 2:2]]
     assert second == [16 * i for i in range(16)]  # one tile column
+
+
+def test_banded_order_follows_the_rays():
+    """Banded order: within a chunk of direction groups, consecutive tiles advance along the
+    chunk's mean ray direction inside a band across it (here 45 degrees: the diagonal)."""
+    import math
+
+    from radiancecascade2dglobalillumination_amd import _build, load_library
+
+    _build.build()
+    lib = load_library()
+    ng, dg = 8, 1  # chunk 1 of 8: mean angle 2 pi * 1.5 / 8 = 67.5 deg; chunk 0: 22.5 deg
+    m = _plan_order(lib, 1 | 1 << 8 | dg << 16 | 2 << 24, 16, 16, ng)
+    for ch in (0, 1):
+        th = 2 * math.pi * (ch + 0.5) / ng
+        seq = [t for t, g in m[ch * 256:(ch + 1) * 256]]
+        assert all(g == ch for _, g in m[ch * 256:(ch + 1) * 256])
+        us = [((t % 16) + 0.5) * math.cos(th) + ((t // 16) + 0.5) * math.sin(th) for t in seq]
+        vs = [math.floor((-((t % 16) + 0.5) * math.sin(th) + ((t // 16) + 0.5) * math.cos(th))) for t in seq]
+        # bands in order, positions along the ray increasing inside each band
+        assert vs == sorted(vs)
+        for a, b, va, vb in zip(us, us[1:], vs, vs[1:]):
+            assert va != vb or a <= b
