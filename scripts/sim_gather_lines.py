@@ -39,6 +39,12 @@ def line_ids(ix, iy, layout, W):
         return (iy // 8) * (W // 8) + ix // 8
     if layout == "t16x4":
         return (iy // 4) * (W // 16) + ix // 16
+    if layout == "pk14x8":  # 16-byte packets of 14 texels, 8 rows of one packet column per line
+        return (iy // 8) * (W // 14 + 1) + ix // 14
+    if layout == "pk28x4":  # 2 packets wide x 4 rows per line
+        return (iy // 4) * (W // 28 + 1) + ix // 28
+    if layout == "pk56x2":
+        return (iy // 2) * (W // 56 + 1) + ix // 56
     raise ValueError(layout)
 
 
@@ -70,6 +76,8 @@ def main():
     N = int(sys.argv[3]) if len(sys.argv) > 3 else 6
     rr = float(sys.argv[4]) if len(sys.argv) > 4 else 2.0
     nwg = int(sys.argv[5]) if len(sys.argv) > 5 else 400
+    TXW = int(sys.argv[6]) if len(sys.argv) > 6 else 16  # probe-mapping tile width (waves are TXW x 64/TXW)
+    TYW = 256 // TXW
     H = W
     D = dist_field(W, H)
     b = 1 << L
@@ -78,16 +86,16 @@ def main():
     t1 = (4 ** (L + 1) - 1) / (4 ** N - 1) * rr
     delta = 2 * math.pi / (4 * b * b)
     rng = np.random.default_rng(1)
-    layouts = ("lin", "pack", "t8", "t16x4")
+    layouts = ("pack", "pk56x2", "pk28x4", "pk14x8")
     # a workgroup = 16x16 probes of one direction block (4 directions): 4 waves of 16x4 probes
     tot = {(m, lay): 0 for m in ("probe", "dir") for lay in layouts}
     instr = {"probe": 0, "dir": 0}
     for _ in range(nwg):
         bi = int(rng.integers(b * b))
-        tx, ty = int(rng.integers(bd // 16)), int(rng.integers(bd // 16))
-        cx = tx * 16 + np.arange(16)
-        cy = ty * 16 + np.arange(16)
-        CX, CY = np.meshgrid(cx, cy)  # [16 rows, 16 cols]
+        tx, ty = int(rng.integers(max(1, bd // TXW))), int(rng.integers(max(1, bd // TYW)))
+        cx = tx * TXW + np.arange(TXW)
+        cy = ty * TYW + np.arange(TYW)
+        CX, CY = np.meshgrid(cx, cy)  # [TYW rows, TXW cols]
         ox = ((CX + 0.5) * b / W).astype(np.float32)
         oy = ((CY + 0.5) * b / H).astype(np.float32)
         th = (np.arange(4) + bi * 4 + 0.5) * delta
@@ -98,15 +106,16 @@ def main():
         its = len(R)
         if its == 0:
             continue
-        ix = np.stack([r[0] for r in R]).reshape(its, 16, 16, 4)
-        iy = np.stack([r[1] for r in R]).reshape(its, 16, 16, 4)
-        lv = np.stack([r[2] for r in R]).reshape(its, 16, 16, 4)
+        ix = np.stack([r[0] for r in R]).reshape(its, TYW, TXW, 4)
+        iy = np.stack([r[1] for r in R]).reshape(its, TYW, TXW, 4)
+        lv = np.stack([r[2] for r in R]).reshape(its, TYW, TXW, 4)
         for lay in layouts:
             ids = line_ids(ix, iy, lay, W)
             # probe mapping: wave w = rows 4w..4w+3 (16x4 probes); instruction = (iteration, r); a wave
             # iterates while any of its rays is live; dead lanes read texel 0 (one line)
+            rpw = 64 // TXW  # probe rows per wave
             for w in range(4):
-                sl = slice(4 * w, 4 * w + 4)
+                sl = slice(rpw * w, rpw * w + rpw)
                 lw = lv[:, sl]
                 nit = int(np.max(np.nonzero(lw.reshape(its, -1).any(1))[0], initial=-1)) + 1
                 for it in range(nit):
@@ -114,10 +123,10 @@ def main():
                         l = lw[it, :, :, r].ravel()
                         s = set(ids[it, sl, :, r].ravel()[l].tolist())
                         tot[("probe", lay)] += len(s) + (0 if l.all() else 1)
-                        if lay == "lin":
+                        if lay == layouts[0]:
                             instr["probe"] += 1
             # dir mapping: wave = 16 probes x 4 dirs; probes as an 8x2 patch; 16 waves per workgroup
-            for wy in range(8):
+            for wy in (range(8) if TXW == 16 else ()):
                 for wx in range(2):
                     sl = (slice(2 * wy, 2 * wy + 2), slice(8 * wx, 8 * wx + 8))
                     lw = lv[:, sl[0], sl[1], :]
@@ -126,11 +135,11 @@ def main():
                         l = lw[it].ravel()
                         s = set(ids[it, sl[0], sl[1], :].ravel()[l].tolist())
                         tot[("dir", lay)] += len(s) + (0 if l.all() else 1)
-                        if lay == "lin":
+                        if lay == layouts[0]:
                             instr["dir"] += 1
     rays = nwg * 1024
     print(f"{W}^2 L{L} N{N} rr{rr}: {nwg} workgroups, {rays} rays")
-    for m in ("probe", "dir"):
+    for m in (("probe", "dir") if instr["dir"] else ("probe",)):
         print(f"  {m:5s}: wave gathers/ray {instr[m] * 64 / rays:.2f}  " +
               "  ".join(f"{lay} {tot[(m, lay)] / instr[m]:.1f} lines/gather ({tot[(m, lay)] * 64 / rays:.1f}/ray-slot)"
                         for lay in layouts))
