@@ -181,12 +181,32 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
 //   otherwise the fp32 form.
 // The no-seed value 0x80008000 is at least max(W,H) away from every texel (and below overflow),
 // so it never beats the initial minDist and needs no test of its own.
+// physical workgroup id -> logical id: every XCD (own L2) a contiguous chunk of the logical order
+__host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
+  const int q = n >> 3, r = n & 7, x = p & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (p >> 3);
+}
+
 template <bool FIRST, bool IKEY>
 __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src, int src_pitch,
                                                 unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
-                                                ScreenDims s, JfaTaps o, int row0, int row1) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j0 = row0 + blockIdx.y * (4 * JT) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+                                                ScreenDims s, JfaTaps o, int row0, int row1, int lattice) {
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (lattice) {
+    // Lattice order for the long steps: the tiles (bx + a * ptx, by + b * pty) tap one another
+    // (offsets are whole multiples of the 64 x 16 tile), so walk one such lattice after the
+    // other, each XCD a contiguous run (xcd_logical_id): a tile's 9 taps are then read from that
+    // XCD's L2 by the 9 workgroups that need them.  Powers of two throughout (host-checked).
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int l = xcd_logical_id(by * gx + bx, gx * gy);
+    const int sx = __builtin_ctz((unsigned)max(1, o.dx[2] >> 6)), sy = __builtin_ctz((unsigned)max(1, o.dy[2] >> 4));
+    const int lxs = __builtin_ctz((unsigned)gx) - sx, lys = __builtin_ctz((unsigned)gy) - sy;  // log2 lattice extent
+    const int ph = l >> (lxs + lys), k = l & ((1 << (lxs + lys)) - 1);
+    bx = (ph & ((1 << sx) - 1)) + ((k & ((1 << lxs) - 1)) << sx);
+    by = (ph >> sx) + ((k >> lxs) << sy);
+  }
+  const int i = bx * 64 + (threadIdx.x & 63);
+  const int j0 = row0 + by * (4 * JT) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (i >= s.W) return;
   unsigned ti[3];  // unsigned: scalar row base + 32-bit lane offset addressing
 #pragma unroll
@@ -286,10 +306,6 @@ __device__ __forceinline__ float div_res(float a, float n, float inv_n, int pow2
 // together trace ALL directions of neighbouring probe tiles, so their distance-field
 // samples stay in a ring around those tiles (L2-resident) instead of sweeping the whole
 // field once per direction.
-__host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
-  const int q = n >> 3, r = n & 7, x = p & 7;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (p >> 3);
-}
 
 // logical workgroup -> (tile, direction group).  odg == 0: tile-major, direction-minor.
 // Otherwise for patch: for direction group: for tile in patch: for direction in group -- the
@@ -1177,8 +1193,15 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
                          row1);
   } else if (jfa_p2_taps(s, off_x, off_y, &tp)) {
     const bool ikey = s.W == s.H && s.W <= 4096;
-#define RC2DGI_JFA(F, K) \
-  hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1)
+    // lattice order (k_jfa_p2) for whole-frame launches whose steps span several tiles (not the
+    // first step: its taps read the 2 MB occupancy mask, which every L2 holds anyway)
+    const bool full = !first && row0 == 0 && row1 == s.H && s.W >= 64 && s.H >= 4 * JT && s.H % (4 * JT) == 0;
+    const int lattice = full && (tp.dx[2] >= 128 || tp.dy[2] >= 64) && tp.dx[2] >= 0 && tp.dy[2] >= 0 &&
+                        (tp.dx[2] & (tp.dx[2] - 1)) == 0 && (tp.dy[2] & (tp.dy[2] - 1)) == 0 &&
+                        tp.dx[2] <= s.W && tp.dy[2] <= s.H;
+#define RC2DGI_JFA(F, K)                                                                                      \
+  hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1, \
+                     lattice)
     if (first) {
       if (ikey) RC2DGI_JFA(true, true); else RC2DGI_JFA(true, false);
     } else {
