@@ -51,21 +51,24 @@ __device__ __forceinline__ bool seed_u8_ok(unsigned sd) { return (sd & 0xFFFFu) 
 // ScreenUV.fs:19 `any(greaterThan(color.rgb, 0))` as a 1-bit occupancy mask (one 64-texel ballot
 // per wave; mask row pitch s.mpitch words).  The seed texture J0 itself is never observable when
 // the JFA runs >= 2 steps (step 1 overwrites jumpRT1), so step 0 reads the mask instead.
+constexpr int kOccRows = 16;  // rows per wave in k_occupancy (4 rows apart), all loads issued together
 __global__ __launch_bounds__(256) void k_occupancy(const float4 *__restrict__ color, unsigned *__restrict__ mask,
                                                    ScreenDims s, int mpitch) {
-  // 4 rows per wave (loads issued together), one 64-texel ballot per row
+  // kOccRows rows per wave, one 64-texel ballot per row; non-temporal loads (colorRT is read
+  // again only by the merge, after the cascades have cycled the caches)
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j0 = blockIdx.y * 16 + (threadIdx.x >> 6);
-  float4 c[4];
+  const int j0 = blockIdx.y * (4 * kOccRows) + (threadIdx.x >> 6);
+  v4f_t c[kOccRows];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < kOccRows; ++t) {
     const int j = j0 + 4 * t;
-    c[t] = (i < s.W && j < s.H) ? color[(size_t)j * s.pitch + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    c[t] = __builtin_nontemporal_load(
+        reinterpret_cast<const v4f_t *>(color + (size_t)min(j, s.H - 1) * s.pitch + min(i, s.W - 1)));
   }
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < kOccRows; ++t) {
     const int j = j0 + 4 * t;
-    const bool occ = c[t].x > 0.0f || c[t].y > 0.0f || c[t].z > 0.0f;
+    const bool occ = i < s.W && j < s.H && (c[t].x > 0.0f || c[t].y > 0.0f || c[t].z > 0.0f);
     const unsigned long long b = __ballot(occ);
     if ((threadIdx.x & 63) == 0 && j < s.H) {
       unsigned *row = mask + (size_t)j * mpitch + (blockIdx.x * 2);
@@ -1134,8 +1137,8 @@ __global__ __launch_bounds__(256) void k_quantize_u8(float4 *__restrict__ buf, i
 static dim3 grid2d(int w, int h) { return dim3(ceil_div(w, 64), ceil_div(h, 4)); }
 
 hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, ScreenDims s, hipStream_t st) {
-  hipLaunchKernelGGL(k_occupancy, dim3(ceil_div(s.W, 64), ceil_div(s.H, 16)), dim3(256), 0, st, color, mask, s,
-                     mpitch);
+  hipLaunchKernelGGL(k_occupancy, dim3(ceil_div(s.W, 64), ceil_div(s.H, 4 * kOccRows)), dim3(256), 0, st, color, mask,
+                     s, mpitch);
   return hipGetLastError();
 }
 
