@@ -84,6 +84,31 @@ def cpu_baseline(W, H, N, rr, budget_s=12.0):
                        f"oracle/rc2dgi_oracle.c, {platform.processor() or platform.machine()})")
 
 
+# Random 128-byte line requests one MI355X sustains (scripts/gather_ceiling.hip,
+# profiles/r01/gather_ceiling.txt): table resident in every XCD's L2 vs in the Infinity Cache
+# (mean of the 16 MB and 32 MB rows).
+GATHER_L2_GLINES, GATHER_MALL_GLINES = 260.0, 73.0
+
+
+def gather_roofline(rec, N, level_ms):
+    """The march-bound levels' L1->L2 line-request rate (PMC l2_requests from the committed profile
+    over this run's level times) against the random-gather ceiling blended by their L2 hit rate
+    (DESIGN.md §5.2).  The upper half of the levels, where the distance gathers dominate."""
+    lv = rec.get("per_level", {})
+    top = list(range(N // 2, N))
+    req = [lv.get(f"k_rc_level L{L}", {}).get("l2_requests") for L in top]
+    hit = [lv.get(f"k_rc_level L{L}", {}).get("l2_hit") for L in top]
+    if any(x is None for x in req + hit):
+        return None
+    t = sum(level_ms[L] for L in top) / 1e3
+    h = sum(r * x for r, x in zip(req, hit)) / sum(req)
+    achieved = sum(req) / t / 1e9
+    ceiling = 1.0 / (h / GATHER_L2_GLINES + (1.0 - h) / GATHER_MALL_GLINES)
+    return {"kernel": f"k_rc_level L{top[0]}-L{top[-1]}", "achieved": round(achieved, 1), "peak": round(ceiling, 1),
+            "unit": "G line requests/s", "frac": round(achieved / ceiling, 4), "l2_hit": round(h, 4),
+            "source": "profiles/rc_level_pmc.json (TCC_HIT+TCC_MISS per launch), profiles/r01/gather_ceiling.txt"}
+
+
 def input_costs(ctx, W, H, color, emis, reps=5):
     """Per-frame cost of producing the painted inputs (outside the timed frames): painting the
     demo scene on the device (rc2dgi_paint) vs uploading both textures from host
@@ -356,13 +381,14 @@ def main():
     bytes_launch = b_rc(W, H, CW, CH, N, {"f32": 16, "f16": 8, "rgba8": 4}[a.storage]) / N
     avg_launch_s = (t_rc / 1e3) / (a.steps * N)
     achieved = bytes_launch / avg_launch_s / 1e9
-    traffic = None
+    traffic, gather = None, None
     pmc = os.path.join(ROOT, "profiles", "rc_level_pmc.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
         if rec.get("config") == f"{W}x{H}_N{N}" and a.storage == "f32":
             traffic = rec.get("hbm_bytes_per_launch")
+            gather = gather_roofline(rec, N, lvl_ms / a.steps)
     line = {
         "metric": (f"Mpixel*cascades/s (RC pass) at {W}^2, cascadeCount={N}" if W == H else
                    f"Mpixel*cascades/s (RC pass) at {W}x{H}, cascadeCount={N}"),
@@ -391,6 +417,8 @@ def main():
                      "kernel": "k_rc_level", "bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(avg_launch_s * 1e3, 5)},
     }
+    if gather:
+        line["gather_roofline"] = gather
     line["inputs"] = input_costs(ctx, W, H, color, emis)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the CPU leg: rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(W, H, N, a.ray_range, a.cpu_budget)
