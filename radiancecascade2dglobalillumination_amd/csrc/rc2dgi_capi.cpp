@@ -220,7 +220,9 @@ const int kOrderCandidates[][4] = {{0, 0, 0, 0},  {2, 2, 8, 0},  {4, 4, 4, 0},  
                                    {8, 1, 32, 1},  {32, 1, 8, 1},  {8, 4, 8, 1},   {4, 2, 32, 1},  {1, 1, 16, 2},
                                    {1, 1, 32, 2},  {1, 2, 8, 2},   {1, 2, 16, 2},  {1, 4, 4, 2},   {1, 4, 8, 2},
                                    {1, 1, 8, 2},   {1, 2, 32, 2},  {1, 1, 4, 2},   {1, 2, 4, 2},   {1, 4, 2, 2},
-                                   {1, 8, 4, 2},   {1, 1, 64, 2},  {1, 2, 64, 2},  {1, 1, 128, 2}, {1, 8, 8, 2}};
+                                   {1, 8, 4, 2},   {1, 1, 64, 2},  {1, 2, 64, 2},  {1, 1, 128, 2}, {1, 8, 8, 2},
+                                   {1, 3, 8, 2},   {1, 6, 8, 2},   {1, 3, 16, 2},  {1, 6, 4, 2},   {1, 12, 4, 2},
+                                   {1, 16, 2, 2},  {1, 3, 32, 2},  {1, 6, 16, 2}};
 
 // (re)allocate every render texture for the current W, H, N (RC2DGI.cs:79-98)
 int allocate(rc2dgi_ctx *c) {
