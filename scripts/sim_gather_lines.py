@@ -86,10 +86,10 @@ def main():
     t1 = (4 ** (L + 1) - 1) / (4 ** N - 1) * rr
     delta = 2 * math.pi / (4 * b * b)
     rng = np.random.default_rng(1)
-    layouts = ("pack", "pk56x2", "pk28x4", "pk14x8")
+    layouts = ("pack", "lin", "t8")
     # a workgroup = 16x16 probes of one direction block (4 directions): 4 waves of 16x4 probes
-    tot = {(m, lay): 0 for m in ("probe", "dir") for lay in layouts}
-    instr = {"probe": 0, "dir": 0}
+    tot = {(m, lay): 0 for m in ("probe", "dir", "hyb") for lay in layouts}
+    instr = {"probe": 0, "dir": 0, "hyb": 0}
     for _ in range(nwg):
         bi = int(rng.integers(b * b))
         tx, ty = int(rng.integers(max(1, bd // TXW))), int(rng.integers(max(1, bd // TYW)))
@@ -125,6 +125,21 @@ def main():
                         tot[("probe", lay)] += len(s) + (0 if l.all() else 1)
                         if lay == layouts[0]:
                             instr["probe"] += 1
+            # hybrid: lanes = 16 probes of one wave row x 4 directions (lane = 4 * column + r); slot k
+            # of a lane = wave row k; the lane marches its 4 slots in lockstep (merge layout unchanged
+            # after a quad transpose)
+            if TXW == 16:
+                for w in range(4):
+                    sl = slice(rpw * w, rpw * w + rpw)
+                    lw = lv[:, sl]  # [its, 4 rows, 16 cols, 4 dirs]
+                    nit = int(np.max(np.nonzero(lw.reshape(its, -1).any(1))[0], initial=-1)) + 1
+                    for it in range(nit):
+                        for k in range(4):
+                            l = lw[it, k].ravel()  # 16 cols x 4 dirs = 64 lanes
+                            s_ = set(ids[it, sl][k].ravel()[l].tolist())
+                            tot[("hyb", lay)] += len(s_) + (0 if l.all() else 1)
+                            if lay == layouts[0]:
+                                instr["hyb"] += 1
             # dir mapping: wave = 16 probes x 4 dirs; probes as an 8x2 patch; 16 waves per workgroup
             for wy in (range(8) if TXW == 16 else ()):
                 for wx in range(2):
@@ -139,7 +154,7 @@ def main():
                             instr["dir"] += 1
     rays = nwg * 1024
     print(f"{W}^2 L{L} N{N} rr{rr}: {nwg} workgroups, {rays} rays")
-    for m in (("probe", "dir") if instr["dir"] else ("probe",)):
+    for m in [m for m in ("probe", "hyb", "dir") if instr[m]]:
         print(f"  {m:5s}: wave gathers/ray {instr[m] * 64 / rays:.2f}  " +
               "  ".join(f"{lay} {tot[(m, lay)] / instr[m]:.1f} lines/gather ({tot[(m, lay)] * 64 / rays:.1f}/ray-slot)"
                         for lay in layouts))
