@@ -183,6 +183,16 @@ def bench_batch(a, rank, local, world):
         g.upload("emissive", e)
         ctxs.append(g)
     CW, CH = ctxs[0].cascade_resolution
+    if a.batch_streams == 1 and len(ctxs) > 1:  # every scene on one stream: frames back to back
+        shared = torch.cuda.Stream(device=local)
+        for g in ctxs:
+            g.set_stream(shared.cuda_stream)
+    if ctxs and not a.no_autotune:  # setup: one context picks the schedule, the others reuse it
+        ctxs[0].autotune(3)
+        for g in ctxs[1:]:
+            for L in range(N):
+                for k in (f"rc_order_L{L}", f"rc_variant_L{L}"):
+                    g.set_tuning(k, ctxs[0].get_tuning(k))
     for _ in range(a.warmup):
         for g in ctxs:
             g.do_rc2dgi()
@@ -207,7 +217,8 @@ def bench_batch(a, rank, local, world):
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall * 1e3 / a.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic random scenes resident in HBM",
-            "config": {"workload": f"batch {a.batch} x DoRC2DGI {W}x{H} N={N} per GPU, one stream each",
+            "config": {"workload": f"batch {a.batch} x DoRC2DGI {W}x{H} N={N} per GPU, "
+                                   + ("one shared stream" if a.batch_streams == 1 else "one stream each"),
                        "parallelism": f"replicas{world}x{a.batch}"},
             "frames_per_s": round(a.steps * len(items) * world / wall, 2)}), flush=True)
     for g in ctxs:
@@ -300,6 +311,8 @@ def main():
     ap.add_argument("--scene", default="demo", help="demo | random:<seed>")
     ap.add_argument("--batch", type=int, default=0,
                     help="scenes per GPU, one context + stream each (BASELINE configs[4] batch mode)")
+    ap.add_argument("--batch-streams", type=int, default=1,
+                    help="batch mode: 0 = one stream per scene (frames overlap), 1 = all scenes on one stream")
     ap.add_argument("--mode", default="replicas", choices=("replicas", "strips"),
                     help="strips: one frame split into row strips over the ranks (BASELINE configs[3])")
     ap.add_argument("--storage", default="f32", choices=("f32", "f16", "rgba8"),
