@@ -190,7 +190,9 @@ __host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (p >> 3);
 }
 
-template <bool FIRST, bool IKEY>
+// U8: RGBA8 jumpRT (quantized seed uv, pack_seed_u8): the same integer taps, the float distance of
+// k_jfa_step's U8 path (the seed's uv is k * (1/255), not its texel centre).
+template <bool FIRST, bool IKEY, bool U8 = false>
 __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src, int src_pitch,
                                                 unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                 ScreenDims s, JfaTaps o, int row0, int row1, int lattice) {
@@ -226,7 +228,10 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
       for (int x = 0; x < 3; ++x) {
         if (FIRST) {
           const bool occ = (row[ti[x] >> 5] >> (ti[x] & 31)) & 1u;
-          seed[t][y * 3 + x] = occ ? ((tj << 16) | ti[x]) : kNoSeed;
+          if constexpr (U8)
+            seed[t][y * 3 + x] = occ ? pack_seed_u8((int)ti[x], (int)tj, Axis{s.W, 1}, Axis{s.H, 1}) : 0u;
+          else
+            seed[t][y * 3 + x] = occ ? ((tj << 16) | ti[x]) : kNoSeed;
         } else {
           seed[t][y * 3 + x] = *reinterpret_cast<const unsigned *>(reinterpret_cast<const char *>(row) + (ti[x] << 2));
         }
@@ -238,6 +243,35 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
   for (int t = 0; t < JT; ++t) {
     const int j = j0 + 4 * t;
     if (j >= row1) break;
+    if constexpr (U8) {  // JumpFlood.fs on RGBA8 seeds, as k_jfa_step<., true>
+      const Axis ax{s.W, 1}, ay{s.H, 1};
+      const float u = texcoord(i, ax), v = texcoord(j, ay);
+      float minDist = 1.0f, bx = 0.0f, by = 0.0f;
+      unsigned best = 0u;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
+        const unsigned sd = seed[t][k];
+        if (seed_u8_ok(sd)) {
+          const float px = (float)(sd & 0xFFFFu) * kInv255, py = (float)(sd >> 16) * kInv255;
+          const float dx = px - u, dy = py - v;
+          const float d = dx * dx + dy * dy;
+          if (d < minDist) {
+            minDist = d;
+            bx = px;
+            by = py;
+            best = sd;
+          }
+        }
+      }
+      dst[(size_t)j * s.pitch + i] = best;
+      if (dist) {
+        const float dx = u - bx, dy = v - by;
+        const float d = sqrtf(dx * dx + dy * dy);
+        const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
+        dist[(size_t)j * s.pitch + i] = (unsigned short)(unsigned)(cl * 65535.0f + 0.5f);
+      }
+      continue;
+    }
     float minKey = o.dinit;
     unsigned best = kNoSeed;
     const unsigned here = pack_seed(i, j);
@@ -1188,20 +1222,28 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   }
   const dim3 grid(ceil_div(s.W, 64), ceil_div(row1 - row0, 4 * JT));
   JfaTaps tp;
-  if (s.u8) {  // RGBA8 jumpRT: quantized seed uv, the float path
+  const bool p2 = jfa_p2_taps(s, off_x, off_y, &tp);
+  // lattice order (k_jfa_p2) for whole-frame launches whose steps span several tiles (not the
+  // first step: its taps read the 2 MB occupancy mask, which every L2 holds anyway)
+  const bool full = !first && row0 == 0 && row1 == s.H && s.W >= 64 && s.H >= 4 * JT && s.H % (4 * JT) == 0;
+  const int lattice = p2 && full && (tp.dx[2] >= 128 || tp.dy[2] >= 64) && tp.dx[2] >= 0 && tp.dy[2] >= 0 &&
+                      (tp.dx[2] & (tp.dx[2] - 1)) == 0 && (tp.dy[2] & (tp.dy[2] - 1)) == 0 &&
+                      tp.dx[2] <= s.W && tp.dy[2] <= s.H;
+  if (s.u8 && p2) {  // RGBA8 jumpRT on a power-of-two screen: integer taps, quantized-uv distance
+    if (first)
+      hipLaunchKernelGGL((k_jfa_p2<true, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp,
+                         row0, row1, lattice);
+    else
+      hipLaunchKernelGGL((k_jfa_p2<false, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp,
+                         row0, row1, lattice);
+  } else if (s.u8) {  // RGBA8 jumpRT: quantized seed uv, the float path
     if (first)
       hipLaunchKernelGGL((k_jfa_step<true, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
     else
       hipLaunchKernelGGL((k_jfa_step<false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
                          row1);
-  } else if (jfa_p2_taps(s, off_x, off_y, &tp)) {
+  } else if (p2) {
     const bool ikey = s.W == s.H && s.W <= 4096;
-    // lattice order (k_jfa_p2) for whole-frame launches whose steps span several tiles (not the
-    // first step: its taps read the 2 MB occupancy mask, which every L2 holds anyway)
-    const bool full = !first && row0 == 0 && row1 == s.H && s.W >= 64 && s.H >= 4 * JT && s.H % (4 * JT) == 0;
-    const int lattice = full && (tp.dx[2] >= 128 || tp.dy[2] >= 64) && tp.dx[2] >= 0 && tp.dy[2] >= 0 &&
-                        (tp.dx[2] & (tp.dx[2] - 1)) == 0 && (tp.dy[2] & (tp.dy[2] - 1)) == 0 &&
-                        tp.dx[2] <= s.W && tp.dy[2] <= s.H;
 #define RC2DGI_JFA(F, K)                                                                                      \
   hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1, \
                      lattice)
