@@ -310,7 +310,7 @@ def main():
                     help="time every RC tile variant per level (interleaved rounds) instead of the bench line")
     ap.add_argument("--scene", default="demo", help="demo | random:<seed>")
     ap.add_argument("--batch", type=int, default=0,
-                    help="scenes per GPU, one context + stream each (BASELINE configs[4] batch mode)")
+                    help="scenes per GPU, one context each (BASELINE configs[4] batch mode)")
     ap.add_argument("--batch-streams", type=int, default=1,
                     help="batch mode: 0 = one stream per scene (frames overlap), 1 = all scenes on one stream")
     ap.add_argument("--mode", default="replicas", choices=("replicas", "strips"),
