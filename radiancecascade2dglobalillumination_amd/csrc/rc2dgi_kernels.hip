@@ -313,7 +313,6 @@ struct RcParams {
   CascadeDims c;
   int level, bsc, bdx, bdy, tiles_x, tiles_per_block;
   int p0, p1;  // probe rows [p0, p1) of every direction block (row-strip shards; 0, bdy otherwise)
-  int opx, opy, odg;  // workgroup order: patches of opx x opy tiles x groups of odg direction blocks (odg 0: tile-major)
   float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
   float aspx, aspy, t0, t1, reflectivity;
   float sWf, sHf;  // screen size as floats (power-of-two screen path)
