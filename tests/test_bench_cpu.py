@@ -1,0 +1,53 @@
+"""CPU: bench.py's measurement definitions -- the algorithmic byte model of the
+RC pass and the gather roofline built from a PMC record."""
+import json
+import os
+
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def bench():
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench as b
+
+    return b
+
+
+def test_rc_byte_model_matches_survey(bench):
+    # 16·CW·CH·(2N−1) + 4·W·H·N = 3.355 GB per pass at 4096², N=6
+    assert bench.b_rc(4096, 4096, 4096, 4096, 6) == 16 * 4096 * 4096 * 11 + 4 * 4096 * 4096 * 6
+    assert abs(bench.b_rc(4096, 4096, 4096, 4096, 6) / 1e9 - 3.355) < 1e-3
+    # C1 0.231 GB, C2 4.563 GB
+    assert abs(bench.b_rc(1200, 900, 1216, 960, 6) / 1e9 - 0.231) < 1e-3
+    assert abs(bench.b_rc(4096, 4096, 4096, 4096, 8) / 1e9 - 4.563) < 1e-3
+    # RGBA16F cascades halve the cascade terms
+    assert bench.b_rc(64, 64, 64, 64, 2, gi_bytes=8) == 8 * 64 * 64 * 3 + 4 * 64 * 64 * 2
+
+
+def test_gather_roofline_blends_the_ceiling_by_hit_rate(bench):
+    rec = {"per_level": {f"k_rc_level L{L}": {"l2_requests": 1e6 * (L + 1), "l2_hit": 1.0} for L in range(4)}}
+    g = bench.gather_roofline(rec, 4, [0.1, 0.1, 0.1, 0.1])
+    # upper half = L2, L3: 7e6 requests in 0.2 ms -> 35 G/s against the L2-resident ceiling
+    assert g["kernel"] == "k_rc_level L2-L3"
+    assert abs(g["achieved"] - 35.0) < 1e-9 and g["peak"] == bench.GATHER_L2_GLINES
+    rec["per_level"]["k_rc_level L3"]["l2_hit"] = 0.0
+    g = bench.gather_roofline(rec, 4, [0.1, 0.1, 0.1, 0.1])
+    h = 3 / 7
+    want = 1.0 / (h / bench.GATHER_L2_GLINES + (1 - h) / bench.GATHER_MALL_GLINES)
+    assert abs(g["peak"] - round(want, 1)) < 1e-9 and abs(g["l2_hit"] - round(h, 4)) < 1e-9
+    # a record without L2 counters gives no gather roofline
+    assert bench.gather_roofline({"per_level": {}}, 4, [0.1] * 4) is None
+
+
+def test_committed_pmc_record_has_the_gather_fields():
+    with open(os.path.join(ROOT, "profiles", "rc_level_pmc.json")) as f:
+        rec = json.load(f)
+    assert rec["config"] == "4096x4096_N6" and rec["hbm_bytes_per_launch"] > 0
+    for L in range(6):
+        lv = rec["per_level"][f"k_rc_level L{L}"]
+        assert lv["l2_requests"] > 0 and 0.0 < lv["l2_hit"] < 1.0 and lv["dur_us"] > 0
