@@ -176,17 +176,20 @@ struct GiU8 {
   __device__ static S ld_stage(const T *p) { return *p; }
   __device__ static S ld_stage_nt(const T *p) { return __builtin_nontemporal_load(p); }
   __device__ static S stage(unsigned x, unsigned, unsigned, unsigned) { return x; }
+  // lerp8 on two channels at once in 16-bit lanes (v_pk_* ops): a * 256 + (b - a) * w + 128 lies in
+  // [0, 65408], so the lane arithmetic modulo 2^16 gives lerp8's value exactly
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  __device__ static u16x2 lerp8x2(u16x2 a, u16x2 b, unsigned short w) {
+    const u16x2 W = {w, w}, R = {128, 128};
+    return ((a << 8) + (b - a) * W + R) >> 8;
+  }
   __device__ static float4 bilerp(S t00, S t10, S t01, S t11, float wx, float wy) {
-    const int w8x = (int)rintf(wx * 256.0f), w8y = (int)rintf(wy * 256.0f);
-    float r[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int sh = 8 * c;
-      const unsigned l0 = lerp8((t00 >> sh) & 255u, (t10 >> sh) & 255u, w8x);
-      const unsigned l1 = lerp8((t01 >> sh) & 255u, (t11 >> sh) & 255u, w8x);
-      r[c] = (float)lerp8(l0, l1, w8y) * kInv255;
-    }
-    return make_float4(r[0], r[1], r[2], r[3]);
+    const unsigned short w8x = (unsigned short)rintf(wx * 256.0f), w8y = (unsigned short)rintf(wy * 256.0f);
+    auto ch02 = [](unsigned t) { return __builtin_bit_cast(u16x2, t & 0x00FF00FFu); };         // r, b
+    auto ch13 = [](unsigned t) { return __builtin_bit_cast(u16x2, (t >> 8) & 0x00FF00FFu); };  // g, a
+    const u16x2 rb = lerp8x2(lerp8x2(ch02(t00), ch02(t10), w8x), lerp8x2(ch02(t01), ch02(t11), w8x), w8y);
+    const u16x2 ga = lerp8x2(lerp8x2(ch13(t00), ch13(t10), w8x), lerp8x2(ch13(t01), ch13(t11), w8x), w8y);
+    return make_float4((float)rb.x * kInv255, (float)ga.x * kInv255, (float)rb.y * kInv255, (float)ga.y * kInv255);
   }
   __device__ static float blend1(float s, float d, unsigned a8) {
     const unsigned v = mul8(q8(s), a8) + mul8(q8(d), 255u - a8);
