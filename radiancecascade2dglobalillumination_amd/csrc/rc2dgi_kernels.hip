@@ -528,49 +528,55 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(UNR > 1 
   const int lane = (int)threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int yy0 = lane / RW, xx0 = lane - (lane / RW) * RW;
-  if (STG) {
-#pragma unroll
-    for (int j = 0; j < DPW; ++j) {
-      const int r = wv + j * NW;  // direction (of the 4*PD) this wave stages
-      const int a = bi0 * 4 + r;
-      const int bx = (a & umask) * ubx + (cx0 >> 1) - 1, by = (a >> ushift) * uby + (cy0 >> 1) - 1;
-      // REPEAT wrap only where the footprint crosses a texture edge (a wave-uniform branch)
-      const bool wrap = bx < 0 || bx + RW > P.c.CW || by < 0 || by + RH > P.c.CH;
-#pragma unroll
-      for (int q = 0; q < QPD; ++q) {
-        // texel e = lane + 64 q of the footprint: (yy, xx) from the lane's (yy0, xx0), clamped to
-        // the footprint (unconditional loads keep the staging arrays in registers)
-        int xx = xx0 + (64 * q) % RW, yy = yy0 + (64 * q) / RW;
-        if (xx >= RW) {
-          xx -= RW;
-          ++yy;
-        }
-        if (yy >= RH) {
-          yy = RH - 1;
-          xx = RW - 1;
-        }
-        int gx = bx + xx, gy = by + yy;
-        if (wrap) {
-          gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
-          gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
-        }
-        const unsigned off = __umul24((unsigned)gy, (unsigned)P.c.pitch) + (unsigned)gx;
-        const typename GI::T v = upper[off];  // issued now, consumed after the march
-        const int t = j * QPD + q;
-        if constexpr (NWD == 1) {
-          stx[t] = v;
-        } else if constexpr (NWD == 2) {
-          stx[t] = v.x;
-          sty[t] = v.y;
-        } else {
-          stx[t] = __float_as_uint(v.x);
-          sty[t] = __float_as_uint(v.y);
-          stz[t] = __float_as_uint(v.z);
-          stw[t] = __float_as_uint(v.w);
+  // staging loads of the level-(L+1) footprint, issued now and written to LDS after the march.
+  // Level 0 issues its shared first distance sample before them (vmcnt retires in order, so
+  // the march then waits for that sample only).
+  auto stage_loads = [&]() {
+    if (STG) {
+  #pragma unroll
+      for (int j = 0; j < DPW; ++j) {
+        const int r = wv + j * NW;  // direction (of the 4*PD) this wave stages
+        const int a = bi0 * 4 + r;
+        const int bx = (a & umask) * ubx + (cx0 >> 1) - 1, by = (a >> ushift) * uby + (cy0 >> 1) - 1;
+        // REPEAT wrap only where the footprint crosses a texture edge (a wave-uniform branch)
+        const bool wrap = bx < 0 || bx + RW > P.c.CW || by < 0 || by + RH > P.c.CH;
+  #pragma unroll
+        for (int q = 0; q < QPD; ++q) {
+          // texel e = lane + 64 q of the footprint: (yy, xx) from the lane's (yy0, xx0), clamped to
+          // the footprint (unconditional loads keep the staging arrays in registers)
+          int xx = xx0 + (64 * q) % RW, yy = yy0 + (64 * q) / RW;
+          if (xx >= RW) {
+            xx -= RW;
+            ++yy;
+          }
+          if (yy >= RH) {
+            yy = RH - 1;
+            xx = RW - 1;
+          }
+          int gx = bx + xx, gy = by + yy;
+          if (wrap) {
+            gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
+            gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
+          }
+          const unsigned off = __umul24((unsigned)gy, (unsigned)P.c.pitch) + (unsigned)gx;
+          const typename GI::T v = upper[off];  // issued now, consumed after the march
+          const int t = j * QPD + q;
+          if constexpr (NWD == 1) {
+            stx[t] = v;
+          } else if constexpr (NWD == 2) {
+            stx[t] = v.x;
+            sty[t] = v.y;
+          } else {
+            stx[t] = __float_as_uint(v.x);
+            sty[t] = __float_as_uint(v.y);
+            stz[t] = __float_as_uint(v.z);
+            stw[t] = __float_as_uint(v.w);
+          }
         }
       }
     }
-  }
+  };
+  if constexpr (!Z0) stage_loads();
 
   const float cxf = (float)cx;
   const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);  // rayOrigin / _CascadeResolution
@@ -611,14 +617,24 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(UNR > 1 
   if constexpr (Z0) {
     // level 0 (t0 = 0): every ray of a probe starts at the probe centre, x = o + (0*dir)*asp = o
     // exactly, so the first iteration is one shared sample per probe instead of one per ray
+    bool zlive[PY];
+    int zidx[PY];
+    unsigned zq[PY];
 #pragma unroll
     for (int p = 0; p < PY; ++p) {
-      const bool live = act[p * ND] && __float_as_uint(ox) <= 0x3f800000u && __float_as_uint(oy[p]) <= 0x3f800000u;
+      zlive[p] = act[p * ND] && __float_as_uint(ox) <= 0x3f800000u && __float_as_uint(oy[p]) <= 0x3f800000u;
       int ix = cvt_floor(ox * P.sWf) & (P.s.W - 1);
       int iy = cvt_floor(oy[p] * P.sHf) & (P.s.H - 1);
-      if (!live) ix = iy = 0;
-      const int idx = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
-      const float d = decode_dist(fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx));
+      if (!zlive[p]) ix = iy = 0;
+      zidx[p] = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
+      zq[p] = fetch_q<DL>(dist, dpk, P.tpr, ix, iy, zidx[p]);
+    }
+    stage_loads();
+#pragma unroll
+    for (int p = 0; p < PY; ++p) {
+      const bool live = zlive[p];
+      const int idx = zidx[p];
+      const float d = decode_dist(zq[p]);
       const bool hit = live && d < 0.001f;
 #pragma unroll
       for (int r = 0; r < ND; ++r) {
