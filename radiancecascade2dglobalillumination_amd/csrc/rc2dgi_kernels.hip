@@ -433,8 +433,9 @@ __device__ __forceinline__ int cvt_floor(float x) {
 // floor(p * n) & (n - 1) exactly, and the march's screen test is one unsigned compare per axis
 // (p is never NaN, and never -0: the origin term is > 0, and x + (-x) rounds to +0).
 // UNR: unroll factor of the march loop.  Fully unrolled (32) suits the gather-bound high levels;
-// rolled (1) the VALU-bound low levels.  Unrolled builds are held to 8 waves per SIMD
-// (amdgpu_waves_per_eu: SGPRs spill to VGPR lanes instead of capping occupancy at 7).
+// rolled (1) the VALU-bound low levels.  Every build is held to 8 waves per SIMD
+// (amdgpu_waves_per_eu: SGPRs spill to VGPR lanes instead of the 106-SGPR allocation that caps a
+// CU at 6 workgroups of 256; L0 0.143 -> 0.133 ms).
 // TILED: `dist` is the 8x8-tiled copy (k_dist_tile): one 128-byte line holds an 8x8 texel tile,
 // so the nearly parallel rays of a lane (and vertical-ish steps) share lines.
 // GI: storage of the cascade textures (GiF32 / GiF16 / GiU8, rc2dgi_device.h).
@@ -480,7 +481,7 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
 // 14-texel row packets (`dpk`, see kPackTexels; power-of-two screens <= 16384).
 // Z0: level 0 on a power-of-two screen (t0 = 0): the first march iteration is shared by a probe's rays
 template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false>
-__global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(UNR > 1 ? 8 : 1))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
+__global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
                                                      const float4 *__restrict__ color,
