@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
 // on ((si - i) * scx)^2 + ((sj - j) * scy)^2 < max(W,H)^2.
 //   IKEY (W == H <= 4096): (si - i)^2 and (sj - j)^2 are integers below 2^24 (exact in fp32), so
 //     the shader's rounded sum is the integer sum converted with round-to-nearest-even: one packed
-//     16-bit subtract and one clamped 16-bit dot product per tap.
+//     16-bit subtract and one clamped 16-bit dot product per tap, compared as integers (below).
 //   otherwise the fp32 form.
 // The no-seed value 0x80008000 is at least max(W,H) away from every texel (and below overflow),
 // so it never beats the initial minDist and needs no test of its own.
@@ -272,23 +272,37 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
       }
       continue;
     }
-    float minKey = o.dinit;
     unsigned best = kNoSeed;
     const unsigned here = pack_seed(i, j);
+    if constexpr (IKEY) {
+      // The sequential "key < minKey" update keeps the first tap holding the minimum key, if that
+      // minimum is below dinit = max(W,H)^2 <= 2^24.  Integer keys below 2^24 convert exactly, and
+      // a key >= dinit loses both as an integer and as its rounded float, so the integer keys
+      // decide the same: one min3 tree over the 9 keys, then a select from the last tap to the
+      // first (no compare-and-swap chain, whose VCC hand-offs serialise; no conversions).
+      unsigned kb[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
-      const unsigned sd = seed[t][k];
-      float key;
-      if constexpr (IKEY) {
-        const v2s d = __builtin_bit_cast(v2s, sd) - __builtin_bit_cast(v2s, here);
-        key = (float)__builtin_amdgcn_sdot2(d, d, 0, true);
-      } else {
-        const float dx = (float)((int)(sd & 0xFFFFu) - i) * o.scx, dy = (float)((int)(sd >> 16) - j) * o.scy;
-        key = dx * dx + dy * dy;
+      for (int k = 0; k < 9; ++k) {
+        const v2s d = __builtin_bit_cast(v2s, seed[t][k]) - __builtin_bit_cast(v2s, here);
+        kb[k] = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, true);  // clamped: >= 0
       }
-      if (key < minKey) {
-        minKey = key;
-        best = sd;
+      const unsigned m = min(min(min(kb[0], kb[1]), min(kb[2], kb[3])),
+                             min(min(kb[4], kb[5]), min(min(kb[6], kb[7]), kb[8])));
+      best = seed[t][8];
+#pragma unroll
+      for (int k = 7; k >= 0; --k) best = kb[k] == m ? seed[t][k] : best;
+      if (m >= (unsigned)o.dinit) best = kNoSeed;
+    } else {
+      float minKey = o.dinit;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
+        const unsigned sd = seed[t][k];
+        const float dx = (float)((int)(sd & 0xFFFFu) - i) * o.scx, dy = (float)((int)(sd >> 16) - j) * o.scy;
+        const float key = dx * dx + dy * dy;
+        if (key < minKey) {
+          minKey = key;
+          best = sd;
+        }
       }
     }
     dst[(size_t)j * s.pitch + i] = best;
