@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
     // XCD's L2 by the 9 workgroups that need them.  Powers of two throughout (host-checked).
     const int gx = gridDim.x, gy = gridDim.y;
     const int l = xcd_logical_id(by * gx + bx, gx * gy);
-    const int sx = __builtin_ctz((unsigned)max(1, o.dx[2] >> 6)), sy = __builtin_ctz((unsigned)max(1, o.dy[2] >> 4));
+    const int sx = __builtin_ctz((unsigned)max(1, o.dx[2] >> 6)), sy = __builtin_ctz((unsigned)max(1, o.dy[2] / (4 * JT)));
     const int lxs = __builtin_ctz((unsigned)gx) - sx, lys = __builtin_ctz((unsigned)gy) - sy;  // log2 lattice extent
     const int ph = l >> (lxs + lys), k = l & ((1 << (lxs + lys)) - 1);
     bx = (ph & ((1 << sx) - 1)) + ((k & ((1 << lxs) - 1)) << sx);
