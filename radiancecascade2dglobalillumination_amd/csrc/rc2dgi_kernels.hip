@@ -217,6 +217,9 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
 #pragma unroll
   for (int x = 0; x < 3; ++x) ti[x] = (unsigned)(i + o.dx[x]) & (unsigned)(s.W - 1);
   unsigned seed[JT][9];
+  unsigned qx[3];  // U8 first step: the quantized u of each tap column (pack_seed_u8's low half)
+#pragma unroll
+  for (int x = 0; x < 3; ++x) qx[x] = (FIRST && U8) ? pack_seed_u8((int)ti[x], 0, Axis{s.W, 1}, Axis{s.H, 1}) & 0xFFFFu : 0u;
 #pragma unroll
   for (int t = 0; t < JT; ++t) {
     const int j = min(j0 + 4 * t, row1 - 1);  // clamped rows are computed but not stored
@@ -224,12 +227,13 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
     for (int y = 0; y < 3; ++y) {
       const unsigned tj = (unsigned)(j + o.dy[y]) & (unsigned)(s.H - 1);
       const unsigned *row = src + (size_t)tj * src_pitch;
+      const unsigned qy = (FIRST && U8) ? pack_seed_u8(0, (int)tj, Axis{s.W, 1}, Axis{s.H, 1}) & 0xFFFF0000u : 0u;
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
         if (FIRST) {
           const bool occ = (row[ti[x] >> 5] >> (ti[x] & 31)) & 1u;
           if constexpr (U8)
-            seed[t][y * 3 + x] = occ ? pack_seed_u8((int)ti[x], (int)tj, Axis{s.W, 1}, Axis{s.H, 1}) : 0u;
+            seed[t][y * 3 + x] = occ ? (qy | qx[x]) : 0u;  // = pack_seed_u8(ti[x], tj)
           else
             seed[t][y * 3 + x] = occ ? ((tj << 16) | ti[x]) : kNoSeed;
         } else {
@@ -246,25 +250,28 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
     if constexpr (U8) {  // JumpFlood.fs on RGBA8 seeds, as k_jfa_step<., true>
       const Axis ax{s.W, 1}, ay{s.H, 1};
       const float u = texcoord(i, ax), v = texcoord(j, ay);
-      float minDist = 1.0f, bx = 0.0f, by = 0.0f;
-      unsigned best = 0u;
+      // The sequential "d < minDist" update (minDist = 1) keeps the first valid tap holding the
+      // minimum, if below 1.  Distances are non-negative finite floats, ordered as their bit
+      // patterns: a min3 tree over the 9 keys (an invalid tap keys 1.0), then a select from the
+      // last tap to the first; the winner's uv is recomputed from its seed (same bits).
+      unsigned kb[9];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
+      for (int k = 0; k < 9; ++k) {
         const unsigned sd = seed[t][k];
-        if (seed_u8_ok(sd)) {
-          const float px = (float)(sd & 0xFFFFu) * kInv255, py = (float)(sd >> 16) * kInv255;
-          const float dx = px - u, dy = py - v;
-          const float d = dx * dx + dy * dy;
-          if (d < minDist) {
-            minDist = d;
-            bx = px;
-            by = py;
-            best = sd;
-          }
-        }
+        const float px = (float)(sd & 0xFFFFu) * kInv255, py = (float)(sd >> 16) * kInv255;
+        const float dx = px - u, dy = py - v;
+        kb[k] = seed_u8_ok(sd) ? __float_as_uint(dx * dx + dy * dy) : 0x3f800000u;
       }
+      const unsigned m = min(min(min(kb[0], kb[1]), min(kb[2], kb[3])),
+                             min(min(kb[4], kb[5]), min(min(kb[6], kb[7]), kb[8])));
+      unsigned best = seed[t][8];
+#pragma unroll
+      for (int k = 7; k >= 0; --k) best = kb[k] == m ? seed[t][k] : best;
+      if (m >= 0x3f800000u) best = 0u;
       dst[(size_t)j * s.pitch + i] = best;
       if (dist) {
+        const float bx = best ? (float)(best & 0xFFFFu) * kInv255 : 0.0f;
+        const float by = best ? (float)(best >> 16) * kInv255 : 0.0f;
         const float dx = u - bx, dy = v - by;
         const float d = sqrtf(dx * dx + dy * dy);
         const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
