@@ -161,7 +161,7 @@ def sweep_rc(ctx, N, steps, rounds=3):
 def lib_variant_name(v):
     names = ["16x16x1", "16x8x2", "16x16x2", "32x8x1", "64x4x1", "8x8x1", "32x8x2", "16x16x1d2", "16x16x1d4",
              "16x8x1d2", "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t",
-             "16x16x1up"]
+             "16x16x1up", "16x16x1p"]
     return names[v] if v < len(names) else str(v)
 
 

@@ -13,15 +13,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "librc2dgi.so")
-SOURCES = ["rc2dgi_kernels.hip", "rc2dgi_capi.cpp", "rc2dgi_shard.cpp", "rc2dgi_paint.hip"]
-HEADERS = ["rc2dgi_device.h", "rc2dgi_kernels.h", "rc2dgi_shard.h", "rc2dgi_paint.h"]
+SOURCES = ["rc2dgi_kernels.hip", "rc2dgi_rc_f32a.hip", "rc2dgi_rc_f32b.hip", "rc2dgi_rc_f16.hip",
+           "rc2dgi_rc_u8.hip", "rc2dgi_capi.cpp", "rc2dgi_shard.cpp", "rc2dgi_paint.hip"]
+HEADERS = ["rc2dgi_device.h", "rc2dgi_kernels.h", "rc2dgi_rc.h", "rc2dgi_shard.h", "rc2dgi_paint.h"]
 ARCH = os.environ.get("RC2DGI_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: each a*b+c in the kernels is two IEEE roundings, exactly as the GLSL
 # expressions they restate; the GL lerp's fused multiply-add is written as fmaf explicitly.
 # -disable-promote-alloca-to-lds: per-thread staging arrays stay in VGPRs (the AMDGPU
 # promote-alloca pass would otherwise move them to LDS and serialise the staging loads).
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
          f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result", "-mllvm", "-disable-promote-alloca-to-lds"]
 
 
@@ -41,14 +42,34 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) -> str:
-    """extra: additional compiler flags (diagnostic builds go to a different `out`)."""
+    """extra: additional compiler flags (diagnostic builds go to a different `out`).  Every
+    translation unit compiles in its own hipcc process (the k_rc_level variant families are
+    separate units), then one link."""
     if not force and out == LIB and not _stale():
         return LIB
-    cmd = [hipcc()] + FLAGS + list(extra) + ["-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"]
-    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    from concurrent.futures import ThreadPoolExecutor
+
+    objdir = os.path.join(ROOT, "build", "obj", os.path.basename(out).replace(".so", ""))
+    os.makedirs(objdir, exist_ok=True)
+    base = [hipcc()] + FLAGS + list(extra) + ["-I", os.path.join(ROOT, "include")]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = base + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr[-4000:]}")
+        return obj
+
+    jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 4)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    link = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        print(" ".join(link), flush=True)
+    subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
     return out
 

@@ -91,6 +91,7 @@ struct rc2dgi_ctx {
   unsigned short *dist = nullptr;  // packUNorm16 q
   unsigned short *dist_t = nullptr;  // 8x8-tiled copy for the "t" RC variants
   uint4 *dist_p = nullptr;           // packed copy for the "p" RC variants (k_dist_pack)
+  float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
@@ -179,7 +180,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->rc_maps.clear();
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
-                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p};
+                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->shade};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   c->color_in = c->emissive = c->temp = c->color_out = nullptr;
@@ -187,6 +188,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->occ = nullptr;
   c->dist = c->dist_t = nullptr;
   c->dist_p = nullptr;
+  c->shade = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
   c->sky = nullptr;
@@ -243,6 +245,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
+  HIPCHK(c, alloc(&c->shade, ns * sizeof(float4)));
   const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
   HIPCHK(c, alloc(&c->gi1, nc * gsz));
   HIPCHK(c, alloc(&c->gi2, nc * gsz));
@@ -663,6 +666,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   }
   if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
   if (packed) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
+  HIPCHK(c, launch_shade(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, st));
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
@@ -672,8 +676,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.upper = (L == c->N - 1) ? nullptr : srcGI;
     a.out = dstGI;
     a.dist = c->dist;
-    a.color = c->color_in;
-    a.emissive = c->emissive;
+    a.shade = c->shade;
     a.dirs = c->dirs + dir_table_offset(L);
     a.sky = c->sky;
     a.level = L;

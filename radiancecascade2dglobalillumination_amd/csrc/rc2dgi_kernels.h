@@ -66,8 +66,7 @@ struct RcLevelArgs {
   const float4 *upper;   // G_{L+1} (nullptr at the top level)
   float4 *out;           // G_L
   const unsigned short *dist;  // 16-bit distance q (screen)
-  const float4 *color;   // colorRT (screen)
-  const float4 *emissive;
+  const float4 *shade;   // surface records of the hittable texels (launch_shade)
   const float2 *dirs;    // 4^(L+1) (cos, sin)
   const float4 *sky;     // 4^N sky terms (top level)
   int level, N;
@@ -98,6 +97,11 @@ bool rc_variant_packed(int v);  // reads the packed distance field
 size_t dist_packed_bytes(int W, int H);
 hipError_t launch_dist_pack(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st);
 
+
+// surface records for the RC march's hits (k_shade): (emission, 1) or (albedo, reflectivity) at
+// every texel whose distance passes the march's hit test; other texels untouched
+hipError_t launch_shade(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
+                        ScreenDims s, float reflectivity, hipStream_t st);
 
 // one RadianceCascades.fs level
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);

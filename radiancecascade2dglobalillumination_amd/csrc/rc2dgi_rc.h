@@ -1,0 +1,620 @@
+// rc2dgi_rc.h -- the RadianceCascades.fs level kernel (k_rc_level) and its launch template,
+// shared by the translation units that instantiate its tile variants (rc2dgi_rc_*.hip, built in
+// parallel) and by rc2dgi_kernels.hip (decode_dist, the workgroup-order maps).
+#pragma once
+
+#include "rc2dgi_device.h"
+#include "rc2dgi_kernels.h"
+
+namespace rc2dgi {
+
+static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+// host-built workgroup map of one launch geometry (rc2dgi_kernels.hip)
+const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int ngrp, int code, int tile_w,
+                       int tile_h);
+
+// ---------------------------------------------------------------- RadianceCascades
+struct RcParams {
+  ScreenDims s;
+  CascadeDims c;
+  int level, bsc, bdx, bdy, tiles_x, tiles_per_block;
+  int p0, p1;  // probe rows [p0, p1) of every direction block (row-strip shards; 0, bdy otherwise)
+  float CRx, CRy, invCRx, invCRy, bdxf, bdyf, bs2;
+  float aspx, aspy, t0, t1, reflectivity;
+  float sWf, sHf;  // screen size as floats (power-of-two screen path)
+  const uint2 *wg_map;  // workgroup -> (tile x | y << 16, direction group), host-built (XCD remap + order)
+  int tpr;              // 8x8 tiles per row of the tiled distance field (TILED)
+};
+
+// q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
+// multiply and one fma residual correction reproduce the correctly rounded quotient for every
+// q in [0, 65535] (checked exhaustively with exact rational arithmetic, tests/test_kernels_cpu.py)
+__device__ __forceinline__ float decode_dist(unsigned q) {
+  const float c1 = 1.0f / 65535.0f;
+  const float qf = (float)q;
+  const float x = qf * c1;
+  const float r = __builtin_fmaf(-x, 65535.0f, qf);
+  return __builtin_fmaf(r, c1, x);
+}
+
+// a / n for the shader's divisions by a resolution: for a power-of-two n the quotient is
+// exactly a * (1/n) (both roundings are exact scalings), otherwise a true IEEE division
+__device__ __forceinline__ float div_res(float a, float n, float inv_n, int pow2) { return pow2 ? a * inv_n : a / n; }
+
+// Workgroup order.  Hardware deals consecutive workgroup ids round-robin over the 8 XCDs
+// (each with its own L2), so the physical id is remapped so that every XCD walks one
+// contiguous chunk of the logical order (bijective for any count, cdna_hip_programming.md
+// §5.5 T1).  Logical order is tile-major, direction-minor: the workgroups an XCD runs
+// together trace ALL directions of neighbouring probe tiles, so their distance-field
+// samples stay in a ring around those tiles (L2-resident) instead of sweeping the whole
+// field once per direction.
+
+// logical workgroup -> (tile, direction group).  odg == 0: tile-major, direction-minor.
+// Otherwise for patch: for direction group: for tile in patch: for direction in group -- the
+// workgroups an XCD runs together trace a few neighbouring tiles in a narrow fan of directions.
+// Patches of opx x opy tiles cover the tile grid row by row; the last patch row / column may be
+// partial (w x h tiles), which keeps the map a bijection for any grid.
+// Oriented orders (`oriented`, order code bit 24): for chunk of odg direction groups: for patch:
+// for tile in patch: for group in chunk.  A patch is opx tiles along the chunk's mean ray
+// direction and opy across it (axis-aligned: opx wide for directions within 45 degrees of the x
+// axis, opx tall otherwise), so the rays of an XCD's resident workgroups sweep a band along
+// their own direction and their distance samples share that XCD's L2.
+__host__ __device__ __forceinline__ void rc_order_map_oriented(int logical, int tiles_x, int tiles_y, int ngrp,
+                                                               int opx, int opy, int odg, int &tile, int &dgi) {
+  const int per_chunk = tiles_x * tiles_y * odg;
+  const int ch = logical / per_chunk;
+  const int rk = logical - ch * per_chunk;
+  const int tr = rk / odg, gi = rk - tr * odg;  // tile rank in the chunk, group in the chunk
+  // mean direction of the chunk: group g covers angles 2 pi [g, g+1) / ngrp
+  const float th = 6.28318530718f * ((float)ch * (float)odg + 0.5f * (float)odg) / (float)ngrp;
+  const bool along_x = fabsf(cosf(th)) >= fabsf(sinf(th));
+  const int px = along_x ? opx : opy, py = along_x ? opy : opx;
+  const int prow = tiles_x * py;  // tiles in a full patch row
+  const int pr = tr / prow;
+  int r = tr - pr * prow;
+  const int h = min(py, tiles_y - pr * py);
+  int pc = r / (px * h);
+  const int nfull = tiles_x / px;
+  if (pc > nfull) pc = nfull;  // the partial last column
+  r -= pc * px * h;
+  const int w = min(px, tiles_x - pc * px);
+  const int iy = r / w, ix = r - iy * w;
+  tile = (pr * py + iy) * tiles_x + pc * px + ix;
+  dgi = ch * odg + gi;
+}
+
+__host__ __device__ __forceinline__ void rc_order_map(int logical, int tiles_x, int tiles_y, int ngrp, int opx,
+                                                      int opy, int odg, int &tile, int &dgi, bool oriented = false) {
+  if (odg > 0 && oriented) {
+    rc_order_map_oriented(logical, tiles_x, tiles_y, ngrp, opx, opy, odg, tile, dgi);
+    return;
+  }
+  if (odg <= 0) {
+    tile = logical / ngrp;
+    dgi = logical - tile * ngrp;
+    return;
+  }
+  const int prow = tiles_x * opy * ngrp;  // workgroups in a full patch row
+  const int pr = logical / prow;
+  int r = logical - pr * prow;
+  const int h = min(opy, tiles_y - pr * opy);
+  const int pfull = opx * h * ngrp;  // workgroups in a full-width patch of this row
+  int pc = r / pfull;
+  const int nfull = tiles_x / opx;
+  if (pc > nfull) pc = nfull;  // the partial last column
+  r -= pc * pfull;
+  const int w = min(opx, tiles_x - pc * opx);
+  const int pt = w * h;
+  const int g = r / (pt * odg);
+  r -= g * pt * odg;
+  const int tip = r / odg, di = r - tip * odg;
+  const int iy = tip / w, ix = tip - iy * w;
+  tile = (pr * opy + iy) * tiles_x + pc * opx + ix;
+  dgi = g * odg + di;
+}
+
+// One workgroup = one TX x (TY*PY) tile of probes (coordsInBlock) and PD consecutive direction
+// blocks.  Every lane traces the same 4*PD directions (wave-uniform scalar table loads, parallel
+// rays); a lane owns PY probes (TY rows apart) and marches their 4*PY*PD rays in lockstep, so
+// each iteration keeps up to that many independent distance gathers in flight.  Rays of one
+// probe in neighbouring directions sample nearly the same texels (their lengths are highly
+// correlated too), so PD > 1 turns most of the extra gathers into L1 hits.
+// The level-(L+1) bilinear footprint of the tile -- block-local by the reference's clamp -- is
+// staged in LDS once per ray direction; its loads are issued before the march and written to
+// LDS after it (their latency hides under the march).
+#ifdef RC2DGI_DIAG_STATS
+// diagnostic builds only (python _build.py stats): per level, [0] lockstep ray slots executed
+// (iterations x rays per lane), [1] samples of live rays, [2] waves
+static __device__ unsigned long long g_rc_stats[16][3];
+#endif
+
+// floor(x) as an int in one instruction (x finite, within int range)
+__device__ __forceinline__ int cvt_floor(float x) {
+  int r;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// P2S: power-of-two screen and cascade sizes.  NEAREST + REPEAT of a position in [0, 1] is then
+// floor(p * n) & (n - 1) exactly, and the march's screen test is one unsigned compare per axis
+// (p is never NaN, and never -0: the origin term is > 0, and x + (-x) rounds to +0).
+// UNR: unroll factor of the march loop.  Fully unrolled (32) suits the gather-bound high levels;
+// rolled (1) the VALU-bound low levels.  Every build is held to 8 waves per SIMD
+// (amdgpu_waves_per_eu: SGPRs spill to VGPR lanes instead of the 106-SGPR allocation that caps a
+// CU at 6 workgroups of 256; L0 0.143 -> 0.133 ms).
+// TILED: `dist` is the 8x8-tiled copy (k_dist_tile): one 128-byte line holds an 8x8 texel tile,
+// so the nearly parallel rays of a lane (and vertical-ish steps) share lines.
+// GI: storage of the cascade textures (GiF32 / GiF16 / GiU8, rc2dgi_device.h).
+// the 16-bit distance q at byte offset `off` (32-bit offsets from the scalar base)
+__device__ __forceinline__ unsigned ld_dist(const unsigned short *dist, unsigned off) {
+  return *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + off);
+}
+
+// Packed distance field (DL = 2, k_dist_pack): one 16-byte packet per 14 texels of a row.  Bytes
+// 0-1 hold the packet's minimum q, byte 2 + t the excess q - min of texel t, or 255 (escape: read
+// the 16-bit field).  A distance field changes by at most 65535 / max(W, H) per texel plus the
+// jump flood's rare wrong seeds, so at 4096^2 the 13-texel span stays within 254 (measured: max
+// 234 over the demo and random scenes).  The 1.14 B/texel layout puts 112 texels of a row in one
+// 128-byte line instead of 64, and the field (19 MB at 4096^2 instead of 32 MB) fits the L2s better.
+constexpr int kPackTexels = 14;
+__host__ __device__ __forceinline__ int pack_per_row(int W) { return (W + kPackTexels - 1) / kPackTexels; }
+// ix / 14 for 0 <= ix < 16384 (37450 / 2^19 overestimates 1/14 by 2.3e-5: never crosses an integer)
+__device__ __forceinline__ unsigned pack_div14(unsigned ix) { return __umul24(ix, 37450u) >> 19; }
+__device__ __forceinline__ unsigned pack_byte(uint4 v, unsigned b) {  // byte b (0..15) of the packet
+  const unsigned long long h = b < 8u ? ((unsigned long long)v.y << 32 | v.x) : ((unsigned long long)v.w << 32 | v.z);
+  return (unsigned)(h >> ((b & 7u) * 8u)) & 0xFFu;
+}
+
+// one distance sample (q) of texel (ix, iy) = linear index idx, in layout DL
+template <int DL>
+__device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const uint4 *dpk, int tpr, int ix, int iy,
+                                            int idx) {
+  if constexpr (DL == 1) {
+    const unsigned t = ((__umul24((unsigned)iy >> 3, (unsigned)tpr) + ((unsigned)ix >> 3)) << 6) |
+                       (((unsigned)iy & 7u) << 3) | ((unsigned)ix & 7u);
+    return ld_dist(dist, t << 1);
+  } else if constexpr (DL == 2) {
+    const unsigned pk = pack_div14((unsigned)ix);
+    const uint4 v = dpk[__umul24((unsigned)iy, (unsigned)tpr) + pk];
+    const unsigned e = pack_byte(v, (unsigned)ix - pk * (unsigned)kPackTexels + 2u);
+    return e == 255u ? ld_dist(dist, (unsigned)idx << 1) : (v.x & 0xFFFFu) + e;
+  } else {
+    return ld_dist(dist, (unsigned)idx << 1);
+  }
+}
+
+// DL: distance-field layout the march reads: 0 pitch-linear uint16, 1 8x8-tiled (TILED), 2 packed
+// 14-texel row packets (`dpk`, see kPackTexels; power-of-two screens <= 16384).
+// Z0: level 0 on a power-of-two screen (t0 = 0): the first march iteration is shared by a probe's rays
+template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false>
+__global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
+                                                     typename GI::T *__restrict__ out,
+                                                     const unsigned short *__restrict__ dist,
+                                                     const float4 *__restrict__ shade,
+                                                     const float2 *__restrict__ dirs,
+                                                     const float4 *__restrict__ sky,
+                                                     const uint4 *__restrict__ dpk) {
+  constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
+  constexpr bool TILED = DL == 1, PACKED = DL == 2;
+  static_assert(!PACKED || P2S, "packed distance field: power-of-two screens only");
+  // staged footprint: taps of c in [c0, c0+T) lie in [c0/2 - 1, c0/2 + T/2]
+  constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
+  constexpr int NSTAGE = ND * RH * RW;
+  // staging assignment: wave w stages directions w, w + NW, ...; a lane the texels lane + 64 q of
+  // each, so the direction (and its footprint origin) is wave-uniform scalar arithmetic
+  constexpr int NW = NT / 64, DPW = ND / NW, FP = RH * RW, QPD = (FP + 63) / 64;
+  static_assert(NT % 64 == 0 && ND % NW == 0, "whole waves, whole directions per wave");
+  constexpr int PT = DPW * QPD;
+#ifdef RC2DGI_DIAG_NOMERGE
+  constexpr bool STG = false;  // timing-only ablation build: no upper staging, no merge (WRONG results)
+#else
+  constexpr bool STG = !TOP;  // stage and merge the level-(L+1) cascade
+#endif
+  __shared__ typename GI::S s_up[STG ? NSTAGE : 1];
+
+  const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
+  // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
+  const uint2 wgm = P.wg_map[blockIdx.x];
+  const int tx = (int)(wgm.x & 0xFFFFu), ty = (int)(wgm.x >> 16), dgi = (int)wgm.y;
+  (void)ngrp;
+  const int bi0 = dgi * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
+  const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
+  const int cx = cx0 + (int)(threadIdx.x % TX);
+  const int cyb = cy0 + (int)(threadIdx.x / TX);
+  const bool xok = cx < P.bdx;
+
+  // upper block of angleIndex a = 4*bi + r: (a mod 2b, a div 2b) in blocks of (bdx/2, bdy/2)
+  const int ubx = P.bdx >> 1, uby = P.bdy >> 1;
+  const int umask = 2 * P.bsc - 1, ushift = P.level + 1;
+  // staged texels as plain 32-bit components (HIP's vector unions defeat SROA -> scratch); raw
+  // storage bits, converted when written to LDS after the march
+  constexpr int NWD = GI::kBytes / 4;  // 32-bit words per texel
+  unsigned stx[!STG ? 1 : PT], sty[(!STG || NWD < 2) ? 1 : PT], stz[(!STG || NWD < 4) ? 1 : PT],
+      stw[(!STG || NWD < 4) ? 1 : PT];
+  const int lane = (int)threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int yy0 = lane / RW, xx0 = lane - (lane / RW) * RW;
+  // staging loads of the level-(L+1) footprint, issued now and written to LDS after the march.
+  // Level 0 issues its shared first distance sample before them (vmcnt retires in order, so
+  // the march then waits for that sample only).
+  auto stage_loads = [&]() {
+    if (STG) {
+  #pragma unroll
+      for (int j = 0; j < DPW; ++j) {
+        const int r = wv + j * NW;  // direction (of the 4*PD) this wave stages
+        const int a = bi0 * 4 + r;
+        const int bx = (a & umask) * ubx + (cx0 >> 1) - 1, by = (a >> ushift) * uby + (cy0 >> 1) - 1;
+        // REPEAT wrap only where the footprint crosses a texture edge (a wave-uniform branch)
+        const bool wrap = bx < 0 || bx + RW > P.c.CW || by < 0 || by + RH > P.c.CH;
+  #pragma unroll
+        for (int q = 0; q < QPD; ++q) {
+          // texel e = lane + 64 q of the footprint: (yy, xx) from the lane's (yy0, xx0), clamped to
+          // the footprint (unconditional loads keep the staging arrays in registers)
+          int xx = xx0 + (64 * q) % RW, yy = yy0 + (64 * q) / RW;
+          if (xx >= RW) {
+            xx -= RW;
+            ++yy;
+          }
+          if (yy >= RH) {
+            yy = RH - 1;
+            xx = RW - 1;
+          }
+          int gx = bx + xx, gy = by + yy;
+          if (wrap) {
+            gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
+            gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
+          }
+          const unsigned off = __umul24((unsigned)gy, (unsigned)P.c.pitch) + (unsigned)gx;
+          const typename GI::T v = upper[off];  // issued now, consumed after the march
+          const int t = j * QPD + q;
+          if constexpr (NWD == 1) {
+            stx[t] = v;
+          } else if constexpr (NWD == 2) {
+            stx[t] = v.x;
+            sty[t] = v.y;
+          } else {
+            stx[t] = __float_as_uint(v.x);
+            sty[t] = __float_as_uint(v.y);
+            stz[t] = __float_as_uint(v.z);
+            stw[t] = __float_as_uint(v.w);
+          }
+        }
+      }
+    }
+  };
+  if constexpr (!Z0) stage_loads();
+
+  const float cxf = (float)cx;
+  const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);  // rayOrigin / _CascadeResolution
+  float oy[PY];
+  bool pok[PY];
+#pragma unroll
+  for (int p = 0; p < PY; ++p) {
+    const int cy = cyb + p * TY;
+    pok[p] = xok && cy < P.p1;
+    oy[p] = div_res(((float)cy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P2S || P.c.powH);
+  }
+  const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
+
+  // ---- SampleRadianceSDF (RadianceCascades.fs:60-92), NR rays in lockstep; ray k = p*ND + r
+  float rdx[ND], rdy[ND];
+#pragma unroll
+  for (int r = 0; r < ND; ++r) {
+    const float2 d = dirs[bi0 * 4 + r];
+    rdx[r] = d.x;
+    rdy[r] = d.y;
+  }
+  float t[NR];
+  int hit_idx[NR];
+  bool act[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    t[k] = P.t0;
+    hit_idx[k] = -1;
+    act[k] = pok[k / ND] && !(P.t0 > P.t1);  // act: the ray takes another sample (t <= t1 folded in)
+  }
+#ifndef RC2DGI_DIAG_MAX_ITERS
+#define RC2DGI_DIAG_MAX_ITERS 32  // RadianceCascades.fs:64 (diagnostic builds may cap it; never shipped)
+#endif
+#ifdef RC2DGI_DIAG_STATS
+  unsigned diag_slots = 0, diag_samples = 0;
+#endif
+  constexpr int it0 = Z0 ? 1 : 0;
+  if constexpr (Z0) {
+    // level 0 (t0 = 0): every ray of a probe starts at the probe centre, x = o + (0*dir)*asp = o
+    // exactly, so the first iteration is one shared sample per probe instead of one per ray
+    bool zlive[PY];
+    int zidx[PY];
+    unsigned zq[PY];
+#pragma unroll
+    for (int p = 0; p < PY; ++p) {
+      zlive[p] = act[p * ND] && __float_as_uint(ox) <= 0x3f800000u && __float_as_uint(oy[p]) <= 0x3f800000u;
+      int ix = cvt_floor(ox * P.sWf) & (P.s.W - 1);
+      int iy = cvt_floor(oy[p] * P.sHf) & (P.s.H - 1);
+      if (!zlive[p]) ix = iy = 0;
+      zidx[p] = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
+      zq[p] = fetch_q<DL>(dist, dpk, P.tpr, ix, iy, zidx[p]);
+    }
+    stage_loads();
+#pragma unroll
+    for (int p = 0; p < PY; ++p) {
+      const bool live = zlive[p];
+      const int idx = zidx[p];
+      const float d = decode_dist(zq[p]);
+      const bool hit = live && d < 0.001f;
+#pragma unroll
+      for (int r = 0; r < ND; ++r) {
+        const int k = p * ND + r;
+        hit_idx[k] = hit ? idx : -1;
+        t[k] = live && !hit ? P.t0 + d : P.t0;
+        act[k] = live && !hit && !(t[k] > P.t1);
+      }
+#ifdef RC2DGI_DIAG_STATS
+      diag_samples += live ? (unsigned)ND : 0u;
+#endif
+    }
+#ifdef RC2DGI_DIAG_STATS
+    diag_slots += NR;
+#endif
+  }
+  bool more = false;  // a ray of this lane still marches
+#pragma unroll
+  for (int k = 0; k < NR; ++k) more |= act[k];
+#pragma unroll UNR
+  for (int it = it0; more && it < RC2DGI_DIAG_MAX_ITERS; ++it) {
+    int idx[NR];
+    unsigned didx[NR];  // distance-field index (tiled or linear) or packet (packed)
+    unsigned psub[PACKED ? NR : 1];  // packed: byte of the texel in its packet
+    bool live[NR];
+    bool any_live = false;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int r = k % ND, p = k / ND;
+      const float px = ox + (t[k] * rdx[r]) * P.aspy;
+      const float py = oy[p] + (t[k] * rdy[r]) * P.aspx;
+      int ix, iy;
+      if constexpr (P2S) {
+        live[k] = act[k] && __float_as_uint(px) <= 0x3f800000u && __float_as_uint(py) <= 0x3f800000u;
+        ix = cvt_floor(px * P.sWf) & (P.s.W - 1);
+        iy = cvt_floor(py * P.sHf) & (P.s.H - 1);
+      } else {
+        live[k] = act[k] && !(px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+        ix = wrap_nearest(px, sax);
+        iy = wrap_nearest(py, say);
+      }
+      if (!live[k]) ix = iy = 0;
+      idx[k] = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;  // < 2^24 operands
+      if constexpr (TILED) {
+        didx[k] = ((__umul24((unsigned)iy >> 3, (unsigned)P.tpr) + ((unsigned)ix >> 3)) << 6) |
+                  (((unsigned)iy & 7u) << 3) | ((unsigned)ix & 7u);
+      } else if constexpr (PACKED) {
+        const unsigned pk = pack_div14((unsigned)ix);
+        didx[k] = __umul24((unsigned)iy, (unsigned)P.tpr) + pk;  // packet
+        psub[k] = (unsigned)ix - pk * (unsigned)kPackTexels + 2u;  // its byte
+      } else {
+        didx[k] = (unsigned)idx[k];
+      }
+      act[k] = live[k];
+      any_live |= live[k];
+    }
+    if (!any_live) break;  // every ray left its interval or the screen: no more samples
+#ifdef RC2DGI_DIAG_STATS
+    diag_slots += NR;
+    for (int k = 0; k < NR; ++k) diag_samples += live[k] ? 1u : 0u;
+#endif
+    unsigned q[NR];
+    if constexpr (PACKED) {
+      uint4 pv[NR];
+#pragma unroll
+      for (int k = 0; k < NR; ++k)  // dead rays re-read packet 0
+        pv[k] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(dpk) + (didx[k] << 4));
+      bool esc = false;
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        const unsigned e = pack_byte(pv[k], psub[k]);
+        q[k] = (pv[k].x & 0xFFFFu) + e;
+        esc |= e == 255u;
+      }
+      if (esc) {  // rare: some texel's excess did not fit a byte
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+          if (pack_byte(pv[k], psub[k]) == 255u) q[k] = ld_dist(dist, (unsigned)idx[k] << 1);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
+        q[k] = ld_dist(dist, didx[k] << 1);
+    }
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {  // branch-free: selects, no exec-mask juggling
+      const float d = decode_dist(q[k]);
+      const bool hit = live[k] && d < 0.001f;
+      hit_idx[k] = hit ? idx[k] : hit_idx[k];
+      t[k] = live[k] && !hit ? t[k] + d : t[k];
+      act[k] = live[k] && !hit && !(t[k] > P.t1);  // the next iteration's interval test, done now
+      any |= act[k];
+    }
+    if (!any) break;
+  }
+#ifdef RC2DGI_DIAG_STATS
+  if (pok[0] || true) {
+    atomicAdd(&g_rc_stats[P.level][0], (unsigned long long)diag_slots);
+    atomicAdd(&g_rc_stats[P.level][1], (unsigned long long)diag_samples);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_rc_stats[P.level][2], 1ull);
+  }
+#endif
+
+  if (STG) {
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+#pragma unroll
+      for (int q = 0; q < QPD; ++q) {
+        const int e = lane + 64 * q, t = j * QPD + q;
+        const int k = (wv + j * NW) * FP + e;
+        if (64 * (q + 1) <= FP || e < FP) {
+          if constexpr (NWD == 1)
+            s_up[k] = GI::stage(stx[t], 0u, 0u, 0u);
+          else if constexpr (NWD == 2)
+            s_up[k] = GI::stage(stx[t], sty[t], 0u, 0u);
+          else
+            s_up[k] = GI::stage(stx[t], sty[t], stz[t], stw[t]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
+  const bool pow2c = P2S || (P.c.powW && P.c.powH);  // P2S implies power-of-two cascades
+#pragma unroll
+  for (int p = 0; p < PY; ++p) {
+    if (!pok[p]) continue;
+    const int cy = cyb + p * TY;
+    const float cyf = (float)cy;
+    // upper sample position inside the level-(L+1) block (RadianceCascades.fs:131-139)
+    float px = cxf * 0.5f + 0.25f, py = cyf * 0.5f + 0.25f;
+    px = fminf(fmaxf(px, 0.5f), P.bdxf * 0.5f - 0.5f);
+    py = fminf(fmaxf(py, 0.5f), P.bdyf * 0.5f - 0.5f);
+    // Power-of-two cascade resolution: every quantity below is an exact multiple of 1/4, so
+    // x = samplePos * CW - 0.5 = px - 0.5 + offset*blockDim/2 exactly: all rays share the
+    // bilinear weights and (relative to their staged footprints) the tap coordinates.
+    int lx0 = 0, ly0 = 0;
+    float wx = 0.0f, wy = 0.0f;
+    if (!TOP && pow2c) {
+      const float fx = floorf(px - 0.5f), fy = floorf(py - 0.5f);
+      wx = (px - 0.5f) - fx;
+      wy = (py - 0.5f) - fy;
+      lx0 = (int)fx - ((cx0 >> 1) - 1);
+      ly0 = (int)fy - ((cy0 >> 1) - 1);
+    }
+    // hit shading of the probe's rays (RadianceCascades.fs:79-86): one load of the texel's
+    // surface record (k_shade: the emissive or the albedo + reflectivity branch, resolved once
+    // per frame for every hittable texel)
+    float4 hr[ND];
+#pragma unroll
+    for (int r = 0; r < ND; ++r) {
+      const int k = p * ND + r;
+      hr[r] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+      if (hit_idx[k] >= 0) hr[r] = shade[hit_idx[k]];
+    }
+#pragma unroll
+    for (int dblk = 0; dblk < PD; ++dblk) {
+      const int bi = bi0 + dblk;
+      float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int r = dblk * 4 + r4;  // index into the 4*PD directions
+        float4 rad = hr[r];
+        const int ai = bi * 4 + r4;  // angleIndex
+        if (rad.w != 0.0f && (STG || TOP)) {
+          if (!TOP) {
+            typename GI::S t00, t10, t01, t11;
+            float ux = wx, uy = wy;
+            if (pow2c) {
+              const typename GI::S *sr = s_up + r * RH * RW;
+              t00 = sr[ly0 * RW + lx0];
+              t10 = sr[ly0 * RW + lx0 + 1];
+              t01 = sr[(ly0 + 1) * RW + lx0];
+              t11 = sr[(ly0 + 1) * RW + lx0 + 1];
+            } else if constexpr (!P2S) {
+              // general GL path (mod(float(angleIndex), 2b), floor(float(angleIndex)/2b) are exact integers)
+              const float offx = (float)(ai & umask), offy = (float)(ai >> ushift);
+              const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
+              const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
+              int x0, x1, y0, y1;
+              wrap_linear(sx, Axis{P.c.CW, 0}, x0, x1, ux);
+              wrap_linear(sy, Axis{P.c.CH, 0}, y0, y1, uy);
+              const int rx0 = (ai & umask) * ubx + (cx0 >> 1) - 1, ry0 = (ai >> ushift) * uby + (cy0 >> 1) - 1;
+              auto rel = [](int g, int o, int n) {
+                int l = g - o;
+                return l < 0 ? l + n : (l >= n ? l - n : l);
+              };
+              const int a0 = rel(x0, rx0, P.c.CW), a1 = rel(x1, rx0, P.c.CW);
+              const int b0 = rel(y0, ry0, P.c.CH), b1 = rel(y1, ry0, P.c.CH);
+              if ((unsigned)a0 < (unsigned)RW && (unsigned)a1 < (unsigned)RW && (unsigned)b0 < (unsigned)RH &&
+                  (unsigned)b1 < (unsigned)RH) {
+                const typename GI::S *sr = s_up + r * RH * RW;
+                t00 = sr[b0 * RW + a0];
+                t10 = sr[b0 * RW + a1];
+                t01 = sr[b1 * RW + a0];
+                t11 = sr[b1 * RW + a1];
+              } else {
+                // rounding stepped outside the staged footprint: read HBM.  Non-temporal loads
+                // keep the compiler from fusing this path with the LDS path into flat loads.
+                t00 = GI::ld_stage_nt(&upper[(size_t)y0 * P.c.pitch + x0]);
+                t10 = GI::ld_stage_nt(&upper[(size_t)y0 * P.c.pitch + x1]);
+                t01 = GI::ld_stage_nt(&upper[(size_t)y1 * P.c.pitch + x0]);
+                t11 = GI::ld_stage_nt(&upper[(size_t)y1 * P.c.pitch + x1]);
+              }
+            }
+            const float4 up = GI::bilerp(t00, t10, t01, t11, ux, uy);
+            rad.x = rad.x + up.x * rad.w;
+            rad.y = rad.y + up.y * rad.w;
+            rad.z = rad.z + up.z * rad.w;
+            rad.w = rad.w * up.w;
+          } else {
+            const float4 sk = sky[ai];  // top cascade: analytic sky, tabulated per angleIndex
+            rad.x = rad.x + sk.x;
+            rad.y = rad.y + sk.y;
+            rad.z = rad.z + sk.z;
+          }
+        }
+        acc.x = acc.x + rad.x * 0.25f;
+        acc.y = acc.y + rad.y * 0.25f;
+        acc.z = acc.z + rad.z * 0.25f;
+        acc.w = acc.w + rad.w * 0.25f;
+      }
+      const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
+      const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
+      GI::st(&out[(size_t)j * P.c.pitch + i], GI::blend_black(acc));
+    }
+  }
+}
+
+template <int TX, int TY, int PY, int PD = 1, int UNR = 1, int DL = 0, class GI = GiF32>
+static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
+  const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
+  if constexpr (DL == 2) {  // packed field: power-of-two screens up to 16384 wide; same bits either way
+    if (!p2s || P.s.W > 16384) return launch_rc_tiles<TX, TY, PY, PD, UNR, 0, GI>(a, P, st);
+    if (!a.dist_packed) return hipErrorInvalidValue;
+  }
+  P.tiles_x = ceil_div(P.bdx, TX);
+  const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
+  P.tiles_per_block = P.tiles_x * tiles_y;
+  const int nwg = P.tiles_per_block * P.bsc * P.bsc / PD;
+  // workgroup order (tuning "rc_order", rc_logical_order); tile coordinates fit the map's
+  // 16-bit fields (<= 32768 probes per axis)
+  const int ngrp = P.bsc * P.bsc / PD;
+  P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, a.order_code, TX, TY * PY);
+  if (!P.wg_map) return hipErrorOutOfMemory;
+  P.tpr = DL == 2 ? pack_per_row(P.s.W) : (P.s.W + 7) / 8;
+  if (DL == 1 && !a.dist_tiled) return hipErrorInvalidValue;
+  P.sWf = (float)P.s.W;
+  P.sHf = (float)P.s.H;
+#define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \
+  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL == 2 ? 0 : DL)), GI, Z0V>), \
+                     dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),   \
+                     reinterpret_cast<typename GI::T *>(a.out), DL == 1 ? a.dist_tiled : a.dist, a.shade,     \
+                     a.dirs, a.sky, a.dist_packed)
+  const bool top = a.level == a.N - 1;
+  if (top) {
+    if (p2s) RC2DGI_RC(true, true, false); else RC2DGI_RC(true, false, false);
+  } else if (p2s) {
+    // level 0: t0 = CalculateRayRange's start 0 -> the shared first sample
+    if (a.level == 0 && P.t0 == 0.0f) RC2DGI_RC(false, true, true); else RC2DGI_RC(false, true, false);
+  } else {
+    RC2DGI_RC(false, false, false);
+  }
+#undef RC2DGI_RC
+  return hipGetLastError();
+}
+
+// per translation unit dispatchers of the tile variants (rc2dgi_rc_*.hip)
+hipError_t launch_rc_f32_rolled(const RcLevelArgs &a, RcParams P, hipStream_t st);
+hipError_t launch_rc_f32_unrolled(const RcLevelArgs &a, RcParams P, hipStream_t st);
+hipError_t launch_rc_f16(const RcLevelArgs &a, RcParams P, hipStream_t st);
+hipError_t launch_rc_u8(const RcLevelArgs &a, RcParams P, hipStream_t st);
+
+}  // namespace rc2dgi

@@ -1,0 +1,18 @@
+// rc2dgi_rc_u8.hip -- k_rc_level tile variants: RGBA8 cascades (RC2DGI_STORAGE_RGBA8_COMPAT), the 16x16 family (one translation unit per family so
+// that the variants compile in parallel; the kernel itself is rc2dgi_rc.h).
+#include "rc2dgi_rc.h"
+
+namespace rc2dgi {
+
+hipError_t launch_rc_u8(const RcLevelArgs &a, RcParams P, hipStream_t st) {
+  switch (a.variant) {
+    case 13: return launch_rc_tiles<16, 16, 1, 1, 32, 0, GiU8>(a, P, st);
+    case 14: return launch_rc_tiles<16, 16, 1, 1, 32, 1, GiU8>(a, P, st);
+    case 15: return launch_rc_tiles<16, 16, 1, 1, 1, 1, GiU8>(a, P, st);
+    case 16: return launch_rc_tiles<16, 16, 1, 1, 32, 2, GiU8>(a, P, st);
+    case 17: return launch_rc_tiles<16, 16, 1, 1, 1, 2, GiU8>(a, P, st);
+    default: return launch_rc_tiles<16, 16, 1, 1, 1, 0, GiU8>(a, P, st);
+  }
+}
+
+}  // namespace rc2dgi
