@@ -158,10 +158,17 @@ def sweep_rc(ctx, N, steps, rounds=3):
                       "names": [lib_variant_name(v) for v in range(nv)]}), flush=True)
 
 
+def schedule_path(W, H, N, storage="f32"):
+    """The committed RC schedule (per-level rc_order / rc_variant) for a configuration: picked by
+    rc2dgi_autotune on an MI355X (bench.py --autotune --save-tuning), loaded by the bench and by
+    the parity tests, so the schedule that is timed is the schedule that is tested."""
+    return os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning", f"{W}x{H}_N{N}_{storage}.json")
+
+
 def lib_variant_name(v):
     names = ["16x16x1", "16x8x2", "16x16x2", "32x8x1", "64x4x1", "8x8x1", "32x8x2", "16x16x1d2", "16x16x1d4",
              "16x8x1d2", "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t",
-             "16x16x1up", "16x16x1p"]
+             "16x16x1up", "16x16x1un", "16x16x1p", "16x16x1n"]
     return names[v] if v < len(names) else str(v)
 
 
@@ -187,7 +194,15 @@ def bench_batch(a, rank, local, world):
         shared = torch.cuda.Stream(device=local)
         for g in ctxs:
             g.set_stream(shared.cuda_stream)
-    if ctxs and not a.no_autotune:  # setup: one context picks the schedule, the others reuse it
+    committed = schedule_path(W, H, N)
+    if ctxs and not a.no_autotune and not a.autotune and os.path.exists(committed):
+        with open(committed) as f:  # the committed schedule of this size (tested by the parity suite)
+            tun = json.load(f)
+        for g in ctxs:
+            for L in range(N):
+                g.set_tuning(f"rc_order_L{L}", tun["rc_order"][L])
+                g.set_tuning(f"rc_variant_L{L}", tun["rc_variant"][L])
+    elif ctxs and not a.no_autotune:  # setup: one context picks the schedule, the others reuse it
         ctxs[0].autotune(3)
         for g in ctxs[1:]:
             for L in range(N):
@@ -319,7 +334,10 @@ def main():
                     help="f16: giRT1/2 as RGBA16F (RC2DGI.cs:105-106, SURVEY 8 f4); rgba8: every render texture "
                          "RGBA8 with GL unorm8 arithmetic, the literal app (SURVEY 8 f3)")
     ap.add_argument("--no-autotune", action="store_true",
-                    help="keep the default RC workgroup order (setup otherwise times the candidates per level)")
+                    help="keep the library's default RC schedule (no committed schedule, no autotune)")
+    ap.add_argument("--autotune", action="store_true",
+                    help="time the RC schedule candidates in setup instead of loading the committed schedule "
+                         "(radiancecascade2dglobalillumination_amd/tuning/<W>x<H>_N<N>_<storage>.json)")
     ap.add_argument("--save-tuning", default="", help="write the chosen per-level rc_order / rc_variant (JSON)")
     ap.add_argument("--load-tuning", default="",
                     help="apply per-level rc_order / rc_variant from a --save-tuning file instead of autotuning "
@@ -352,6 +370,9 @@ def main():
     # inputs resident in HBM before the timed region
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
+    committed = schedule_path(W, H, N, a.storage)
+    if not a.load_tuning and not a.autotune and not a.no_autotune and os.path.exists(committed):
+        a.load_tuning = committed  # the committed schedule: the one the parity tests check at this size
     if a.load_tuning:
         with open(a.load_tuning) as f:
             tun = json.load(f)
@@ -365,7 +386,8 @@ def main():
     orders = [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)] if orders else None
     if a.save_tuning and rank == 0:
         with open(a.save_tuning, "w") as f:
-            json.dump({"rc_order": [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)], "rc_variant": variants}, f)
+            json.dump({"config": f"{W}x{H} N={N} rayRange={a.ray_range} {a.storage}",
+                       "rc_order": [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)], "rc_variant": variants}, f)
     ctx.set_timing(True)
     if a.sweep_rc:
         sweep_rc(ctx, N, a.steps, rounds=3)
@@ -420,7 +442,9 @@ def main():
         "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}", "screen": [W, H],
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
                    "parallelism": f"replicas{world}",
-                   "rc_order": orders or "default", "rc_variant": variants},
+                   "rc_order": orders or "default", "rc_variant": variants,
+                   "rc_schedule": (os.path.relpath(a.load_tuning, ROOT) if a.load_tuning else
+                                   ("default" if a.no_autotune else "autotune in setup"))},
         "rc_ms_per_frame": round(t_rc / a.steps, 4),
         "rc_level_ms": [round(x / a.steps, 4) for x in lvl_ms.tolist()],
         "full_pipeline_ms": round(t_tot / a.steps, 4),

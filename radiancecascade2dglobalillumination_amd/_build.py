@@ -51,6 +51,7 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) 
 
     objdir = os.path.join(ROOT, "build", "obj", os.path.basename(out).replace(".so", ""))
     os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     base = [hipcc()] + FLAGS + list(extra) + ["-I", os.path.join(ROOT, "include")]
 
     def compile_one(src):
@@ -81,12 +82,17 @@ if __name__ == "__main__":
         # timing-only ablation build: march capped at N iterations (WRONG results by design)
         n = sys.argv[2] if len(sys.argv) > 2 else "6"
         print(build(force=True, verbose=True, extra=[f"-DRC2DGI_DIAG_MAX_ITERS={n}"],
-                    out=os.path.join(HERE, f"librc2dgi_diag{n}.so")))
+                    out=os.path.join(ROOT, "build", "diag", f"librc2dgi_diag{n}.so")))
     elif len(sys.argv) > 1 and sys.argv[1] == "nomerge":
         # timing-only ablation build: RC levels without the upper-cascade staging and merge (WRONG results)
-        print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_NOMERGE"], out=os.path.join(HERE, "librc2dgi_nomerge.so")))
+        print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_NOMERGE"], out=os.path.join(ROOT, "build", "diag", "librc2dgi_nomerge.so")))
+    elif len(sys.argv) > 1 and sys.argv[1] == "escplain":
+        # diagnostic build reproducing DESIGN.md §5.3: packed-field escape loads waited for at the branch
+        # join (WRONG, run-to-run different results on gfx950).  Extra flags after the mode are passed on.
+        print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_ESC_PLAIN"] + sys.argv[2:],
+                    out=os.path.join(ROOT, "build", "diag", "librc2dgi_escplain.so")))
     elif len(sys.argv) > 1 and sys.argv[1] == "stats":
         # diagnostic build: march statistics per level (rc2dgi_diag_stats; atomics, slower)
-        print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_STATS"], out=os.path.join(HERE, "librc2dgi_stats.so")))
+        print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_STATS"], out=os.path.join(ROOT, "build", "diag", "librc2dgi_stats.so")))
     else:
         print(build(force=True, verbose=True))

@@ -91,6 +91,7 @@ struct rc2dgi_ctx {
   unsigned short *dist = nullptr;  // packUNorm16 q
   unsigned short *dist_t = nullptr;  // 8x8-tiled copy for the "t" RC variants
   uint4 *dist_p = nullptr;           // packed copy for the "p" RC variants (k_dist_pack)
+  uint4 *dist_n = nullptr;           // nibble-predicted copy for the "n" RC variants (k_dist_nib)
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
@@ -180,7 +181,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->rc_maps.clear();
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
-                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->shade};
+                  c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   c->color_in = c->emissive = c->temp = c->color_out = nullptr;
@@ -188,6 +189,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->occ = nullptr;
   c->dist = c->dist_t = nullptr;
   c->dist_p = nullptr;
+  c->dist_n = nullptr;
   c->shade = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
@@ -245,6 +247,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
   HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
+  HIPCHK(c, alloc(&c->dist_n, dist_nib_bytes(c->W, c->H)));
   HIPCHK(c, alloc(&c->shade, ns * sizeof(float4)));
   const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
   HIPCHK(c, alloc(&c->gi1, nc * gsz));
@@ -659,13 +662,15 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362).  The "t" / "p" / "o" variants read re-laid-out
   // copies of distRT; building them is timed with the top level (it is RC work, not DistanceField's)
   if (T) HIPCHK(c, hipEventRecord(c->ev_level[c->N], st));
-  bool tiled = false, packed = false;
+  bool tiled = false, packed = false, nib = false;
   for (int v : c->rc_variant) {
     tiled |= rc_variant_tiled(v);
     packed |= rc_variant_packed(v);
+    nib |= rc_variant_nib(v);
   }
   if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
   if (packed) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
+  if (nib) HIPCHK(c, launch_dist_nib(c->dist, c->sd.pitch, c->dist_n, c->W, c->H, st));
   HIPCHK(c, launch_shade(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, st));
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
@@ -688,6 +693,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.map_cache = &c->rc_maps;
     a.dist_tiled = c->dist_t;
     a.dist_packed = c->dist_p;
+    a.dist_nib = c->dist_n;
 
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
@@ -789,8 +795,9 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   const bool timing = c->timing;
   c->timing = true;
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
-  // march rolled / unrolled x linear / 8x8-tiled / packed distance field; 32x8 tiles (x2 probes per lane)
-  const int kVariants[] = {0, 3, 6, 13, 14, 15, 16};
+  // march rolled / unrolled x linear / 8x8-tiled / packed / nibble-predicted distance field; 32x8 tiles
+  // (x2 probes per lane)
+  const int kVariants[] = {0, 3, 6, 13, 14, 15, 16, 17, 18, 19};
   const int nv = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
   std::vector<float> best(c->N, 1e30f);
   std::vector<int> pick(c->rc_order), pickv(c->rc_variant);
@@ -823,6 +830,7 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   c->rc_order = pick;
   c->rc_variant = pickv;
   c->timing = timing;
+  c->rc_maps.retain(pick);  // the maps of the candidates that lost are device memory for nothing
   return RC2DGI_OK;
 }
 

@@ -59,6 +59,7 @@ struct RcMapCache {
   };
   std::vector<Entry> entries;
   void clear();
+  void retain(const std::vector<int> &codes);  // free the maps of every other order code
   ~RcMapCache();
 };
 
@@ -77,6 +78,7 @@ struct RcLevelArgs {
   RcMapCache *map_cache = nullptr;  // where the launch finds / builds its workgroup map
   const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
+  const uint4 *dist_nib = nullptr;             // nibble-predicted distance field (variants "n", k_dist_nib)
 };
 
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
@@ -92,10 +94,14 @@ int rc_variant_count();
 const char *rc_variant_name(int v);
 bool rc_variant_tiled(int v);  // reads the 8x8-tiled distance field
 bool rc_variant_packed(int v);  // reads the packed distance field
+bool rc_variant_nib(int v);     // reads the nibble-predicted distance field
 
 // distRT -> packed 14-texel packets (16 B each: the minimum q + one excess byte per texel)
 size_t dist_packed_bytes(int W, int H);
 hipError_t launch_dist_pack(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st);
+// distRT -> nibble-predicted 26-texel packets (base, slope, one 4-bit residual per texel)
+size_t dist_nib_bytes(int W, int H);
+hipError_t launch_dist_nib(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st);
 
 
 // surface records for the RC march's hits (k_shade): (emission, 1) or (albedo, reflectivity) at

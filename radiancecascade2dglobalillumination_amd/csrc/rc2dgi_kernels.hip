@@ -404,6 +404,61 @@ __global__ __launch_bounds__(256) void k_dist_pack(const unsigned short *__restr
   packed[(size_t)j * ppr + k] = o;
 }
 
+// dist (pitch-linear) -> nibble-predicted packets (kNibTexels, packet_q<3>): one thread per packet.
+// The slope is the best (fewest escapes) of five around the packet's end-to-end slope; the base
+// centres the residuals of that slope, clamped to 16 bits.  Texels past the row's end are escapes.
+__global__ __launch_bounds__(256) void k_dist_nib(const unsigned short *__restrict__ dist, int pitch,
+                                                  uint4 *__restrict__ packed, int ppr, int W, int H) {
+  const int k = blockIdx.x * 256 + (int)threadIdx.x, j = blockIdx.y;
+  if (k >= ppr || j >= H) return;
+  const int x0 = k * kNibTexels;
+  const int cnt = min(kNibTexels, W - x0);
+  // 26 texels = 13 dwords, 4-byte aligned (a packet starts at byte 52 k of a 128-byte aligned row)
+  const unsigned *src = reinterpret_cast<const unsigned *>(dist + (size_t)j * pitch + x0);
+  int q[kNibTexels];
+#pragma unroll
+  for (int w = 0; w < kNibTexels / 2; ++w) {
+    const unsigned v = x0 + 2 * w < W ? src[w] : 0u;
+    q[2 * w] = (int)(v & 0xFFFFu);
+    q[2 * w + 1] = (int)(v >> 16);
+  }
+  const int qa = q[0], qb = q[cnt - 1 < 0 ? 0 : cnt - 1];
+  const int s0 = cnt > 1 ? (int)floorf((float)(qb - qa) / (float)(cnt - 1) + 0.5f) : 0;
+  int best_s = 0, best_base = 0, best_esc = kNibTexels + 1;
+  for (int ds = -2; ds <= 2; ++ds) {
+    const int sl = min(127, max(-128, s0 + ds));
+    int lo = 1 << 30, hi = -(1 << 30);
+#pragma unroll
+    for (int t = 0; t < kNibTexels; ++t)
+      if (t < cnt) {
+        const int r = q[t] - sl * t;
+        lo = min(lo, r);
+        hi = max(hi, r);
+      }
+    const int base = min(65535, max(0, (lo + hi) >> 1));
+    int esc = 0;
+#pragma unroll
+    for (int t = 0; t < kNibTexels; ++t) {
+      const int r = q[t] - sl * t - base;
+      esc += (t < cnt && (r < -7 || r > 7)) ? 1 : 0;
+    }
+    if (esc < best_esc) {
+      best_esc = esc;
+      best_s = sl;
+      best_base = base;
+    }
+  }
+  unsigned w[4] = {(unsigned)best_base | ((unsigned)(best_s & 0xFF) << 16), 0u, 0u, 0u};
+#pragma unroll
+  for (int t = 0; t < kNibTexels; ++t) {
+    const int r = q[t] - best_s * t - best_base;
+    const unsigned n = (t < cnt && r >= -7 && r <= 7) ? (unsigned)(r + 7) : 15u;
+    const int b = 24 + 4 * t;
+    w[b >> 5] |= n << (b & 31);
+  }
+  packed[(size_t)j * ppr + k] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // ---------------------------------------------------------------- Blur + copy-back
 template <class GI>
 __global__ __launch_bounds__(256) void k_blur(const typename GI::T *__restrict__ gi,
@@ -760,6 +815,17 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
 
 RcMapCache::~RcMapCache() { clear(); }
 
+void RcMapCache::retain(const std::vector<int> &codes) {
+  std::vector<Entry> kept;
+  for (auto &e : entries) {
+    if (std::find(codes.begin(), codes.end(), e.code) != codes.end() || e.code == 0)
+      kept.push_back(e);
+    else if (e.dev)
+      (void)hipFree(e.dev);
+  }
+  entries.swap(kept);
+}
+
 void RcMapCache::clear() {
   for (auto &e : entries)
     if (e.dev) (void)hipFree(e.dev);
@@ -810,6 +876,10 @@ static std::vector<uint2> rc_logical_order(int code, int tiles_x, int tiles_y, i
 const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int ngrp, int code, int tile_w,
                               int tile_h) {
   if (!cache) return nullptr;
+  {  // an order code that does not tile this geometry runs tile-major: share the code-0 map
+    const int opx = code & 0xFF, opy = (code >> 8) & 0xFF, odg = (code >> 16) & 0xFF;
+    if (odg <= 0 || opx <= 0 || opy <= 0 || ngrp % odg) code = 0;
+  }
   for (auto &e : cache->entries)
     if (e.nwg == nwg && e.tiles_x == tiles_x && e.tiles_y == tiles_y && e.ngrp == ngrp && e.code == code &&
         e.tile_w == tile_w && e.tile_h == tile_h)
@@ -835,15 +905,16 @@ const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int
 
 // RC tile variants (tuning knob "rc_variant"): TXxTYxPY probes per workgroup, "dD" = D direction
 // blocks per workgroup (needs 4^level >= D; falls back to d1 below that)
-// ("u": march loop fully unrolled, "t": 8x8-tiled distance field, "p": packed distance field; the rolled
-// packed march was dropped: its GiF16 build gave run-to-run different results on gfx950)
+// ("u": march loop fully unrolled, "t": 8x8-tiled distance field, "p": packed 14-texel distance field,
+// "n": nibble-predicted 26-texel distance field)
 static const char *kRcVariantNames[] = {"16x16x1", "16x8x2",   "16x16x2",  "32x8x1",   "64x4x1",
                                         "8x8x1",   "32x8x2",   "16x16x1d2", "16x16x1d4", "16x8x1d2",
                                         "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t",
-                                        "16x16x1up", "16x16x1p"};
+                                        "16x16x1up", "16x16x1un", "16x16x1p", "16x16x1n"};
 int rc_variant_count() { return (int)(sizeof(kRcVariantNames) / sizeof(kRcVariantNames[0])); }
 bool rc_variant_tiled(int v) { return v == 14 || v == 15; }
-bool rc_variant_packed(int v) { return v == 16 || v == 17; }
+bool rc_variant_packed(int v) { return v == 16 || v == 18; }
+bool rc_variant_nib(int v) { return v == 17 || v == 19; }
 const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
@@ -878,7 +949,7 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
     e = launch_rc_u8(a, P, st);  // RGBA8 cascades: the 16x16x1 family only
   else if (c.gi_f16)
     e = launch_rc_f16(a, P, st);  // RGBA16F cascades: the 16x16x1 family only
-  else if (a.variant >= 13)
+  else if (a.variant >= 13 && a.variant < rc_variant_count())
     e = launch_rc_f32_unrolled(a, P, st);
   else
     e = launch_rc_f32_rolled(a, P, st);
@@ -1032,6 +1103,14 @@ size_t dist_packed_bytes(int W, int H) { return (size_t)pack_per_row(W) * H * si
 hipError_t launch_dist_pack(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st) {
   const int ppr = pack_per_row(W);
   hipLaunchKernelGGL(k_dist_pack, dim3(ceil_div(ppr, 256), H), dim3(256), 0, st, dist, pitch, packed, ppr, W, H);
+  return hipGetLastError();
+}
+
+size_t dist_nib_bytes(int W, int H) { return (size_t)nib_per_row(W) * H * sizeof(uint4); }
+
+hipError_t launch_dist_nib(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st) {
+  const int ppr = nib_per_row(W);
+  hipLaunchKernelGGL(k_dist_nib, dim3(ceil_div(ppr, 256), H), dim3(256), 0, st, dist, pitch, packed, ppr, W, H);
   return hipGetLastError();
 }
 

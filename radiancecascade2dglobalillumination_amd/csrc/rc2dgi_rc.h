@@ -150,6 +150,22 @@ __device__ __forceinline__ int cvt_floor(float x) {
 __device__ __forceinline__ unsigned ld_dist(const unsigned short *dist, unsigned off) {
   return *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + off);
 }
+// The 16-bit field read of an escaped packet sample, waited for right after it is issued.  A
+// wave's escape loads are issued under per-ray EXEC masks (the escape branch is divergent); left in
+// flight together and waited for at the branch join, as the compiler schedules them, some of them
+// return wrong data on gfx950 when other workgroups share the CU (reproduced on the
+// rolled and unrolled packed marches; the compiler's waitcnts are correct, a forced-zero waitcnt build
+// and L1-bypassing cache scopes still fail, one workgroup per CU or this immediate wait do not).
+// Escapes are rare at the sizes the packed marches are picked for, so the wait costs nothing there.
+__device__ __forceinline__ unsigned ld_dist_esc(const unsigned short *dist, unsigned off) {
+#ifdef RC2DGI_DIAG_ESC_PLAIN  // diagnostic build reproducing the failure: a plain load, waited at the join
+  return ld_dist(dist, off);
+#endif
+  unsigned v;
+  const unsigned short *p = reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + off);
+  asm volatile("global_load_ushort %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
 
 // Packed distance field (DL = 2, k_dist_pack): one 16-byte packet per 14 texels of a row.  Bytes
 // 0-1 hold the packet's minimum q, byte 2 + t the excess q - min of texel t, or 255 (escape: read
@@ -166,6 +182,45 @@ __device__ __forceinline__ unsigned pack_byte(uint4 v, unsigned b) {  // byte b 
   return (unsigned)(h >> ((b & 7u) * 8u)) & 0xFFu;
 }
 
+// Nibble-predicted distance field (DL = 3, k_dist_nib): one 16-byte packet per 26 texels of a
+// row, q(t) = base + slope * t + (n_t - 7) for texel t of the packet: bits 0-15 base, 16-23 the
+// signed slope, 24 + 4t the nibble n_t (15 = escape: read the 16-bit field).  Along a row the
+// distance field is piecewise close to linear (a wall's distance is linear, a point's bends
+// slowly), so with the best of a few slopes per packet 1.4 % of the texels escape at 4096^2 (demo
+// scene).  0.62 B/texel: the field takes 10 MB at 4096^2 (the 14-texel packets 19 MB, the plain
+// field 32 MB), and one 128-byte line covers 208 texels of a row.
+constexpr int kNibTexels = 26;
+__host__ __device__ __forceinline__ int nib_per_row(int W) { return (W + kNibTexels - 1) / kNibTexels; }
+// ix / 26 for 0 <= ix < 16384 (20165 / 2^19 overestimates 1/26 by 3.8e-6: never crosses an integer)
+__device__ __forceinline__ unsigned pack_div26(unsigned ix) { return __umul24(ix, 20165u) >> 19; }
+// packet index and sub-texel of column ix in layout DL (2: 14-texel byte packets, 3: nibble packets)
+template <int DL>
+__device__ __forceinline__ void packet_of(unsigned ix, unsigned &pk, unsigned &sub) {
+  if constexpr (DL == 3) {
+    pk = pack_div26(ix);
+    sub = ix - pk * (unsigned)kNibTexels;
+  } else {
+    pk = pack_div14(ix);
+    sub = ix - pk * (unsigned)kPackTexels + 2u;  // its byte
+  }
+}
+// q of sub-texel `sub` of packet v; esc: the packet does not hold it (read the 16-bit field)
+template <int DL>
+__device__ __forceinline__ unsigned packet_q(uint4 v, unsigned sub, bool &esc) {
+  if constexpr (DL == 3) {
+    const unsigned b = 24u + 4u * sub;
+    const unsigned long long h = b < 64u ? ((unsigned long long)v.y << 32 | v.x) : ((unsigned long long)v.w << 32 | v.z);
+    const unsigned n = (unsigned)(h >> (b & 63u)) & 15u;
+    esc = n == 15u;
+    const int slope = (int)(v.x << 8) >> 24;
+    return (unsigned)((int)(v.x & 0xFFFFu) + slope * (int)sub + (int)n - 7);
+  } else {
+    const unsigned e = pack_byte(v, sub);
+    esc = e == 255u;
+    return (v.x & 0xFFFFu) + e;
+  }
+}
+
 // one distance sample (q) of texel (ix, iy) = linear index idx, in layout DL
 template <int DL>
 __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const uint4 *dpk, int tpr, int ix, int iy,
@@ -174,11 +229,13 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
     const unsigned t = ((__umul24((unsigned)iy >> 3, (unsigned)tpr) + ((unsigned)ix >> 3)) << 6) |
                        (((unsigned)iy & 7u) << 3) | ((unsigned)ix & 7u);
     return ld_dist(dist, t << 1);
-  } else if constexpr (DL == 2) {
-    const unsigned pk = pack_div14((unsigned)ix);
+  } else if constexpr (DL == 2 || DL == 3) {
+    unsigned pk, sub;
+    packet_of<DL>((unsigned)ix, pk, sub);
     const uint4 v = dpk[__umul24((unsigned)iy, (unsigned)tpr) + pk];
-    const unsigned e = pack_byte(v, (unsigned)ix - pk * (unsigned)kPackTexels + 2u);
-    return e == 255u ? ld_dist(dist, (unsigned)idx << 1) : (v.x & 0xFFFFu) + e;
+    bool esc;
+    const unsigned q = packet_q<DL>(v, sub, esc);
+    return esc ? ld_dist_esc(dist, (unsigned)idx << 1) : q;
   } else {
     return ld_dist(dist, (unsigned)idx << 1);
   }
@@ -196,7 +253,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                      const float4 *__restrict__ sky,
                                                      const uint4 *__restrict__ dpk) {
   constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
-  constexpr bool TILED = DL == 1, PACKED = DL == 2;
+  constexpr bool TILED = DL == 1, PACKED = DL == 2 || DL == 3;
   static_assert(!PACKED || P2S, "packed distance field: power-of-two screens only");
   // staged footprint: taps of c in [c0, c0+T) lie in [c0/2 - 1, c0/2 + T/2]
   constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
@@ -212,6 +269,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr bool STG = !TOP;  // stage and merge the level-(L+1) cascade
 #endif
   __shared__ typename GI::S s_up[STG ? NSTAGE : 1];
+#ifdef RC2DGI_DIAG_LDS_PAD  // diagnostic build: one workgroup per CU (LDS-limited residency)
+  __shared__ unsigned s_pad[RC2DGI_DIAG_LDS_PAD];
+  if (P.level == 99) s_pad[threadIdx.x] = 0u;
+#endif
 
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
   // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
@@ -389,9 +450,9 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         didx[k] = ((__umul24((unsigned)iy >> 3, (unsigned)P.tpr) + ((unsigned)ix >> 3)) << 6) |
                   (((unsigned)iy & 7u) << 3) | ((unsigned)ix & 7u);
       } else if constexpr (PACKED) {
-        const unsigned pk = pack_div14((unsigned)ix);
+        unsigned pk;
+        packet_of<DL>((unsigned)ix, pk, psub[k]);
         didx[k] = __umul24((unsigned)iy, (unsigned)P.tpr) + pk;  // packet
-        psub[k] = (unsigned)ix - pk * (unsigned)kPackTexels + 2u;  // its byte
       } else {
         didx[k] = (unsigned)idx[k];
       }
@@ -409,17 +470,16 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
       for (int k = 0; k < NR; ++k)  // dead rays re-read packet 0
         pv[k] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(dpk) + (didx[k] << 4));
-      bool esc = false;
+      bool esc = false, ek[NR];
 #pragma unroll
       for (int k = 0; k < NR; ++k) {
-        const unsigned e = pack_byte(pv[k], psub[k]);
-        q[k] = (pv[k].x & 0xFFFFu) + e;
-        esc |= e == 255u;
+        q[k] = packet_q<DL>(pv[k], psub[k], ek[k]);
+        esc |= ek[k];
       }
-      if (esc) {  // rare: some texel's excess did not fit a byte
+      if (esc) {  // rare: some texel the packet does not hold
 #pragma unroll
         for (int k = 0; k < NR; ++k)
-          if (pack_byte(pv[k], psub[k]) == 255u) q[k] = ld_dist(dist, (unsigned)idx[k] << 1);
+          if (ek[k]) q[k] = ld_dist_esc(dist, (unsigned)idx[k] << 1);
       }
     } else {
 #pragma unroll
@@ -576,9 +636,9 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 template <int TX, int TY, int PY, int PD = 1, int UNR = 1, int DL = 0, class GI = GiF32>
 static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
   const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
-  if constexpr (DL == 2) {  // packed field: power-of-two screens up to 16384 wide; same bits either way
+  if constexpr (DL == 2 || DL == 3) {  // packed field: power-of-two screens up to 16384 wide; same bits either way
     if (!p2s || P.s.W > 16384) return launch_rc_tiles<TX, TY, PY, PD, UNR, 0, GI>(a, P, st);
-    if (!a.dist_packed) return hipErrorInvalidValue;
+    if (!(DL == 2 ? a.dist_packed : a.dist_nib)) return hipErrorInvalidValue;
   }
   P.tiles_x = ceil_div(P.bdx, TX);
   const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
@@ -589,15 +649,15 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   const int ngrp = P.bsc * P.bsc / PD;
   P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, a.order_code, TX, TY * PY);
   if (!P.wg_map) return hipErrorOutOfMemory;
-  P.tpr = DL == 2 ? pack_per_row(P.s.W) : (P.s.W + 7) / 8;
+  P.tpr = DL == 2 ? pack_per_row(P.s.W) : (DL == 3 ? nib_per_row(P.s.W) : (P.s.W + 7) / 8);
   if (DL == 1 && !a.dist_tiled) return hipErrorInvalidValue;
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
 #define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \
-  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL == 2 ? 0 : DL)), GI, Z0V>), \
+  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL >= 2 ? 0 : DL)), GI, Z0V>), \
                      dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),   \
                      reinterpret_cast<typename GI::T *>(a.out), DL == 1 ? a.dist_tiled : a.dist, a.shade,     \
-                     a.dirs, a.sky, a.dist_packed)
+                     a.dirs, a.sky, DL == 3 ? a.dist_nib : a.dist_packed)
   const bool top = a.level == a.N - 1;
   if (top) {
     if (p2s) RC2DGI_RC(true, true, false); else RC2DGI_RC(true, false, false);

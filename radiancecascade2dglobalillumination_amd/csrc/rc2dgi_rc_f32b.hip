@@ -10,7 +10,9 @@ hipError_t launch_rc_f32_unrolled(const RcLevelArgs &a, RcParams P, hipStream_t 
     case 14: return launch_rc_tiles<16, 16, 1, 1, 32, 1>(a, P, st);
     case 15: return launch_rc_tiles<16, 16, 1, 1, 1, 1>(a, P, st);
     case 16: return launch_rc_tiles<16, 16, 1, 1, 32, 2>(a, P, st);
-    case 17: return launch_rc_tiles<16, 16, 1, 1, 1, 2>(a, P, st);
+    case 17: return launch_rc_tiles<16, 16, 1, 1, 32, 3>(a, P, st);
+    case 18: return launch_rc_tiles<16, 16, 1, 1, 1, 2>(a, P, st);
+    case 19: return launch_rc_tiles<16, 16, 1, 1, 1, 3>(a, P, st);
     default: return launch_rc_tiles<16, 16, 1>(a, P, st);
   }
 }

@@ -368,7 +368,7 @@ def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene, storage):
     ctx.set_keep_levels(True)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
-    variants = range(ctx.get_tuning("rc_variant_count")) if storage == "f32" else (0, 13, 14, 15, 16, 17)
+    variants = range(ctx.get_tuning("rc_variant_count")) if storage == "f32" else (0, 13, 14, 15, 16, 17, 18, 19)
     for v in variants:
         ctx.set_tuning("rc_variant", v)
         for rep in range(2):  # twice: a schedule must also be deterministic run to run
@@ -439,17 +439,19 @@ def test_rc_orders_and_autotune_are_bit_identical(RC2DGI):
 
 
 @pytest.mark.parametrize("storage,W,N", [("f16", 512, 6), ("f32", 512, 6), ("rgba8", 512, 6), ("f16", 1024, 6),
-                                         ("f16", 256, 4)])
-def test_rolled_packed_variant_first_in_fresh_context(RC2DGI, storage, W, N):
-    """The rolled packed-field march (variant 17, "16x16x1p") as the first and only schedule of
-    a fresh context, three frames: it must build the packed field itself (rc_variant_packed) and
-    match the oracle every time (the round-1 failure: DESIGN.md §5.1)."""
+                                         ("f32", 256, 4)])
+@pytest.mark.parametrize("variant", [16, 17, 18, 19])
+def test_packed_fields_first_in_fresh_context(RC2DGI, storage, W, N, variant):
+    """The packed (16 unrolled, 18 rolled) and nibble-predicted (17 unrolled, 19 rolled)
+    distance-field marches as the first and only schedule of a fresh context (the context must
+    build its packed field itself), at sizes where many samples escape to the 16-bit field, three
+    frames: every level bit-exact every time (the round-1 failure of the rolled form)."""
     color, emis = make_scene("demo", W, W)
     fr = oracle.frame(oracle.Params(W=W, H=W, N=N, ray_range=2.0, **mode_params(storage)), color, emis,
                       keep_levels=True)
     ctx = RC2DGI(W, W, cascade_count=N, ray_range=2.0, storage=storage)
     ctx.set_keep_levels(True)
-    ctx.set_tuning("rc_variant", 17)
+    ctx.set_tuning("rc_variant", variant)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
     for rep in range(3):

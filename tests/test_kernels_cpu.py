@@ -161,3 +161,55 @@ def test_banded_order_follows_the_rays():
         assert vs == sorted(vs)
         for a, b, va, vb in zip(us, us[1:], vs, vs[1:]):
             assert va != vb or a <= b
+
+
+def test_packet_index_magic_divisions():
+    """k_rc_level's packet index ix / 14 and ix / 26 as one 24-bit multiply and a shift
+    (pack_div14, pack_div26 in csrc/rc2dgi_rc.h), exact for every column of a screen <= 16384."""
+    ix = np.arange(16384, dtype=np.int64)
+    assert np.array_equal((ix * 37450) >> 19, ix // 14)
+    assert np.array_equal((ix * 20165) >> 19, ix // 26)
+    assert int(ix[-1] * 20165) < 2 ** 32 and int(ix[-1] * 37450) < 2 ** 32
+
+
+def _nib_encode(q, W):
+    """numpy restatement of k_dist_nib for one row (the device decoder is packet_q<3>)."""
+    out = []
+    for x0 in range(0, W, 26):
+        seg = q[x0:x0 + 26].astype(np.int64)
+        cnt = len(seg)
+        s0 = int(np.floor(np.float32(seg[-1] - seg[0]) / np.float32(max(cnt - 1, 1)) + np.float32(0.5))) if cnt > 1 else 0
+        best = None
+        for ds in range(-2, 3):
+            sl = min(127, max(-128, s0 + ds))
+            r = seg - sl * np.arange(cnt)
+            base = min(65535, max(0, (int(r.min()) + int(r.max())) >> 1))
+            esc = int(np.count_nonzero(np.abs(r - base) > 7))
+            if best is None or esc < best[0]:
+                best = (esc, sl, base)
+        _, sl, base = best
+        r = seg - sl * np.arange(cnt) - base
+        nib = np.where(np.abs(r) <= 7, r + 7, 15)
+        out.append((base, sl, np.concatenate([nib, np.full(26 - cnt, 15)])))
+    return out
+
+
+def test_nibble_packets_round_trip():
+    """Every texel decodes to its q exactly or is flagged as an escape (read from the 16-bit
+    field), on a distance-like row (|dq| <= 16 per texel, kinks) and on random rows."""
+    rng = np.random.default_rng(5)
+    rows = [np.clip(np.cumsum(rng.integers(-16, 17, 4096)) + 30000, 0, 65535),
+            np.abs(np.arange(1000) - 377) * 16 + 3,
+            rng.integers(0, 65536, 300)]
+    for q in rows:
+        W = len(q)
+        esc = 0
+        for k, (base, sl, nib) in enumerate(_nib_encode(q, W)):
+            for t in range(min(26, W - 26 * k)):
+                if nib[t] == 15:
+                    esc += 1
+                    continue
+                assert base + sl * t + int(nib[t]) - 7 == q[26 * k + t]
+        assert esc <= W
+    # the smooth row mostly fits
+    assert sum(int(np.count_nonzero(n == 15)) for _, _, n in _nib_encode(rows[1], len(rows[1]))) < 60
