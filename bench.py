@@ -158,11 +158,12 @@ def sweep_rc(ctx, N, steps, rounds=3):
                       "names": [lib_variant_name(v) for v in range(nv)]}), flush=True)
 
 
-def schedule_path(W, H, N, storage="f32"):
+def schedule_path(W, H, N, ray_range=2.0, storage="f32"):
     """The committed RC schedule (per-level rc_order / rc_variant) for a configuration: picked by
     rc2dgi_autotune on an MI355X (bench.py --autotune --save-tuning), loaded by the bench and by
     the parity tests, so the schedule that is timed is the schedule that is tested."""
-    return os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning", f"{W}x{H}_N{N}_{storage}.json")
+    return os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning",
+                        f"{W}x{H}_N{N}_rr{ray_range:g}_{storage}.json")
 
 
 def lib_variant_name(v):
@@ -194,7 +195,7 @@ def bench_batch(a, rank, local, world):
         shared = torch.cuda.Stream(device=local)
         for g in ctxs:
             g.set_stream(shared.cuda_stream)
-    committed = schedule_path(W, H, N)
+    committed = schedule_path(W, H, N, a.ray_range)
     if ctxs and not a.no_autotune and not a.autotune and os.path.exists(committed):
         with open(committed) as f:  # the committed schedule of this size (tested by the parity suite)
             tun = json.load(f)
@@ -337,7 +338,7 @@ def main():
                     help="keep the library's default RC schedule (no committed schedule, no autotune)")
     ap.add_argument("--autotune", action="store_true",
                     help="time the RC schedule candidates in setup instead of loading the committed schedule "
-                         "(radiancecascade2dglobalillumination_amd/tuning/<W>x<H>_N<N>_<storage>.json)")
+                         "(radiancecascade2dglobalillumination_amd/tuning/<W>x<H>_N<N>_rr<rayRange>_<storage>.json)")
     ap.add_argument("--save-tuning", default="", help="write the chosen per-level rc_order / rc_variant (JSON)")
     ap.add_argument("--load-tuning", default="",
                     help="apply per-level rc_order / rc_variant from a --save-tuning file instead of autotuning "
@@ -370,7 +371,7 @@ def main():
     # inputs resident in HBM before the timed region
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
-    committed = schedule_path(W, H, N, a.storage)
+    committed = schedule_path(W, H, N, a.ray_range, a.storage)
     if not a.load_tuning and not a.autotune and not a.no_autotune and os.path.exists(committed):
         a.load_tuning = committed  # the committed schedule: the one the parity tests check at this size
     if a.load_tuning:

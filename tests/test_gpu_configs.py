@@ -1,0 +1,252 @@
+"""GPU: parity of every BASELINE.json configuration, run with the schedule the bench times.
+
+Each configuration of BASELINE.json ``configs`` on the MI355X, checked against
+the CPU oracle (oracle/, pinned to the reference shaders by tests/test_oracle_golden.py):
+
+* H   4096^2, N=6, rayRange 2   -- the metric's configuration, committed bench schedule
+* C1  1200x900, N=6             -- the reference app's own size, f32, every texel of every texture
+* C2  4096^2, N=8, rayRange 64  -- committed bench schedule
+* C3  8192^2, N=8, rayRange 64  -- 8 row-strip shards (rc2dgi_do_group) vs the unsharded frame
+* C4  batch of 4096^2 N=8 scenes on one shared stream (the bench's batch mode)
+
+At the 4096^2 / 8192^2 sizes the oracle checks the JFA state and distRT over the whole frame,
+every cascade level on sampled rows (the oracle level pass fed the HIP pipeline's own G_{L+1}
+and distRT), and blur / copy-back / merge over the whole frame (sampled rows at 8192^2).  The
+bar is bit-exact equality (the written tolerance, max rel err <= 1e-4, is implied).
+Reference: RC2DGI.cs:66-77 (knobs), RC2DGI.cs:267-406 (the pass chain).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import ROOT, rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def R():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from radiancecascade2dglobalillumination_amd import rc2dgi
+
+    return rc2dgi
+
+
+def committed_schedule(W, H, N, rr, storage="f32"):
+    """bench.py's schedule_path: the per-level rc_order / rc_variant the bench loads and times."""
+    p = os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning", f"{W}x{H}_N{N}_rr{rr:g}_{storage}.json")
+    with open(p) as f:
+        return json.load(f)
+
+
+def apply_schedule(ctx, sched, N):
+    for L in range(N):
+        ctx.set_tuning(f"rc_order_L{L}", sched["rc_order"][L])
+        ctx.set_tuning(f"rc_variant_L{L}", sched["rc_variant"][L])
+
+
+def level_offsets(N):
+    offs, off = [], 0
+    for L in range(N):
+        offs.append(off)
+        off += 4 << (2 * L)
+    return offs
+
+
+def oracle_jfa(color, W, H):
+    """ScreenUV + every JumpFlood step (RC2DGI.cs:276-326) + DistanceField on the oracle."""
+    mx = max(W, H)
+    S = int(np.log(mx) / np.log(2))  # RC2DGI.cs:290, double precision
+    j = oracle.screen_uv(color)
+    step = np.float32(1.0)
+    for _ in range(S):
+        step = np.float32(step * np.float32(0.5))
+        j = oracle.jfa_step(j, float(step), float(np.float32(W) / mx), float(np.float32(H) / mx))
+    return j, oracle.distance_field(j)
+
+
+def check_levels_sampled(p, levels, color, emis, dist, rows_per_level, what):
+    """Every cascade level on sampled probe rows of every direction block: the oracle level pass
+    (RadianceCascades.fs) fed the HIP pipeline's own upper level and distRT."""
+    N = p.N
+    dirs = oracle.dir_tables(p)
+    sky = oracle.sky_table(p)
+    offs = level_offsets(N)
+    CH = levels(0).shape[0]
+    rows = np.unique(np.linspace(0, CH - 1, rows_per_level).astype(int))
+    upper = None
+    for L in range(N - 1, -1, -1):
+        got = levels(L)
+        out = np.zeros_like(got)
+        for r in rows:
+            oracle.rc_level(p, L, upper, color, emis, dist, out, np.ascontiguousarray(dirs[offs[L]:]), sky, int(r),
+                            int(r) + 1)
+        a, b = got[rows], out[rows]
+        assert rel_err(a, b).max() <= TOL, f"{what}: level {L} max rel err {rel_err(a, b).max():.3e}"
+        assert np.count_nonzero(a != b) == 0, f"{what}: level {L}: {np.count_nonzero(np.any(a != b, -1))} texels"
+        upper = got
+
+
+def check_frame(ctx, p, color, emis, rows_per_level=32, what=""):
+    """JFA + DF whole frame, levels on sampled rows, blur / copy-back / merge whole frame."""
+    W, H = p.W, p.H
+    jfin, dist = oracle_jfa(color, W, H)
+    final_rt = "jump1" if (ctx.jfa_steps % 2 == 0) else "jump2"
+    assert np.array_equal(ctx.download(final_rt), jfin), f"{what}: final JFA state"
+    got_dist = ctx.download("dist")
+    assert np.array_equal(got_dist, dist), f"{what}: distRT"
+    check_levels_sampled(p, ctx.download_level, color, emis, got_dist, rows_per_level, what)
+    g0 = ctx.download_level(0)
+    if p.blur_radius > 0:
+        bl = oracle.blur(g0, p.blur_radius)
+        assert np.array_equal(ctx.download("blur"), bl), f"{what}: cascadeBlurRT"
+        fin = oracle.blur_copyback(bl, g0)
+    else:
+        fin = g0
+    assert np.array_equal(ctx.download("final_gi"), fin), f"{what}: final GI"
+    temp, col = oracle.merge(color, fin)
+    assert np.array_equal(ctx.download("temp"), temp), f"{what}: tempRT"
+    assert np.array_equal(ctx.download("color"), col), f"{what}: colorRT"
+
+
+def run_config(R, W, H, N, rr, sched, scene):
+    from radiancecascade2dglobalillumination_amd import scenes
+
+    color, emis = scenes.demo(W, H) if scene == "demo" else scenes.random_scene(W, H, int(scene.split(":")[1]))
+    p = oracle.Params(W=W, H=H, N=N, ray_range=rr)
+    ctx = R.RC2DGI(W, H, cascade_count=N, ray_range=rr)
+    if sched is not None:
+        apply_schedule(ctx, sched, N)
+    ctx.set_keep_levels(True)
+    ctx.frame(color, emis)
+    ctx.sync()
+    return ctx, p, color, emis
+
+
+# ---------------------------------------------------------------- H and C2: the schedules the bench times
+@pytest.mark.parametrize("W,N,rr", [(4096, 6, 2.0), (4096, 8, 64.0)])
+def test_committed_bench_schedule_full_size(R, W, N, rr):
+    """The bench's committed schedule (tile variants incl. the packed / nibble marches, banded
+    workgroup orders) at the size it is timed, bit-exact: H (the metric) and C2."""
+    sched = committed_schedule(W, W, N, rr)
+    ctx, p, color, emis = run_config(R, W, W, N, rr, sched, "demo")
+    for L in range(N):
+        assert ctx.get_tuning(f"rc_variant_L{L}") == sched["rc_variant"][L]
+    check_frame(ctx, p, color, emis, rows_per_level=32, what=f"{W}^2 N={N} rr={rr:g} committed schedule")
+    ctx.close()
+
+
+# ---------------------------------------------------------------- C1: the reference app's size, f32
+def test_c1_app_size_f32_every_texel(R):
+    """1200x900, cascadeCount=6 (RC2DGI.cs:7-8, 66-68): cascades 1216x960, non-power-of-two
+    texture coordinates; the committed schedule; every texel of every render texture vs the
+    oracle frame."""
+    W, H, N, rr = 1200, 900, 6, 2.0
+    ctx, p, color, emis = run_config(R, W, H, N, rr, committed_schedule(W, H, N, rr), "demo")
+    assert ctx.cascade_resolution == (1216, 960)
+    fr = oracle.frame(p, color, emis, keep_levels=True)
+    want = dict(color=fr.color_out, jump1=fr.jump1, jump2=fr.jump2, dist=fr.dist, temp=fr.temp, gi1=fr.gi1,
+                gi2=fr.gi2, blur=fr.blur, final_gi=fr.gi_final)
+    for k, w in want.items():
+        g = ctx.download(k)
+        assert rel_err(g, w).max() <= TOL and np.array_equal(g, w), f"C1 {k}: {np.count_nonzero(g != w)}"
+    for L in range(N):
+        assert np.array_equal(ctx.download_level(L), fr.gi_levels[L]), f"C1 level {L}"
+    ctx.close()
+
+
+# ---------------------------------------------------------------- C3: 8192^2 row strips
+def test_c3_8192_eight_row_strips(R):
+    """8192^2, N=8, rayRange 64 split into 8 row strips, run as 8 in-process shard
+    contexts with the distRT exchange (rc2dgi_do_group), intermediates poisoned: every shard's
+    colorRT / tempRT strip equals the unsharded frame bit for bit, and the unsharded frame is
+    checked against the oracle (JFA + DF whole frame, levels on sampled rows, blur / merge on
+    sampled rows)."""
+    from radiancecascade2dglobalillumination_amd import scenes
+
+    W = H = 8192
+    N, rr, P = 8, 64.0, 8
+    color, emis = scenes.demo(W, H)
+    p = oracle.Params(W=W, H=H, N=N, ray_range=rr)
+    whole = R.RC2DGI(W, H, cascade_count=N, ray_range=rr)
+    whole.set_keep_levels(True)
+    whole.frame(color, emis)
+    whole.sync()
+    # the unsharded frame vs the oracle
+    jfin, dist = oracle_jfa(color, W, H)
+    final_rt = "jump1" if (whole.jfa_steps % 2 == 0) else "jump2"
+    assert np.array_equal(whole.download(final_rt), jfin), "C3 final JFA state"
+    del jfin
+    got_dist = whole.download("dist")
+    assert np.array_equal(got_dist, dist), "C3 distRT"
+    del dist
+    check_levels_sampled(p, whole.download_level, color, emis, got_dist, 12, "C3")
+    want_color, want_temp = whole.download("color"), whole.download("temp")
+    g0 = whole.download_level(0)
+    rows = np.unique(np.linspace(0, H - 1, 24).astype(int))
+    bl = oracle.blur(g0, p.blur_radius)
+    fin = oracle.blur_copyback(bl, g0)
+    temp, col = oracle.merge(color, fin)
+    assert np.array_equal(want_color[rows], col[rows]) and np.array_equal(want_temp[rows], temp[rows]), "C3 merge"
+    del bl, fin, temp, col, g0, got_dist
+    whole.close()
+    # 8 shards, two frames (the second reuses the exchange buffers)
+    shards = []
+    for k in range(P):
+        g = R.RC2DGI(W, H, cascade_count=N, ray_range=rr)
+        g.upload("color", color)
+        g.upload("emissive", emis)
+        g.set_tuning("poison", 1)
+        g.set_shard(k, P)
+        shards.append(g)
+    for _ in range(2):
+        R.do_group(shards)
+    for g in shards:
+        g.sync()
+        y0, y1 = g.shard_rows()
+        c, t = g.download("color"), g.download("temp")
+        assert np.array_equal(c[y0:y1], want_color[y0:y1]), f"C3 shard rows {y0}:{y1} colorRT"
+        assert np.array_equal(t[y0:y1], want_temp[y0:y1]), f"C3 shard rows {y0}:{y1} tempRT"
+        g.close()
+
+
+# ---------------------------------------------------------------- C4: batch of independent scenes
+def test_c4_batch_of_4096_scenes_one_stream(R):
+    """BASELINE configs[4] on one GPU: 8 independent 4096^2 N=8 scenes, one context each, all on
+    one shared stream with the frames back to back (bench.py --batch), two frames in flight per
+    context; each context's frame vs the oracle (JFA + DF whole frame, levels on sampled rows,
+    merge whole frame)."""
+    import torch
+
+    from radiancecascade2dglobalillumination_amd import dist as rdist
+    from radiancecascade2dglobalillumination_amd import scenes
+
+    W = H = 4096
+    N, rr, B = 8, 2.0, 8
+    stream = torch.cuda.Stream(device=0)
+    ctxs, inputs = [], []
+    for i in range(B):
+        color, emis = scenes.random_scene(W, H, seed=rdist.scene_seed(i))
+        g = R.RC2DGI(W, H, cascade_count=N, ray_range=rr)
+        g.set_stream(stream.cuda_stream)
+        g.set_keep_levels(True)
+        g.upload("color", color)
+        g.upload("emissive", emis)
+        ctxs.append(g)
+        inputs.append((color, emis))
+    for _ in range(2):
+        for g in ctxs:
+            g.do_rc2dgi()
+    for g in ctxs:
+        g.sync()
+    p = oracle.Params(W=W, H=H, N=N, ray_range=rr)
+    for i, (g, (color, emis)) in enumerate(zip(ctxs, inputs)):
+        check_frame(g, p, color, emis, rows_per_level=8, what=f"C4 scene {i}")
+        g.close()
