@@ -343,6 +343,8 @@ def main():
     ap.add_argument("--load-tuning", default="",
                     help="apply per-level rc_order / rc_variant from a --save-tuning file instead of autotuning "
                          "(profiler runs replay the bench's schedule)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra rc2dgi_set_tuning knob applied after the schedule (e.g. rc_skip=0), repeatable")
     ap.add_argument("--shards", type=int, default=1,
                     help="strips on one process: run this many shards as in-process contexts")
     a = ap.parse_args()
@@ -383,6 +385,9 @@ def main():
         orders = tun["rc_order"]
     else:
         orders = None if a.no_autotune else ctx.autotune(3)  # setup: schedule choice, results identical
+    for kv in a.tune:
+        k, v = kv.split("=")
+        ctx.set_tuning(k, int(v))
     variants = [ctx.get_tuning(f"rc_variant_L{L}") for L in range(N)]
     orders = [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)] if orders else None
     if a.save_tuning and rank == 0:
@@ -444,6 +449,7 @@ def main():
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
                    "parallelism": f"replicas{world}",
                    "rc_order": orders or "default", "rc_variant": variants,
+                   "rc_skip": ctx.get_tuning("rc_skip"),
                    "rc_schedule": (os.path.relpath(a.load_tuning, ROOT) if a.load_tuning else
                                    ("default" if a.no_autotune else "autotune in setup"))},
         "rc_ms_per_frame": round(t_rc / a.steps, 4),

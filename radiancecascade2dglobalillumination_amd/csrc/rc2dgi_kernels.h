@@ -79,7 +79,17 @@ struct RcLevelArgs {
   const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
   const uint4 *dist_nib = nullptr;             // nibble-predicted distance field (variants "n", k_dist_nib)
+  const float *cmin = nullptr;  // coarse lower bound of the field (launch_dist_cmin); nullptr: no exit proofs
+  int cmin_screen = 0;          // the exit proof also tests the screen edge (worth it for long rays)
+  int tail_k = 0;               // tail compaction after this many lockstep march iterations (0: off)
+  int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
 };
+
+// coarse lower bound of the distance field: kCminDim x kCminDim cells of 2^dist_cmin_shift texels,
+// float per cell (row-major, kCminDim per row) = decode_dist(min q) or 0 where a texel is a hit
+constexpr int kCminDim = 32;
+int dist_cmin_shift(int W, int H);
+hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, float *cmin, int W, int H, hipStream_t st);
 
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,
@@ -108,6 +118,11 @@ hipError_t launch_dist_nib(const unsigned short *dist, int pitch, uint4 *packed,
 // every texel whose distance passes the march's hit test; other texels untouched
 hipError_t launch_shade(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
                         ScreenDims s, float reflectivity, hipStream_t st);
+
+// CalculateRayRange's end of level L (RadianceCascades.fs:38-46), as k_rc_level computes it
+inline float rc_ray_end(int level, int N, float ray_range) {
+  return ((float)((1 << (level * 2 + 2)) - 1) / (float)((1 << (N * 2)) - 1)) * ray_range;
+}
 
 // one RadianceCascades.fs level
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);

@@ -358,6 +358,46 @@ __global__ __launch_bounds__(256) void k_shade(const unsigned short *__restrict_
   }
 }
 
+// ---------------------------------------------------------------- coarse lower bound of the field
+// One workgroup per cell of 2^csh x 2^csh texels (a 32 x 32 grid covers the screen): the cell's
+// smallest distance decode_dist(min q), or 0 when some texel of the cell passes the march's hit
+// test.  decode_dist is monotone, so the value bounds every texel of the cell from below: a ray
+// whose sample lies in the cell advances by at least that much and does not stop there
+// (k_rc_level's exit proof, kCminDim).
+__global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restrict__ dist, int pitch,
+                                                   float *__restrict__ cmin, int W, int H, int csh) {
+  const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
+  unsigned m = 0xFFFFu;
+  const bool in = x0 < W && y0 < H;
+  if (in) {
+    const int x1 = min(W, x0 + (1 << csh)), y1 = min(H, y0 + (1 << csh));
+    const int n4 = (x1 - x0 + 3) >> 2;  // 4-texel groups per row of the cell
+    const int tot = n4 * (y1 - y0);
+    for (int e = (int)threadIdx.x; e < tot; e += 256) {
+      const int r = e / n4;
+      const int xx = x0 + 4 * (e - r * n4);
+      const unsigned short *p = dist + (size_t)(y0 + r) * pitch + xx;
+      if (csh >= 2 && xx + 3 < x1) {  // 8-byte aligned: x0 is a multiple of 4, rows of 64-texel pitch
+        const uint2 v = *reinterpret_cast<const uint2 *>(p);
+        m = min(m, min(min(v.x & 0xFFFFu, v.x >> 16), min(v.y & 0xFFFFu, v.y >> 16)));
+      } else {
+        for (int t = 0; t < 4; ++t)
+          if (xx + t < x1) m = min(m, (unsigned)p[t]);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, o, 64));
+  __shared__ unsigned s_m[4];
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
+    const float d = decode_dist(m);
+    cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? d : 0.0f;
+  }
+}
+
 // ---------------------------------------------------------------- tiled distance field
 // dist (pitch-linear) -> 8x8 tiles of 64 texels (one 128-byte line), tiles row-major, tpr tiles per
 // row; a thread moves one 16-byte row segment (8 texels) of one tile
@@ -917,8 +957,21 @@ bool rc_variant_packed(int v) { return v == 16 || v == 18; }
 bool rc_variant_nib(int v) { return v == 17 || v == 19; }
 const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
+#ifdef RC2DGI_DIAG_STATS
+// the diagnostic counters (one device buffer per process, zeroed when made)
+unsigned long long *diag_stats_buffer() {
+  static unsigned long long *d = nullptr;
+  if (!d && hipMalloc(&d, 16 * 3 * sizeof(unsigned long long)) == hipSuccess)
+    (void)hipMemset(d, 0, 16 * 3 * sizeof(unsigned long long));
+  return d;
+}
+#endif
+
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
   RcParams P;
+#ifdef RC2DGI_DIAG_STATS
+  P.stats = diag_stats_buffer();
+#endif
   P.s = s;
   P.c = c;
   P.level = a.level;
@@ -1114,6 +1167,18 @@ hipError_t launch_dist_nib(const unsigned short *dist, int pitch, uint4 *packed,
   return hipGetLastError();
 }
 
+int dist_cmin_shift(int W, int H) {
+  int s = 0;
+  while (((W - 1) >> s) >= kCminDim || ((H - 1) >> s) >= kCminDim) ++s;
+  return s;
+}
+
+hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, float *cmin, int W, int H, hipStream_t st) {
+  hipLaunchKernelGGL(k_dist_cmin, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, pitch, cmin, W, H,
+                     dist_cmin_shift(W, H));
+  return hipGetLastError();
+}
+
 hipError_t launch_shade(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
                         ScreenDims s, float reflectivity, hipStream_t st) {
   hipLaunchKernelGGL(k_shade, dim3(ceil_div(s.W, 256), ceil_div(s.H, 4)), dim3(256), 0, st, dist, color, emis, shade, s,
@@ -1138,11 +1203,9 @@ hipError_t launch_quantize_u8(float4 *buf, int pitch, int W, int H, hipStream_t 
 #ifdef RC2DGI_DIAG_STATS
 extern "C" int rc2dgi_diag_stats(unsigned long long *out, int reset) {
   hipDeviceSynchronize();
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rc2dgi::g_rc_stats), sizeof(rc2dgi::g_rc_stats)) != hipSuccess) return -3;
-  if (reset) {
-    static unsigned long long zero[16][3] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(rc2dgi::g_rc_stats), zero, sizeof(zero)) != hipSuccess) return -3;
-  }
+  unsigned long long *d = rc2dgi::diag_stats_buffer();
+  if (!d || hipMemcpy(out, d, 16 * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -3;
+  if (reset && hipMemset(d, 0, 16 * 3 * sizeof(unsigned long long)) != hipSuccess) return -3;
   return 0;
 }
 #endif

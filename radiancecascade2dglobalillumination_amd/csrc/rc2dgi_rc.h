@@ -25,6 +25,14 @@ struct RcParams {
   float sWf, sHf;  // screen size as floats (power-of-two screen path)
   const uint2 *wg_map;  // workgroup -> (tile x | y << 16, direction group), host-built (XCD remap + order)
   int tpr;              // 8x8 tiles per row of the tiled distance field (TILED)
+  const float4 *cmin;   // coarse lower bound of the field (kCminDim^2 floats as float4), nullptr: off
+  int csh;              // its cells are 2^csh texels square
+  int cscr;             // the exit proof tests the screen edge too
+  int tailk;            // tail compaction after this many lockstep iterations (0: off)
+  int wgp;              // workgroup-wide exit proof of the first samples
+#ifdef RC2DGI_DIAG_STATS
+  unsigned long long *stats;  // diagnostic builds: [16][3] counters (rc2dgi_diag_stats)
+#endif
 };
 
 // q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
@@ -123,11 +131,15 @@ __host__ __device__ __forceinline__ void rc_order_map(int logical, int tiles_x, 
 // The level-(L+1) bilinear footprint of the tile -- block-local by the reference's clamp -- is
 // staged in LDS once per ray direction; its loads are issued before the march and written to
 // LDS after it (their latency hides under the march).
-#ifdef RC2DGI_DIAG_STATS
-// diagnostic builds only (python _build.py stats): per level, [0] lockstep ray slots executed
-// (iterations x rays per lane), [1] samples of live rays, [2] waves
-static __device__ unsigned long long g_rc_stats[16][3];
-#endif
+// diagnostic builds only (python _build.py stats): P.stats holds per level [0] lockstep ray slots
+// executed (iterations x rays per lane), [1] samples of live rays, [2] waves
+
+// x inside [0, 1]^2 as the march tests it (P2S: one unsigned compare per axis, see below)
+template <bool P2S>
+__device__ __forceinline__ bool on_screen(float px, float py) {
+  if constexpr (P2S) return __float_as_uint(px) <= 0x3f800000u && __float_as_uint(py) <= 0x3f800000u;
+  return !(px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+}
 
 // floor(x) as an int in one instruction (x finite, within int range)
 __device__ __forceinline__ int cvt_floor(float x) {
@@ -269,6 +281,36 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr bool STG = !TOP;  // stage and merge the level-(L+1) cascade
 #endif
   __shared__ typename GI::S s_up[STG ? NSTAGE : 1];
+  // Exit proofs.  The march's last sample of a ray that misses only decides that the ray ends: it
+  // is not a hit and t + d leaves the interval or (further along the ray) the screen.  A coarse
+  // lower bound dl <= d of the sample's cell (k_dist_cmin) proves both when dl passes the hit test
+  // and t + dl already leaves: t + d >= t + dl (fp addition is monotone), and the position
+  // o + (t dir) asp moves monotonically along each axis, so once outside [0, 1] it stays outside.
+  // Such a sample is not read: same result, one gather fewer (most of the samples of L0-L2, half
+  // at L3, a quarter at L4/L5 on the demo scene).  Level 0's shared first sample is issued before
+  // the staging loads and hides under them, so Z0 kernels keep the plain march.
+  constexpr bool CMS = !Z0;
+  constexpr int CMN = kCminDim * kCminDim;
+  __shared__ float s_cm[CMS ? CMN : 1];
+  const bool cm = CMS && P.cmin != nullptr;
+  constexpr int CPT = CMS ? (CMN / 4 + NT - 1) / NT : 1;  // float4 of the table per thread
+  float4 cmv[CPT];
+  if (cm) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+      if (CMN / 4 % NT == 0 || (int)threadIdx.x + j * NT < CMN / 4) cmv[j] = P.cmin[threadIdx.x + j * NT];
+  }
+  // Tail compaction.  A lane marches its NR rays in lockstep and a wave runs until its longest ray
+  // ends, so the few rays that pass close to a surface (steps shrink, then grow geometrically) set
+  // the loop count of the whole wave: at L4 the waves run ~1.8x the iterations of their average
+  // lane.  After P.tailk lockstep iterations the rays still marching are queued in LDS (t and the
+  // owner's lane / ray slot) and the workgroup finishes them one ray per lane, packed densely into
+  // as few waves as they fill; the owners read the hit texels back.  Each ray's march is unchanged
+  // (same samples, same iteration cap), so the results are too.
+  constexpr bool TLC = !Z0 && NR == 4;  // one probe and one direction block per lane (the high-level tiles)
+  __shared__ uint2 s_q[TLC ? NT * NR : 1];
+  __shared__ unsigned s_qn;
+  const bool tl = TLC && P.tailk > 0;
 #ifdef RC2DGI_DIAG_LDS_PAD  // diagnostic build: one workgroup per CU (LDS-limited residency)
   __shared__ unsigned s_pad[RC2DGI_DIAG_LDS_PAD];
   if (P.level == 99) s_pad[threadIdx.x] = 0u;
@@ -345,6 +387,19 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
   };
   if constexpr (!Z0) stage_loads();
+  if (cm || tl) {  // the bound table to LDS; its loads were issued first (vmcnt retires in order, so
+                   // this waits for them only, not for the staging loads in flight over the march)
+    if (cm) {
+#pragma unroll
+      for (int j = 0; j < CPT; ++j)
+        if (CMN / 4 % NT == 0 || (int)threadIdx.x + j * NT < CMN / 4)
+          reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
+    }
+    if (tl && threadIdx.x == 0) s_qn = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  }
 
   const float cxf = (float)cx;
   const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);  // rayOrigin / _CascadeResolution
@@ -374,6 +429,36 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     t[k] = P.t0;
     hit_idx[k] = -1;
     act[k] = pok[k / ND] && !(P.t0 > P.t1);  // act: the ray takes another sample (t <= t1 folded in)
+  }
+  // Workgroup-wide exit proof: a ray's first sample o + (t0 dir) asp lies within t0 (uv) of its
+  // probe on each axis, so inside the tile's probe box grown by t0.  When every bound-table cell
+  // under that box proves exit for a first sample (dl > 0 and t0 + dl > t1: every sample there
+  // misses and ends its ray), no ray of the workgroup samples at all: the march is skipped.  The
+  // box carries two texels of slack for its approximate float arithmetic; a box touching the far
+  // screen edge (where p = 1 wraps to texel 0) is not tried.  Compiled into the kernels without
+  // tail compaction (the several-probes-per-lane tiles that serve the short-ray levels): at the
+  // long-ray levels the box spans many cells and the unused test alone cost 3 % (measured).
+  constexpr bool WGC = !Z0 && !TLC;
+  if (WGC && cm && P.wgp && !(P.t0 > P.t1)) {
+    const float bx0 = ((((float)cx0 + 0.5f) * (float)P.bsc) / P.CRx - P.t0) * P.sWf - 2.0f;
+    const float bx1 = ((((float)(cx0 + TX) - 0.5f) * (float)P.bsc) / P.CRx + P.t0) * P.sWf + 2.0f;
+    const float by0 = ((((float)cy0 + 0.5f) * (float)P.bsc) / P.CRy - P.t0) * P.sHf - 2.0f;
+    const float by1 = ((((float)(cy0 + THY) - 0.5f) * (float)P.bsc) / P.CRy + P.t0) * P.sHf + 2.0f;
+    if (bx1 < P.sWf - 1.0f && by1 < P.sHf - 1.0f) {
+      const int c0 = __builtin_amdgcn_readfirstlane(max(0, (int)bx0) >> P.csh);
+      const int c1 = __builtin_amdgcn_readfirstlane((int)bx1 >> P.csh);
+      const int r0 = __builtin_amdgcn_readfirstlane(max(0, (int)by0) >> P.csh);
+      const int r1 = __builtin_amdgcn_readfirstlane((int)by1 >> P.csh);
+      if ((c1 - c0 + 1) * (r1 - r0 + 1) <= 16) {
+        float m = 3.0e38f;
+        for (int rr = r0; rr <= r1; ++rr)
+          for (int cc = c0; cc <= c1; ++cc) m = fminf(m, s_cm[rr * kCminDim + cc]);
+        if (m > 0.0f && P.t0 + m > P.t1) {
+#pragma unroll
+          for (int k = 0; k < NR; ++k) act[k] = false;
+        }
+      }
+    }
   }
 #ifndef RC2DGI_DIAG_MAX_ITERS
 #define RC2DGI_DIAG_MAX_ITERS 32  // RadianceCascades.fs:64 (diagnostic builds may cap it; never shipped)
@@ -422,8 +507,9 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   bool more = false;  // a ray of this lane still marches
 #pragma unroll
   for (int k = 0; k < NR; ++k) more |= act[k];
+  const int itend = tl ? min(P.tailk, RC2DGI_DIAG_MAX_ITERS) : RC2DGI_DIAG_MAX_ITERS;
 #pragma unroll UNR
-  for (int it = it0; more && it < RC2DGI_DIAG_MAX_ITERS; ++it) {
+  for (int it = it0; more && it < itend; ++it) {
     int idx[NR];
     unsigned didx[NR];  // distance-field index (tiled or linear) or packet (packed)
     unsigned psub[PACKED ? NR : 1];  // packed: byte of the texel in its packet
@@ -443,6 +529,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         live[k] = act[k] && !(px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
         ix = wrap_nearest(px, sax);
         iy = wrap_nearest(py, say);
+      }
+      if (cm) {  // exit proof (see s_cm); ix, iy are in range for every lane
+        const float dl = s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)];
+        const float tl = t[k] + dl;
+        bool ex = tl > P.t1;
+        if (P.cscr) ex = ex || !on_screen<P2S>(ox + (tl * rdx[r]) * P.aspy, oy[p] + (tl * rdy[r]) * P.aspx);
+        live[k] = live[k] && !(dl > 0.0f && ex);
       }
       if (!live[k]) ix = iy = 0;
       idx[k] = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;  // < 2^24 operands
@@ -500,11 +593,90 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
 #ifdef RC2DGI_DIAG_STATS
   if (pok[0] || true) {
-    atomicAdd(&g_rc_stats[P.level][0], (unsigned long long)diag_slots);
-    atomicAdd(&g_rc_stats[P.level][1], (unsigned long long)diag_samples);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_rc_stats[P.level][2], 1ull);
+    atomicAdd(&P.stats[P.level * 3 + 0], (unsigned long long)diag_slots);
+    atomicAdd(&P.stats[P.level * 3 + 1], (unsigned long long)diag_samples);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&P.stats[P.level * 3 + 2], 1ull);
   }
 #endif
+
+  int qpos[TLC ? NR : 1];  // queue entry of each pending ray of this lane
+  if (tl) {
+    // pending rays (still marching after itend iterations) -> LDS queue, wave-contiguous ranges
+    unsigned n = 0;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) n += act[k] ? 1u : 0u;
+    unsigned excl = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {  // n <= NR <= 8: exclusive prefix over the wave, bit by bit
+      const unsigned long long m = __ballot((n >> b) & 1u);
+      excl += __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
+      tot += (unsigned)__popcll(m) << b;
+    }
+    unsigned base = 0;
+    if (tot) {
+      if (lane == 0) base = atomicAdd(&s_qn, tot);
+      base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
+    }
+    unsigned pos = base + excl;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      qpos[k] = (int)pos;
+      if (act[k]) s_q[pos++] = make_uint2(__float_as_uint(t[k]), (threadIdx.x << 3) | (unsigned)k);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    const unsigned nq = s_qn;
+    for (unsigned j = (unsigned)wv * 64u + (unsigned)lane; j < nq; j += NT) {
+      const uint2 e = s_q[j];
+      const unsigned otid = e.y >> 3, k = e.y & 7u;
+      const int r = (int)(k % ND), p = (int)(k / ND);
+      // the owner's origin and direction, by the owner's own expressions
+      const int ocx = cx0 + (int)(otid % TX), ocy = cy0 + (int)(otid / TX) + p * TY;
+      const float qox = div_res(((float)ocx + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);
+      const float qoy = div_res(((float)ocy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P2S || P.c.powH);
+      float qdx = rdx[0], qdy = rdy[0];
+#pragma unroll
+      for (int q2 = 1; q2 < ND; ++q2) {
+        qdx = r == q2 ? rdx[q2] : qdx;
+        qdy = r == q2 ? rdy[q2] : qdy;
+      }
+      float tt = __uint_as_float(e.x);
+      int hit = -1;
+      for (int it = itend; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
+        const float px = qox + (tt * qdx) * P.aspy;
+        const float py = qoy + (tt * qdy) * P.aspx;
+        bool live;
+        int ix, iy;
+        if constexpr (P2S) {
+          live = on_screen<true>(px, py);
+          ix = cvt_floor(px * P.sWf) & (P.s.W - 1);
+          iy = cvt_floor(py * P.sHf) & (P.s.H - 1);
+        } else {
+          live = on_screen<false>(px, py);
+          ix = wrap_nearest(px, sax);
+          iy = wrap_nearest(py, say);
+        }
+        if (cm) {
+          const float dl = s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)];
+          const float tq = tt + dl;
+          bool ex = tq > P.t1;
+          if (P.cscr) ex = ex || !on_screen<P2S>(qox + (tq * qdx) * P.aspy, qoy + (tq * qdy) * P.aspx);
+          live = live && !(dl > 0.0f && ex);
+        }
+        if (!live) break;
+        const int idx = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
+        const float d = decode_dist(fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx));
+        if (d < 0.001f) {
+          hit = idx;
+          break;
+        }
+        tt = tt + d;
+        if (tt > P.t1) break;
+      }
+      s_q[j].x = (unsigned)hit;
+    }
+  }
 
   if (STG) {
 #pragma unroll
@@ -523,7 +695,12 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         }
       }
     }
-    __syncthreads();
+  }
+  if (STG || tl) __syncthreads();
+  if (tl) {  // hit texels of this lane's rays that finished in the tail
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      if (act[k]) hit_idx[k] = (int)s_q[qpos[k]].x;
   }
 
   // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
@@ -653,6 +830,11 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   if (DL == 1 && !a.dist_tiled) return hipErrorInvalidValue;
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
+  P.cmin = reinterpret_cast<const float4 *>(a.cmin);
+  P.csh = dist_cmin_shift(P.s.W, P.s.H);
+  P.cscr = a.cmin_screen;
+  P.tailk = a.tail_k;
+  P.wgp = a.wg_proof;
 #define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \
   hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL >= 2 ? 0 : DL)), GI, Z0V>), \
                      dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),   \

@@ -20,9 +20,11 @@ def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     rr = float(sys.argv[3]) if len(sys.argv) > 3 else 2.0
+    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # tuning rc_skip (exit proofs)
     L = load_library()
     L.rc2dgi_diag_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
     ctx = RC2DGI(W, W, cascade_count=N, ray_range=rr)
+    ctx.set_tuning("rc_skip", skip)
     c, e = scenes.demo(W, W)
     ctx.upload("color", c)
     ctx.upload("emissive", e)
@@ -40,7 +42,7 @@ def main():
         out[f"L{lv}"] = {"samples_per_ray": round(samples / rays, 3), "slot_iters_per_ray": round(slots / rays, 3),
                          "lockstep_efficiency": round(samples / max(slots, 1), 3),
                          "wave_iterations": round(slots / max(waves * 64 * 4, 1), 2)}
-    print(json.dumps({"size": W, "N": N, "ray_range": rr, "levels": out}))
+    print(json.dumps({"size": W, "N": N, "ray_range": rr, "rc_skip": skip, "levels": out}))
 
 
 if __name__ == "__main__":

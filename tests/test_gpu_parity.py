@@ -462,3 +462,33 @@ def test_packed_fields_first_in_fresh_context(RC2DGI, storage, W, N, variant):
             assert np.array_equal(g, fr.gi_levels[L]), \
                 f"run {rep} level {L}: {np.count_nonzero(np.any(g != fr.gi_levels[L], axis=-1))} texels differ"
     ctx.close()
+
+
+@pytest.mark.parametrize("W,H,N,rr,rs,scene", [(333, 200, 4, 8.0, 1.0, "demo"), (512, 512, 6, 2.0, 1.0, "demo"),
+                                               (256, 128, 5, 64.0, 1.0, "rand:12"), (256, 256, 4, 2.0, 0.5, "rand:3"),
+                                               (17, 5, 2, 8.0, 1.0, "rand:9"), (1024, 1024, 6, 2.0, 1.0, "rand:5")])
+def test_exit_proofs_and_tail_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene):
+    """The march's exit proofs (tuning rc_skip: 0 off, 1 auto, 2 interval only, 3 interval and
+    screen edge; k_dist_cmin's coarse lower bound) skip only samples whose outcome is already
+    decided, and tail compaction (rc_tail: rays still marching after that many lockstep iterations
+    finish one per lane) only moves rays between lanes: every level is bit-exact with each
+    setting, in every tile variant family."""
+    color, emis = make_scene(scene, W, H)
+    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr, render_scale=rs), color, emis, keep_levels=True)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr, render_scale=rs)
+    ctx.set_keep_levels(True)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    for v in (0, 3, 6, 9, 13, 18, 19):
+        ctx.set_tuning("rc_variant", v)
+        for skip, tail in ((0, 0), (1, 0), (2, 1), (3, 3), (1, 2), (0, 5), (1, 31)):
+            ctx.set_tuning("rc_skip", skip)
+            ctx.set_tuning("rc_tail", tail)
+            assert ctx.get_tuning("rc_skip") == skip and ctx.get_tuning(f"rc_tail_L{N - 1}") == tail
+            ctx.do_rc2dgi()
+            ctx.sync()
+            for L in range(N):
+                g = ctx.download_level(L)
+                assert np.array_equal(g, fr.gi_levels[L]), \
+                    f"variant {v} rc_skip {skip} rc_tail {tail} level {L}: {np.count_nonzero(g != fr.gi_levels[L])}"
+    ctx.close()
