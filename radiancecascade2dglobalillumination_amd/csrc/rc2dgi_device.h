@@ -48,8 +48,18 @@ __device__ __forceinline__ void wrap_linear(float u, Axis a, int &i0, int &i1, f
 
 __device__ __forceinline__ float lerp_gl(float a, float b, float w) { return __builtin_fmaf(w, b - a, a); }
 
+// the same per channel, as two packed-FP32 pairs (v_pk_add_f32 / v_pk_fma_f32: identical IEEE
+// roundings, half the VALU issues; written out because the vectorizer pairs channels of different
+// texels and adds moves)
+typedef float f2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v_t lerp_gl2(f2v_t a, f2v_t b, float w) {
+  const f2v_t ww = {w, w};
+  return __builtin_elementwise_fma(ww, b - a, a);
+}
 __device__ __forceinline__ float4 lerp_gl(float4 a, float4 b, float w) {
-  return make_float4(lerp_gl(a.x, b.x, w), lerp_gl(a.y, b.y, w), lerp_gl(a.z, b.z, w), lerp_gl(a.w, b.w, w));
+  const f2v_t lo = lerp_gl2(f2v_t{a.x, a.y}, f2v_t{b.x, b.y}, w);
+  const f2v_t hi = lerp_gl2(f2v_t{a.z, a.w}, f2v_t{b.z, b.w}, w);
+  return make_float4(lo.x, lo.y, hi.x, hi.y);
 }
 
 // texture(T, (u, v)) with LINEAR filtering on a pitch-linear float4 image

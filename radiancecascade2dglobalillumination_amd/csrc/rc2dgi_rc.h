@@ -728,7 +728,9 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
     // hit shading of the probe's rays (RadianceCascades.fs:79-86): one load of the texel's
     // surface record (k_shade: the emissive or the albedo + reflectivity branch, resolved once
-    // per frame for every hittable texel)
+    // per frame for every hittable texel).  Loaded under the hit mask: a wave whose rays all miss
+    // skips the load (and its round trip) entirely; an unconditional load of a "miss" record was
+    // measured 5 % slower at L0-L2.
     float4 hr[ND];
 #pragma unroll
     for (int r = 0; r < ND; ++r) {
@@ -787,8 +789,9 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
               }
             }
             const float4 up = GI::bilerp(t00, t10, t01, t11, ux, uy);
-            rad.x = rad.x + up.x * rad.w;
-            rad.y = rad.y + up.y * rad.w;
+            const f2v_t rxy = f2v_t{rad.x, rad.y} + f2v_t{up.x, up.y} * f2v_t{rad.w, rad.w};  // packed pair
+            rad.x = rxy.x;
+            rad.y = rxy.y;
             rad.z = rad.z + up.z * rad.w;
             rad.w = rad.w * up.w;
           } else {
@@ -798,10 +801,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
             rad.z = rad.z + sk.z;
           }
         }
-        acc.x = acc.x + rad.x * 0.25f;
-        acc.y = acc.y + rad.y * 0.25f;
-        acc.z = acc.z + rad.z * 0.25f;
-        acc.w = acc.w + rad.w * 0.25f;
+        const f2v_t q = {0.25f, 0.25f};  // acc += rad * 0.25, unfused, as packed pairs
+        const f2v_t axy = f2v_t{acc.x, acc.y} + f2v_t{rad.x, rad.y} * q;
+        const f2v_t azw = f2v_t{acc.z, acc.w} + f2v_t{rad.z, rad.w} * q;
+        acc = make_float4(axy.x, axy.y, azw.x, azw.y);
       }
       const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
       const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex

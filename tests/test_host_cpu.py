@@ -1,0 +1,85 @@
+"""The host side of the drop-in boundary without a GPU.
+
+* The C# P/Invoke structs of host/csharp/RC2DGINative.cs (StructLayout Sequential) have the
+  byte layout of include/rc2dgi.h's rc2dgi_config / rc2dgi_prim as gcc lays them out, field by
+  field (RC2DGI.cs:65-98 knobs; rc2dgi_paint's primitives, RC2DGI.cs:224-264).
+* host/c/rc2dgi_replay (the C replay of the reference's call sequence, tests/test_gpu_replay.py)
+  builds with gcc against the header and the in-tree library and rejects bad usage.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST_C = os.path.join(ROOT, "host", "c")
+CS = os.path.join(ROOT, "host", "csharp", "RC2DGINative.cs")
+
+# C# blittable field sizes (System.Int32 / Single / Byte) -- Sequential layout aligns each field
+# to its own size, the struct to its largest field
+CS_SIZES = {"int": 4, "float": 4, "byte": 1}
+C_NAMES = {"Config": ("rc2dgi_config", ["screen_width", "screen_height", "cascade_count", "render_scale",
+                                        "ray_range", "storage", "device", "reserved"]),
+           "Prim": ("rc2dgi_prim", ["kind", "x", "y", "w", "h", "r", "g", "b", "a"])}
+
+
+def cs_layout(struct):
+    """[(field, offset, size)] and total size of a StructLayout(Sequential) struct of the C# file."""
+    src = open(CS).read()
+    body = re.search(r"public struct " + struct + r"\s*\{(.*?)\}", src, re.S).group(1)
+    fields = []
+    for line in body.splitlines():
+        line = line.split("//")[0].strip()
+        m = re.match(r"public (int|float|byte) (.+);", line)
+        if m:
+            fields += [(n.strip(), CS_SIZES[m.group(1)]) for n in m.group(2).split(",")]
+    out, off, align = [], 0, 1
+    for name, size in fields:
+        off = (off + size - 1) // size * size
+        out.append((name, off, size))
+        off += size
+        align = max(align, size)
+    return out, (off + align - 1) // align * align
+
+
+def c_layout():
+    subprocess.run(["make", "-s", "-C", HOST_C, "layout"], check=True)
+    out = subprocess.run([os.path.join(HOST_C, "layout")], capture_output=True, text=True, check=True).stdout
+    sizes, fields = {}, {}
+    for line in out.splitlines():
+        parts = line.split()
+        if len(parts) == 2:
+            sizes[parts[0]] = int(parts[1])
+        else:
+            s, f = parts[0].split(".")
+            fields[(s, f)] = (int(parts[1]), int(parts[2]))
+    return sizes, fields
+
+
+@pytest.mark.parametrize("struct", ["Config", "Prim"])
+def test_csharp_structs_match_the_c_abi(struct):
+    cname, cfields = C_NAMES[struct]
+    sizes, fields = c_layout()
+    cs, cs_size = cs_layout(struct)
+    assert cs_size == sizes[cname], f"{struct}: C# {cs_size} bytes, C {sizes[cname]}"
+    # the C# mirror spells the reserved array as R0..R4: fold trailing fields onto the array
+    i = 0
+    for cf in cfields:
+        off, size = fields[(cname, cf)]
+        got_off = cs[i][1]
+        span = 0
+        while i < len(cs) and cs[i][1] < off + size:
+            span += cs[i][2]
+            i += 1
+        assert got_off == off and span == size, f"{struct}.{cf}: C# at {got_off} ({span} B), C at {off} ({size} B)"
+    assert i == len(cs)
+
+
+def test_replay_driver_builds_and_checks_usage():
+    lib = os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "librc2dgi.so")
+    if not os.path.exists(lib):
+        pytest.skip("librc2dgi.so not built")
+    subprocess.run(["make", "-s", "-C", HOST_C, "rc2dgi_replay"], check=True)
+    r = subprocess.run([os.path.join(HOST_C, "rc2dgi_replay")], capture_output=True, text=True)
+    assert r.returncode == 2 and "usage" in r.stderr
