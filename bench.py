@@ -259,11 +259,21 @@ def bench_strips(a, rank, local, world):
     virtual = world == 1 and a.shards > 1
     nsh = a.shards if virtual else world
 
+    committed = schedule_path(W, H, N, a.ray_range, a.storage)
+    tun = None
+    if not a.autotune and not a.no_autotune and os.path.exists(committed):
+        with open(committed) as f:
+            tun = json.load(f)  # the whole frame's committed schedule carries over to the shards
+
     def make(k):
         g = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local)
         g.upload("color", color)
         g.upload("emissive", emis)
-        if not a.no_autotune:
+        if tun:
+            for L in range(N):
+                g.set_tuning(f"rc_order_L{L}", tun["rc_order"][L])
+                g.set_tuning(f"rc_variant_L{L}", tun["rc_variant"][L])
+        elif not a.no_autotune:
             g.autotune(1)  # on the whole frame; the orders carry over to the shard
         g.set_shard(k, nsh)
         return g

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RC2DGI_ABI_VERSION 2  /* 2: row-strip sharding entry points */
+#define RC2DGI_ABI_VERSION 3  /* 2: row-strip sharding entry points; 3: JumpFlood exchange planner */
 
 typedef struct rc2dgi_ctx rc2dgi_ctx;
 
@@ -190,15 +190,17 @@ int rc2dgi_paint(rc2dgi_ctx *ctx, int which, const unsigned char *clear_rgba, co
  * Other rows of its render textures are not meaningful.  Color / emissive inputs are uploaded
  * whole to every rank.  The one exchange is distRT: after phase 1 (ScreenUV, JumpFlood,
  * DistanceField) every rank's distRT strip goes to every other rank, then phase 2 (cascades,
- * blur, merge) runs.  Three ways to run a sharded frame:
+ * blur, merge) runs.  Inside phase 1 the JumpFlood steps compute the own strip only and exchange
+ * the rows their taps reach (ring halos for short steps, strip-sized blocks at +-offset for long
+ * ones; rc2dgi_plan_jfa_exchange), into strip-sized jumpRT windows.  Ways to run a sharded frame:
  *   - rc2dgi_shard_connect: an RCCL communicator owned by the context (one process per GPU,
  *     ranks = shards); rc2dgi_do then runs the frame with the exchange (ncclBroadcast of each
  *     strip, grouped) on the context stream.  rc2dgi_shard_unique_id makes the id on rank 0;
  *     the host passes it to the other ranks.
  *   - rc2dgi_do_group: n contexts of one process, context k = shard k of n (any devices):
  *     phase 1 on each, strips exchanged by device copies, phase 2 on each.
- *   - rc2dgi_do_phase(ctx, 1); the host's own exchange (rc2dgi_device_buffer gives the
- *     device pointer and pitch of distRT); rc2dgi_do_phase(ctx, 2).
+ *   - rc2dgi_do_phase(ctx, 1 | 2) on an unsharded context (world 1) runs the two halves of a
+ *     frame; phase 1 of a shard returns RC2DGI_E_STATE (its JumpFlood exchanges between steps).
  * rc2dgi_do on a sharded context without a communicator returns RC2DGI_E_STATE. */
 #define RC2DGI_UNIQUE_ID_BYTES 128
 int rc2dgi_set_shard(rc2dgi_ctx *ctx, int rank, int world);
@@ -208,7 +210,8 @@ int rc2dgi_shard_connect(rc2dgi_ctx *ctx, const void *id, int nbytes);
 int rc2dgi_do_phase(rc2dgi_ctx *ctx, int phase);
 int rc2dgi_do_group(rc2dgi_ctx **ctxs, int n);
 /* raw device storage of a render texture: float4 texels (COLOR = merged output after a frame,
- * else the input; GI1/GI2/BLUR/TEMP/EMISSIVE), uint16 q (DIST), uint32 packed seeds (JUMP1/2) */
+ * else the input; GI1/GI2/BLUR/TEMP/EMISSIVE), uint16 q (DIST), uint32 packed seeds (JUMP1/2; on
+ * a row-strip shard its window: row 0 = global row y0 - m, see rc2dgi_plan_jfa_exchange) */
 int rc2dgi_device_buffer(rc2dgi_ctx *ctx, int which, void **dev, int *pitch_bytes);
 
 /* host-only planner (no device needed): the rows a shard computes for one pass.
@@ -219,6 +222,17 @@ int rc2dgi_device_buffer(rc2dgi_ctx *ctx, int which, void **dev, int *pitch_byte
 enum { RC2DGI_PLAN_JFA = 0, RC2DGI_PLAN_LEVEL = 1000, RC2DGI_PLAN_BLUR = 2000, RC2DGI_PLAN_MERGE = 2001 };
 int rc2dgi_plan_rows(const rc2dgi_config *cfg, float blur_radius, int rank, int world, int pass, int *intervals,
                      int max_intervals);
+
+/* host-only JumpFlood exchange plan of row-strip shards (world >= 2): for JFA step
+ * `step` (1 .. S-1, the step that reads J_{step-1}) writes info[9] = {m (halo rows of a window),
+ * hmax (tallest strip), mg_max, halo (1 halo step, 0 block step), sh[3] (tap row shifts), mg
+ * (rounding margin), same_block} and up to max_xfers transfers of 6 ints {src shard, src window
+ * row, rows, dst shard, dst buffer (0 window, 1 block A, 2 block B), dst row}; returns the
+ * number of transfers.  A shard's window holds global rows [y0 - m, y1 + m) modulo H. */
+int rc2dgi_plan_jfa_exchange(const rc2dgi_config *cfg, int world, int step, int *info, int *xfers, int max_xfers);
+/* where shard `rank` reads tap y (dy = -1, 0, +1) of step `step`: buffer buf[y] (0 window, 1 A,
+ * 2 B) whose local row 0 is global row row0[y] (modulo H) */
+int rc2dgi_plan_jfa_window(const rc2dgi_config *cfg, int rank, int world, int step, int *buf, int *row0);
 
 /* Schedule introspection (no GPU): the RC workgroup order `code` (tuning key rc_order_L<n>:
  * px | py << 8 | dg << 16 | mode << 24, mode 0 patches, 1 oriented patches, 2 bands along the

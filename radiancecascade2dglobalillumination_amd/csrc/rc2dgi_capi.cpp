@@ -42,6 +42,8 @@ struct Rccl {
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclBroadcast) broadcast = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   bool ok = false;
 };
@@ -58,9 +60,11 @@ const Rccl &rccl() {
     x.group_start = reinterpret_cast<decltype(x.group_start)>(dlsym(h, "ncclGroupStart"));
     x.group_end = reinterpret_cast<decltype(x.group_end)>(dlsym(h, "ncclGroupEnd"));
     x.broadcast = reinterpret_cast<decltype(x.broadcast)>(dlsym(h, "ncclBroadcast"));
+    x.send = reinterpret_cast<decltype(x.send)>(dlsym(h, "ncclSend"));
+    x.recv = reinterpret_cast<decltype(x.recv)>(dlsym(h, "ncclRecv"));
     x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
     x.ok = x.get_unique_id && x.comm_init_rank && x.comm_destroy && x.group_start && x.group_end && x.broadcast &&
-           x.error_string;
+           x.send && x.recv && x.error_string;
     return x;
   }();
   return r;
@@ -85,7 +89,12 @@ struct rc2dgi_ctx {
   CascadeDims cd{};
   // device buffers (the reference's render textures)
   float4 *color_in = nullptr, *emissive = nullptr, *temp = nullptr, *color_out = nullptr;
-  unsigned *jump1 = nullptr, *jump2 = nullptr;  // packed seeds
+  unsigned *jump1 = nullptr, *jump2 = nullptr;  // packed seeds (row-strip shards: their windows, see jx)
+  // row-strip shards: the JumpFlood exchange plan, and the two block buffers of its long steps
+  JfaExchange jx;
+  bool strip = false;   // world > 1 and S >= 2: JumpFlood on strip windows with the exchange
+  unsigned *jblk[2] = {nullptr, nullptr};
+  size_t jwin_rows = 0;  // rows of a window (jump1 / jump2)
   unsigned *occ = nullptr;                      // ScreenUV occupancy mask
   int mpitch = 0;                               // mask row pitch (words)
   unsigned short *dist = nullptr;  // packUNorm16 q
@@ -125,6 +134,7 @@ struct rc2dgi_ctx {
   ncclComm_t comm = nullptr;
   hipEvent_t ev_phase1 = nullptr;   // end of phase 1 (group exchange)
   hipEvent_t ev_frame = nullptr;    // end of the last group frame (peers copy from our distRT)
+  hipEvent_t ev_jfa[2] = {nullptr, nullptr};  // end of the last even / odd JFA step (group exchange)
   bool gi1final = false;            // phase 1 -> phase 2 state
   std::string err;
 };
@@ -193,6 +203,10 @@ void free_buffers(rc2dgi_ctx *c) {
                   c->cmin};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
+  for (unsigned *&b : c->jblk) {
+    if (b) (void)hipFree(b);
+    b = nullptr;
+  }
   c->color_in = c->emissive = c->temp = c->color_out = nullptr;
   c->jump1 = c->jump2 = nullptr;
   c->occ = nullptr;
@@ -238,6 +252,37 @@ const int kOrderCandidates[][4] = {{0, 0, 0, 0},  {2, 2, 8, 0},  {4, 4, 4, 0},  
                                    {1, 3, 8, 2},   {1, 6, 8, 2},   {1, 3, 16, 2},  {1, 6, 4, 2},   {1, 12, 4, 2},
                                    {1, 16, 2, 2},  {1, 3, 32, 2},  {1, 6, 16, 2}};
 
+// jumpRT1 / jumpRT2 for the sharding: full-size textures, or (world > 1, >= 2 JFA steps) the
+// strip windows of the JumpFlood exchange (rows [y0 - m, y1 + m) of the strip) and its two
+// block buffers (plan_jfa_exchange)
+int jfa_buffers(rc2dgi_ctx *c) {
+  const bool strip = c->world > 1 && c->S >= 2;
+  for (unsigned **b : {&c->jump1, &c->jump2, &c->jblk[0], &c->jblk[1]}) {
+    if (*b) (void)hipFree(*b);
+    *b = nullptr;
+  }
+  c->strip = strip;
+  const size_t sp = (size_t)c->sd.pitch;
+  if (!strip) {
+    c->jwin_rows = (size_t)c->H;
+    HIPCHK(c, alloc(&c->jump1, sp * c->H * sizeof(unsigned)));
+    HIPCHK(c, alloc(&c->jump2, sp * c->H * sizeof(unsigned)));
+    return RC2DGI_OK;
+  }
+  c->jx = plan_jfa_exchange(c->W, c->H, c->S, c->world);
+  c->jwin_rows = (size_t)c->jx.hmax + 2 * (size_t)c->jx.m;
+  HIPCHK(c, alloc(&c->jump1, sp * c->jwin_rows * sizeof(unsigned)));
+  HIPCHK(c, alloc(&c->jump2, sp * c->jwin_rows * sizeof(unsigned)));
+  bool blocks = false;
+  for (size_t t = 1; t < c->jx.steps.size(); ++t) blocks |= !c->jx.steps[t].halo;
+  if (blocks) {
+    const size_t br = (size_t)c->jx.hmax + 2 * (size_t)c->jx.mg_max;
+    HIPCHK(c, alloc(&c->jblk[0], sp * br * sizeof(unsigned)));
+    HIPCHK(c, alloc(&c->jblk[1], sp * br * sizeof(unsigned)));
+  }
+  return RC2DGI_OK;
+}
+
 // (re)allocate every render texture for the current W, H, N (RC2DGI.cs:79-98)
 int allocate(rc2dgi_ctx *c) {
   free_buffers(c);
@@ -250,6 +295,8 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->emissive, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->temp, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->color_out, ns * sizeof(float4)));
+  c->strip = false;
+  c->jwin_rows = (size_t)c->H;
   HIPCHK(c, alloc(&c->jump1, ns * sizeof(unsigned)));
   HIPCHK(c, alloc(&c->jump2, ns * sizeof(unsigned)));
   c->mpitch = ((c->W + 63) / 64) * 2;
@@ -283,6 +330,7 @@ int allocate(rc2dgi_ctx *c) {
   c->rc_order.resize(c->N);
   for (int L = 0; L < c->N; ++L) c->rc_order[L] = default_rc_order(L);
   c->rc_tail.assign(c->N, kDefaultTail);
+  if (int rc = jfa_buffers(c)) return rc;
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
     for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, nc * gsz));
@@ -436,6 +484,7 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
   for (auto &ev : c->ev) (void)hipEventCreate(&ev);
   (void)hipEventCreateWithFlags(&c->ev_phase1, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&c->ev_frame, hipEventDisableTiming);
+  for (auto &ev : c->ev_jfa) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   rc = allocate(c);
   if (rc != RC2DGI_OK) {
     fprintf(stderr, "rc2dgi_create: %s\n", c->err.c_str());
@@ -454,6 +503,8 @@ int rc2dgi_destroy(rc2dgi_ctx *c) {
   if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
   if (c->ev_phase1) (void)hipEventDestroy(c->ev_phase1);
   if (c->ev_frame) (void)hipEventDestroy(c->ev_frame);
+  for (auto &ev : c->ev_jfa)
+    if (ev) (void)hipEventDestroy(ev);
   free_buffers(c);
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -624,8 +675,45 @@ int rc2dgi_upload_device(rc2dgi_ctx *c, int which, const void *dev, int pitch_by
 // ------------------------------------------------------------------ DoRC2DGI()
 namespace {
 
-// phase 1: ScreenUV, JumpFlood, DistanceField (RC2DGI.cs:276-340)
-int do_phase1(rc2dgi_ctx *c, const FramePlan &plan) {
+// phase 1: ScreenUV, JumpFlood, DistanceField (RC2DGI.cs:276-340), in three parts so that the
+// JumpFlood exchange of row-strip shards can run between the steps: phase1_begin (ScreenUV and
+// step 0), phase1_step (step t >= 1), phase1_end.
+// JumpFlood ping-pong (RC2DGI.cs:287-326): step t writes jumpRT2 for even t, jumpRT1 for odd t.
+unsigned *jfa_out(rc2dgi_ctx *c, int t) { return (t & 1) ? c->jump1 : c->jump2; }
+
+int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
+  float ox[3], oy[3];
+  jfa_offsets(c->W, c->H, t, ox, oy);  // vec2(x, y) * _Aspect.yx * _StepSize
+  unsigned short *dist = t == c->S - 1 ? c->dist : nullptr;  // 3. DistanceField fused into the last step
+  hipStream_t st = c->stream;
+  if (!c->strip) {
+    const unsigned *src = t == 0 ? c->occ : jfa_out(c, t - 1);
+    for (auto &r : plan.jfa[t].iv)
+      HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, jfa_out(c, t), dist, c->sd, ox, oy, st,
+                                r.first, r.second));
+    return RC2DGI_OK;
+  }
+  // row-strip shard: the own strip, into its window (global row y0 - m = local row 0)
+  int y0, y1;
+  strip_rows(c->H, c->rank, c->world, y0, y1);
+  const int wrow0 = y0 - c->jx.m;
+  if (t == 0) {
+    HIPCHK(c, launch_jfa_step(true, c->occ, c->mpitch, jfa_out(c, 0), dist, c->sd, ox, oy, st, y0, y1, nullptr, wrow0));
+    return RC2DGI_OK;
+  }
+  int buf[3], row0[3];
+  jfa_window(c->jx, t, c->rank, buf, row0);
+  JfaSrc win{};
+  win.on = 1;
+  for (int y = 0; y < 3; ++y) {
+    win.base[y] = buf[y] == 0 ? jfa_out(c, t - 1) : c->jblk[buf[y] - 1];
+    win.row0[y] = row0[y];
+  }
+  HIPCHK(c, launch_jfa_step(false, nullptr, c->sd.pitch, jfa_out(c, t), dist, c->sd, ox, oy, st, y0, y1, &win, wrow0));
+  return RC2DGI_OK;
+}
+
+int phase1_begin(rc2dgi_ctx *c, const FramePlan &plan) {
   HIPCHK(c, hipSetDevice(c->device));
   int rc = upload_tables(c);
   if (rc != RC2DGI_OK) return rc;
@@ -633,8 +721,9 @@ int do_phase1(rc2dgi_ctx *c, const FramePlan &plan) {
   const bool T = c->timing;
   if (c->poison) {  // debug: rows a (sharded) frame never writes read as NaN / far seeds / far distance
     const size_t ns = (size_t)c->sd.pitch * c->H, nc = (size_t)c->cd.pitch * c->CH;
-    HIPCHK(c, hipMemsetAsync(c->jump1, 0xFF, ns * 4, st));
-    HIPCHK(c, hipMemsetAsync(c->jump2, 0xFF, ns * 4, st));
+    HIPCHK(c, hipMemsetAsync(c->jump1, 0xFF, (size_t)c->sd.pitch * c->jwin_rows * 4, st));
+    HIPCHK(c, hipMemsetAsync(c->jump2, 0xFF, (size_t)c->sd.pitch * c->jwin_rows * 4, st));
+    HIPCHK(c, hipMemsetAsync(c->occ, 0xFF, (size_t)c->mpitch * c->H * 4, st));
     HIPCHK(c, hipMemsetAsync(c->dist, 0xFF, ns * 2, st));
     HIPCHK(c, hipMemsetAsync(c->temp, 0xFF, ns * 16, st));
     HIPCHK(c, hipMemsetAsync(c->color_out, 0xFF, ns * 16, st));
@@ -644,26 +733,63 @@ int do_phase1(rc2dgi_ctx *c, const FramePlan &plan) {
   if (T) HIPCHK(c, hipEventRecord(c->ev[0], st));
 
   // 1. ScreenUV (RC2DGI.cs:276-285): occupancy mask; J0 itself is only materialised when a
-  //    single JFA step leaves it visible in jumpRT1
-  HIPCHK(c, launch_occupancy(c->color_in, c->occ, c->mpitch, c->sd, st));
+  //    single JFA step leaves it visible in jumpRT1.  A row-strip shard computes the mask rows its
+  //    step 0 taps (from the replicated colorRT).
+  if (c->strip) {
+    for (auto &r : jfa_mask_rows(c->W, c->H, c->rank, c->world).iv)
+      HIPCHK(c, launch_occupancy(c->color_in, c->occ, c->mpitch, c->sd, st, r.first, r.second));
+  } else {
+    HIPCHK(c, launch_occupancy(c->color_in, c->occ, c->mpitch, c->sd, st));
+  }
   if (c->S == 1) HIPCHK(c, launch_seeds_from_mask(c->occ, c->mpitch, c->jump1, c->sd, st));
   if (T) HIPCHK(c, hipEventRecord(c->ev[1], st));
+  // 2. JumpFlood step 0 (from the mask)
+  return jfa_launch(c, plan, 0);
+}
 
-  // 2. JumpFlood ping-pong (RC2DGI.cs:287-326); 3. DistanceField fused into the last step
-  bool j1final = true;
-  for (int i = 0; i < c->S; ++i) {
-    float ox[3], oy[3];
-    jfa_offsets(c->W, c->H, i, ox, oy);  // vec2(x, y) * _Aspect.yx * _StepSize
-    const bool last = i == c->S - 1;
-    const unsigned *src = i == 0 ? c->occ : (j1final ? c->jump1 : c->jump2);
-    unsigned *dst = j1final ? c->jump2 : c->jump1;
-    for (auto &r : plan.jfa[i].iv)
-      HIPCHK(c, launch_jfa_step(i == 0, src, i == 0 ? c->mpitch : c->sd.pitch, dst, last ? c->dist : nullptr,
-                                c->sd, ox, oy, st, r.first, r.second));
-    j1final = !j1final;
-  }
-  if (T) HIPCHK(c, hipEventRecord(c->ev[2], st));
+int phase1_end(rc2dgi_ctx *c) {
+  if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   return RC2DGI_OK;
+}
+
+// device pointer of row `row` of a JumpFlood exchange buffer (0 the window holding J_{t-1}, 1 / 2 blocks)
+unsigned *jfa_xbuf(rc2dgi_ctx *c, int t, int buf, int row) {
+  unsigned *b = buf == 0 ? jfa_out(c, t - 1) : c->jblk[buf - 1];
+  return b + (size_t)row * c->sd.pitch;
+}
+
+// the JumpFlood exchange of step t over RCCL: every transfer this shard sends or receives as
+// ncclSend / ncclRecv in one group on the context stream (rows of its own window to itself:
+// device copies)
+int jfa_exchange_rccl(rc2dgi_ctx *c, int t) {
+  const Rccl &R = rccl();
+  const size_t rowb = (size_t)c->sd.pitch * sizeof(unsigned);
+  ncclResult_t e = R.group_start();
+  for (const JfaXfer &x : c->jx.steps[t].xfers) {
+    if (e != ncclSuccess) break;
+    if (x.src == c->rank && x.dst == c->rank) {
+      HIPCHK(c, hipMemcpyAsync(jfa_xbuf(c, t, x.dst_buf, x.dst_row), jfa_xbuf(c, t, 0, x.src_row), x.rows * rowb,
+                               hipMemcpyDeviceToDevice, c->stream));
+    } else if (x.src == c->rank) {
+      e = R.send(jfa_xbuf(c, t, 0, x.src_row), x.rows * rowb, ncclUint8, x.dst, c->comm, c->stream);
+    } else if (x.dst == c->rank) {
+      e = R.recv(jfa_xbuf(c, t, x.dst_buf, x.dst_row), x.rows * rowb, ncclUint8, x.src, c->comm, c->stream);
+    }
+  }
+  const ncclResult_t e2 = R.group_end();
+  if (e == ncclSuccess) e = e2;
+  if (e != ncclSuccess) return fail(c, RC2DGI_E_HIP, std::string("JumpFlood exchange: ") + R.error_string(e));
+  return RC2DGI_OK;
+}
+
+// one phase 1 on a context with its own exchange (RCCL communicator) or none (unsharded)
+int do_phase1(rc2dgi_ctx *c, const FramePlan &plan) {
+  int rc = phase1_begin(c, plan);
+  for (int t = 1; rc == RC2DGI_OK && t < c->S; ++t) {
+    if (c->strip) rc = jfa_exchange_rccl(c, t);
+    if (rc == RC2DGI_OK) rc = jfa_launch(c, plan, t);
+  }
+  return rc == RC2DGI_OK ? phase1_end(c) : rc;
 }
 
 // phase 2: cascades, blur, merge (RC2DGI.cs:342-404)
@@ -805,6 +931,10 @@ int rc2dgi_do(rc2dgi_ctx *c) {
 int rc2dgi_do_phase(rc2dgi_ctx *c, int phase) {
   if (!c) return RC2DGI_E_ARG;
   if (phase != 1 && phase != 2) return fail(c, RC2DGI_E_ARG, "phase is 1 or 2");
+  if (phase == 1 && c->strip)
+    return fail(c, RC2DGI_E_STATE,
+                "phase 1 of a row-strip shard exchanges JumpFlood rows between its steps: use rc2dgi_do with a "
+                "communicator, or rc2dgi_do_group");
   const FramePlan plan = make_plan(c);
   return phase == 1 ? do_phase1(c, plan) : do_phase2(c, plan);
 }
@@ -870,8 +1000,39 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
     for (int q = 0; q < n; ++q)
       if (q != k) HIPCHK(cs[k], hipStreamWaitEvent(cs[k]->stream, cs[q]->ev_frame, 0));
   }
+  // phase 1, step by step over the group: before step t every shard copies the rows of J_{t-1} it
+  // receives (JumpFlood exchange plan) from their owners, after the owners' step t-1
+  std::vector<FramePlan> plans;
+  for (int k = 0; k < n; ++k) plans.push_back(make_plan(cs[k]));
   for (int k = 0; k < n; ++k) {
-    int rc = do_phase1(cs[k], make_plan(cs[k]));
+    int rc = phase1_begin(cs[k], plans[k]);
+    if (rc != RC2DGI_OK) return rc;
+    HIPCHK(cs[k], hipEventRecord(cs[k]->ev_jfa[0], cs[k]->stream));
+  }
+  for (int t = 1; t < cs[0]->S; ++t) {
+    for (int k = 0; k < n; ++k) {
+      rc2dgi_ctx *c = cs[k];
+      HIPCHK(c, hipSetDevice(c->device));
+      if (c->strip) {
+        const size_t rowb = (size_t)c->sd.pitch * sizeof(unsigned);
+        std::vector<int> waited(n, 0);
+        for (const JfaXfer &x : c->jx.steps[t].xfers) {
+          if (x.dst != k) continue;
+          if (x.src != k && !waited[x.src]) {
+            HIPCHK(c, hipStreamWaitEvent(c->stream, cs[x.src]->ev_jfa[(t - 1) & 1], 0));
+            waited[x.src] = 1;
+          }
+          HIPCHK(c, hipMemcpyAsync(jfa_xbuf(c, t, x.dst_buf, x.dst_row), jfa_xbuf(cs[x.src], t, 0, x.src_row),
+                                   x.rows * rowb, hipMemcpyDeviceToDevice, c->stream));
+        }
+      }
+      int rc = jfa_launch(c, plans[k], t);
+      if (rc != RC2DGI_OK) return rc;
+      HIPCHK(c, hipEventRecord(c->ev_jfa[t & 1], c->stream));
+    }
+  }
+  for (int k = 0; k < n; ++k) {
+    int rc = phase1_end(cs[k]);
     if (rc != RC2DGI_OK) return rc;
     HIPCHK(cs[k], hipEventRecord(cs[k]->ev_phase1, cs[k]->stream));
   }
@@ -890,7 +1051,7 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
   }
   // phase 2 of a context overwrites nothing a peer still copies from (only distRT is read)
   for (int k = 0; k < n; ++k) {
-    int rc = do_phase2(cs[k], make_plan(cs[k]));
+    int rc = do_phase2(cs[k], plans[k]);
     if (rc != RC2DGI_OK) return rc;
     HIPCHK(cs[k], hipEventRecord(cs[k]->ev_frame, cs[k]->stream));
   }
@@ -909,7 +1070,9 @@ int rc2dgi_set_shard(rc2dgi_ctx *c, int rank, int world) {
   c->rank = rank;
   c->world = world;
   c->frame_done = c->have_frame = false;
-  return RC2DGI_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return jfa_buffers(c);  // strip windows (world > 1) or full-size jumpRT1 / jumpRT2
 }
 
 int rc2dgi_shard_rows(rc2dgi_ctx *c, int *y0, int *y1) {
@@ -972,6 +1135,40 @@ int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int tile_w, int tile_h
       n > tiles_x * tiles_y * ngrp || (n && (!tiles || !groups)))
     return RC2DGI_E_ARG;
   return rc_order_plan(code, tiles_x, tiles_y, tile_w, tile_h, ngrp, tiles, groups, n);
+}
+
+int rc2dgi_plan_jfa_exchange(const rc2dgi_config *cfg, int world, int step, int *info, int *xfers, int max_xfers) {
+  if (!cfg || !info || cfg->screen_width < 1 || cfg->screen_height < 1 || cfg->cascade_count < 1 ||
+      cfg->cascade_count > 15 || !(cfg->render_scale > 0.0f) || world < 2 || world > cfg->screen_height ||
+      max_xfers < 0 || (max_xfers > 0 && !xfers))
+    return RC2DGI_E_ARG;
+  int CW, CH, S;
+  derive_sizes(cfg->screen_width, cfg->screen_height, cfg->cascade_count, cfg->render_scale, CW, CH, S);
+  if (S < 2 || step < 1 || step >= S) return RC2DGI_E_ARG;
+  const JfaExchange x = plan_jfa_exchange(cfg->screen_width, cfg->screen_height, S, world);
+  const JfaExStep &st = x.steps[step];
+  const int v[9] = {x.m, x.hmax, x.mg_max, st.halo, st.sh[0], st.sh[1], st.sh[2], st.mg, st.same_block};
+  for (int k = 0; k < 9; ++k) info[k] = v[k];
+  int n = 0;
+  for (const JfaXfer &t : st.xfers) {
+    if (n < max_xfers) {
+      const int r[6] = {t.src, t.src_row, t.rows, t.dst, t.dst_buf, t.dst_row};
+      for (int k = 0; k < 6; ++k) xfers[6 * n + k] = r[k];
+    }
+    ++n;
+  }
+  return n;
+}
+
+int rc2dgi_plan_jfa_window(const rc2dgi_config *cfg, int rank, int world, int step, int *buf, int *row0) {
+  if (!cfg || !buf || !row0 || world < 2 || rank < 0 || rank >= world || world > cfg->screen_height ||
+      cfg->cascade_count < 1 || cfg->cascade_count > 15 || !(cfg->render_scale > 0.0f))
+    return RC2DGI_E_ARG;
+  int CW, CH, S;
+  derive_sizes(cfg->screen_width, cfg->screen_height, cfg->cascade_count, cfg->render_scale, CW, CH, S);
+  if (S < 2 || step < 1 || step >= S) return RC2DGI_E_ARG;
+  jfa_window(plan_jfa_exchange(cfg->screen_width, cfg->screen_height, S, world), step, rank, buf, row0);
+  return RC2DGI_OK;
 }
 
 int rc2dgi_plan_rows(const rc2dgi_config *cfg, float blur_radius, int rank, int world, int pass, int *intervals,
@@ -1237,9 +1434,16 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
       break;
     case RC2DGI_RT_JUMP1:
     case RC2DGI_RT_JUMP2: {  // packed seed -> the reference's (u, v, 0, 1), (0,0,0,1) = no seed
-      std::vector<unsigned> s((size_t)w * h);
-      HIPCHK(c, hipMemcpy2D(s.data(), (size_t)w * 4, which == RC2DGI_RT_JUMP1 ? c->jump1 : c->jump2,
-                            (size_t)pitch * 4, (size_t)w * 4, h, hipMemcpyDeviceToHost));
+      std::vector<unsigned> s((size_t)w * h, rgba8(c) ? 0u : 0x80008000u);
+      const unsigned *jb = which == RC2DGI_RT_JUMP1 ? c->jump1 : c->jump2;
+      if (c->strip) {  // a row-strip shard holds its own rows (window rows m .. m + h - 1)
+        int y0, y1;
+        strip_rows(c->H, c->rank, c->world, y0, y1);
+        HIPCHK(c, hipMemcpy2D(s.data() + (size_t)y0 * w, (size_t)w * 4, jb + (size_t)c->jx.m * pitch,
+                              (size_t)pitch * 4, (size_t)w * 4, y1 - y0, hipMemcpyDeviceToHost));
+      } else {
+        HIPCHK(c, hipMemcpy2D(s.data(), (size_t)w * 4, jb, (size_t)pitch * 4, (size_t)w * 4, h, hipMemcpyDeviceToHost));
+      }
       for (size_t k = 0; k < s.size(); ++k) {
         if (rgba8(c)) {  // the unorm8 seed uv (kv << 16 | ku) itself
           img[k] = make_float4((float)(s[k] & 0xFFFFu) * kInv255h, (float)(s[k] >> 16) * kInv255h, 0.0f, 1.0f);

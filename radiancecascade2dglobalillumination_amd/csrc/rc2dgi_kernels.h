@@ -34,8 +34,9 @@ struct CascadeDims {
                // cascadeBlurRT as bytes, 8-bit blends and filtering
 };
 
-// ScreenUV (shaders/ScreenUV.fs) as a 1-bit occupancy mask (row pitch mpitch 32-bit words)
-hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, ScreenDims s, hipStream_t st);
+// ScreenUV (shaders/ScreenUV.fs) as a 1-bit occupancy mask (row pitch mpitch 32-bit words), rows [row0, row1)
+hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, ScreenDims s, hipStream_t st,
+                            int row0 = 0, int row1 = -1);
 // the ScreenUV seed texture J0 (packed seeds) from the mask
 hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *seeds, ScreenDims s, hipStream_t st);
 
@@ -44,9 +45,19 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
 // first: src is the occupancy mask (pitch in words), else packed seeds (pitch in texels).
 // off_x/off_y = vec2(k,k)*_Aspect.yx*_StepSize for k = -1,0,1 (host-computed).
 // dist != nullptr fuses DistanceField.fs: stores the 16-bit q of packUNorm16.
+// Row-strip shards (window != nullptr, not the first step): tap y (dy = -1, 0, +1) reads its rows
+// from window->base[y], whose local row 0 is global row window->row0[y] (rows taken modulo H: a
+// shard's halo / block buffers, filled by the exchange); the output row j goes to dst row
+// j - dst_row0 (the shard's own window).
+struct JfaSrc {
+  const unsigned *base[3];
+  int row0[3];
+  int on;
+};
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0 = 0,
-                           int row1 = -1);  // output rows [row0, row1) (-1 = H)
+                           int row1 = -1,  // output rows [row0, row1) (-1 = H)
+                           const JfaSrc *window = nullptr, int dst_row0 = 0);
 // integer taps of the power-of-two JFA kernel (false: the float path runs); also used by the
 // row-strip planner
 bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp);

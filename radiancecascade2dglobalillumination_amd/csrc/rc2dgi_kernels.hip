@@ -53,24 +53,24 @@ __device__ __forceinline__ bool seed_u8_ok(unsigned sd) { return (sd & 0xFFFFu) 
 // the JFA runs >= 2 steps (step 1 overwrites jumpRT1), so step 0 reads the mask instead.
 constexpr int kOccRows = 16;  // rows per wave in k_occupancy (4 rows apart), all loads issued together
 __global__ __launch_bounds__(256) void k_occupancy(const float4 *__restrict__ color, unsigned *__restrict__ mask,
-                                                   ScreenDims s, int mpitch) {
+                                                   ScreenDims s, int mpitch, int row0, int row1) {
   // kOccRows rows per wave, one 64-texel ballot per row; non-temporal loads (colorRT is read
   // again only by the merge, after the cascades have cycled the caches)
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j0 = blockIdx.y * (4 * kOccRows) + (threadIdx.x >> 6);
+  const int j0 = row0 + blockIdx.y * (4 * kOccRows) + (threadIdx.x >> 6);
   v4f_t c[kOccRows];
 #pragma unroll
   for (int t = 0; t < kOccRows; ++t) {
     const int j = j0 + 4 * t;
     c[t] = __builtin_nontemporal_load(
-        reinterpret_cast<const v4f_t *>(color + (size_t)min(j, s.H - 1) * s.pitch + min(i, s.W - 1)));
+        reinterpret_cast<const v4f_t *>(color + (size_t)min(j, row1 - 1) * s.pitch + min(i, s.W - 1)));
   }
 #pragma unroll
   for (int t = 0; t < kOccRows; ++t) {
     const int j = j0 + 4 * t;
-    const bool occ = i < s.W && j < s.H && (c[t].x > 0.0f || c[t].y > 0.0f || c[t].z > 0.0f);
+    const bool occ = i < s.W && j < row1 && (c[t].x > 0.0f || c[t].y > 0.0f || c[t].z > 0.0f);
     const unsigned long long b = __ballot(occ);
-    if ((threadIdx.x & 63) == 0 && j < s.H) {
+    if ((threadIdx.x & 63) == 0 && j < row1) {
       unsigned *row = mask + (size_t)j * mpitch + (blockIdx.x * 2);
       row[0] = (unsigned)b;
       row[1] = (unsigned)(b >> 32);
@@ -106,7 +106,8 @@ constexpr int JT = 4;
 template <bool FIRST, bool U8>
 __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ src, int src_pitch,
                                                   unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
-                                                  ScreenDims s, JfaOffsets o, int row0, int row1) {
+                                                  ScreenDims s, JfaOffsets o, int row0, int row1, JfaSrc win,
+                                                  int dst_row0) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j0 = row0 + blockIdx.y * (4 * JT) + (threadIdx.x >> 6);
   if (i >= s.W) return;
@@ -131,6 +132,10 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
             seed[t][y * 3 + x] = occ ? pack_seed_u8(ti[x], tj, ax, ay) : 0u;
           else
             seed[t][y * 3 + x] = occ ? pack_seed(ti[x], tj) : kNoSeed;
+        } else if (win.on) {  // row-strip shard: the tap's rows sit in a local window (JfaSrc)
+          int lr = tj - win.row0[y];
+          lr += lr < 0 ? s.H : 0;
+          seed[t][y * 3 + x] = win.base[y][(size_t)lr * src_pitch + ti[x]];
         } else {
           seed[t][y * 3 + x] = src[(size_t)tj * src_pitch + ti[x]];
         }
@@ -160,7 +165,7 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
         }
       }
     }
-    dst[(size_t)j * s.pitch + i] = best;
+    dst[(size_t)(j - dst_row0) * s.pitch + i] = best;
     if (dist) {
       // DistanceField.fs: distance(fragTexCoord, seed) -> packUNorm16: store the 16-bit q
       // (RadianceCascades.fs unpackUNorm16 recovers exactly q / 65535)
@@ -195,7 +200,8 @@ __host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
 template <bool FIRST, bool IKEY, bool U8 = false>
 __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src, int src_pitch,
                                                 unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
-                                                ScreenDims s, JfaTaps o, int row0, int row1, int lattice) {
+                                                ScreenDims s, JfaTaps o, int row0, int row1, int lattice,
+                                                JfaSrc win, int dst_row0) {
   int bx = blockIdx.x, by = blockIdx.y;
   if (lattice) {
     // Lattice order for the long steps: the tiles (bx + a * ptx, by + b * pty) tap one another
@@ -226,7 +232,10 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
 #pragma unroll
     for (int y = 0; y < 3; ++y) {
       const unsigned tj = (unsigned)(j + o.dy[y]) & (unsigned)(s.H - 1);
-      const unsigned *row = src + (size_t)tj * src_pitch;
+      // row-strip shard (not the first step): the tap's rows sit in a local window (JfaSrc)
+      const unsigned *row = (!FIRST && win.on)
+                                ? win.base[y] + (size_t)((tj - (unsigned)win.row0[y]) & (unsigned)(s.H - 1)) * src_pitch
+                                : src + (size_t)tj * src_pitch;
       const unsigned qy = (FIRST && U8) ? pack_seed_u8(0, (int)tj, Axis{s.W, 1}, Axis{s.H, 1}) & 0xFFFF0000u : 0u;
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
@@ -268,7 +277,7 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
 #pragma unroll
       for (int k = 7; k >= 0; --k) best = kb[k] == m ? seed[t][k] : best;
       if (m >= 0x3f800000u) best = 0u;
-      dst[(size_t)j * s.pitch + i] = best;
+      dst[(size_t)(j - dst_row0) * s.pitch + i] = best;
       if (dist) {
         const float bx = best ? (float)(best & 0xFFFFu) * kInv255 : 0.0f;
         const float by = best ? (float)(best >> 16) * kInv255 : 0.0f;
@@ -312,7 +321,7 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
         }
       }
     }
-    dst[(size_t)j * s.pitch + i] = best;
+    dst[(size_t)(j - dst_row0) * s.pitch + i] = best;
     if (dist) {  // DistanceField.fs, as in k_jfa_step
       const Axis ax{s.W, 1}, ay{s.H, 1};
       float bx = 0.0f, by = 0.0f;
@@ -761,9 +770,13 @@ __global__ __launch_bounds__(256) void k_quantize_u8(float4 *__restrict__ buf, i
 // ---------------------------------------------------------------- launchers
 static dim3 grid2d(int w, int h) { return dim3(ceil_div(w, 64), ceil_div(h, 4)); }
 
-hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, ScreenDims s, hipStream_t st) {
-  hipLaunchKernelGGL(k_occupancy, dim3(ceil_div(s.W, 64), ceil_div(s.H, 4 * kOccRows)), dim3(256), 0, st, color, mask,
-                     s, mpitch);
+hipError_t launch_occupancy(const float4 *color, unsigned *mask, int mpitch, ScreenDims s, hipStream_t st, int row0,
+                            int row1) {
+  if (row1 < 0 || row1 > s.H) row1 = s.H;
+  if (row0 < 0) row0 = 0;
+  if (row0 >= row1) return hipSuccess;
+  hipLaunchKernelGGL(k_occupancy, dim3(ceil_div(s.W, 64), ceil_div(row1 - row0, 4 * kOccRows)), dim3(256), 0, st,
+                     color, mask, s, mpitch, row0, row1);
   return hipGetLastError();
 }
 
@@ -802,7 +815,9 @@ bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTa
 
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0,
-                           int row1) {
+                           int row1, const JfaSrc *window, int dst_row0) {
+  JfaSrc win{};
+  if (window && !first) win = *window;
   if (row1 < 0 || row1 > s.H) row1 = s.H;
   if (row0 < 0) row0 = 0;
   if (row0 >= row1) return hipSuccess;
@@ -816,28 +831,28 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   const bool p2 = jfa_p2_taps(s, off_x, off_y, &tp);
   // lattice order (k_jfa_p2) for whole-frame launches whose steps span several tiles (not the
   // first step: its taps read the 2 MB occupancy mask, which every L2 holds anyway)
-  const bool full = !first && row0 == 0 && row1 == s.H && s.W >= 64 && s.H >= 4 * JT && s.H % (4 * JT) == 0;
+  const bool full = !first && !win.on && row0 == 0 && row1 == s.H && s.W >= 64 && s.H >= 4 * JT && s.H % (4 * JT) == 0;
   const int lattice = p2 && full && (tp.dx[2] >= 128 || tp.dy[2] >= 64) && tp.dx[2] >= 0 && tp.dy[2] >= 0 &&
                       (tp.dx[2] & (tp.dx[2] - 1)) == 0 && (tp.dy[2] & (tp.dy[2] - 1)) == 0 &&
                       tp.dx[2] <= s.W && tp.dy[2] <= s.H;
   if (s.u8 && p2) {  // RGBA8 jumpRT on a power-of-two screen: integer taps, quantized-uv distance
     if (first)
       hipLaunchKernelGGL((k_jfa_p2<true, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp,
-                         row0, row1, lattice);
+                         row0, row1, lattice, win, dst_row0);
     else
       hipLaunchKernelGGL((k_jfa_p2<false, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp,
-                         row0, row1, lattice);
+                         row0, row1, lattice, win, dst_row0);
   } else if (s.u8) {  // RGBA8 jumpRT: quantized seed uv, the float path
     if (first)
-      hipLaunchKernelGGL((k_jfa_step<true, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
+      hipLaunchKernelGGL((k_jfa_step<true, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
     else
       hipLaunchKernelGGL((k_jfa_step<false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
-                         row1);
+                         row1, win, dst_row0);
   } else if (p2) {
     const bool ikey = s.W == s.H && s.W <= 4096;
 #define RC2DGI_JFA(F, K)                                                                                      \
   hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1, \
-                     lattice)
+                     lattice, win, dst_row0)
     if (first) {
       if (ikey) RC2DGI_JFA(true, true); else RC2DGI_JFA(true, false);
     } else {
@@ -845,10 +860,10 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     }
 #undef RC2DGI_JFA
   } else if (first) {
-    hipLaunchKernelGGL((k_jfa_step<true, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1);
+    hipLaunchKernelGGL((k_jfa_step<true, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
   } else {
     hipLaunchKernelGGL((k_jfa_step<false, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
-                       row1);
+                       row1, win, dst_row0);
   }
   return hipGetLastError();
 }

@@ -120,7 +120,16 @@ FramePlan plan_frame(const PlanInputs &in) {
     }
     p.level[L + 1] = up;
   }
-  // JFA, backwards from the distance-field strip
+  // JFA: with two or more steps every step computes the own strip and receives the rows its taps
+  // reach (plan_jfa_exchange)
+  if (in.S >= 2) {
+    for (int t = 0; t < in.S; ++t) {
+      p.jfa[t] = RowSet::none(in.H);
+      p.jfa[t].add(p.y0, p.y1);
+    }
+    return p;
+  }
+  // (a single step: backwards from the distance-field strip)
   ScreenDims sd{in.W, in.H, in.W, (in.W & (in.W - 1)) == 0, (in.H & (in.H - 1)) == 0};
   p.jfa[in.S - 1] = RowSet::none(in.H);
   p.jfa[in.S - 1].add(p.y0, p.y1);
@@ -146,6 +155,125 @@ FramePlan plan_frame(const PlanInputs &in) {
     p.jfa[t - 1] = prev;
   }
   return p;
+}
+
+}  // namespace rc2dgi
+
+namespace rc2dgi {
+
+namespace {
+// tap row shifts of JFA step t and their rounding margin (integer taps of power-of-two screens
+// are exact; NEAREST of fract(v + off) elsewhere lands within +-1 of j + floor(0.5 + off H))
+void jfa_tap_rows(int W, int H, int t, int sh[3], int &mg) {
+  float ox[3], oy[3];
+  jfa_offsets(W, H, t, ox, oy);
+  ScreenDims sd{W, H, W, (W & (W - 1)) == 0, (H & (H - 1)) == 0};
+  JfaTaps tp;
+  if (jfa_p2_taps(sd, ox, oy, &tp)) {
+    for (int y = 0; y < 3; ++y) sh[y] = tp.dy[y];
+    mg = 0;
+  } else {
+    for (int y = 0; y < 3; ++y) sh[y] = (int)std::floor(0.5 + (double)oy[y] * H);
+    mg = 1;
+  }
+}
+
+int mod(long a, int n) {
+  long r = a % n;
+  return (int)(r < 0 ? r + n : r);
+}
+
+int owner_of(int g, int H, int world) {  // the shard whose strip holds global row g in [0, H)
+  int r = (int)((long long)g * world / H);
+  int y0, y1;
+  for (;;) {
+    strip_rows(H, r, world, y0, y1);
+    if (g < y0) --r;
+    else if (g >= y1) ++r;
+    else return r;
+  }
+}
+}  // namespace
+
+JfaExchange plan_jfa_exchange(int W, int H, int S, int world) {
+  JfaExchange x;
+  x.world = world;
+  x.H = H;
+  x.steps.resize(S);
+  int hmin = H;
+  for (int r = 0; r < world; ++r) {
+    int y0, y1;
+    strip_rows(H, r, world, y0, y1);
+    hmin = std::min(hmin, y1 - y0);
+    x.hmax = std::max(x.hmax, y1 - y0);
+  }
+  for (int t = 1; t < S; ++t) {
+    JfaExStep &st = x.steps[t];
+    jfa_tap_rows(W, H, t, st.sh, st.mg);
+    const int s = std::max(std::abs(st.sh[0]), std::abs(st.sh[2]));
+    st.halo = s + st.mg < hmin;
+    if (st.halo) x.m = std::max(x.m, s + st.mg);
+    else x.mg_max = std::max(x.mg_max, st.mg);
+    st.same_block = !st.halo && mod((long)st.sh[2] - st.sh[0], H) == 0;
+  }
+  for (int t = 1; t < S; ++t) {
+    JfaExStep &st = x.steps[t];
+    for (int q = 0; q < world; ++q) {
+      int y0, y1;
+      strip_rows(H, q, world, y0, y1);
+      // (global first row, row count, destination buffer, destination local row)
+      struct Need { long g; int n, buf, row; };
+      std::vector<Need> need;
+      if (st.halo) {
+        const int e = std::max(std::abs(st.sh[0]), std::abs(st.sh[2])) + st.mg;
+        if (e > 0) {
+          need.push_back({(long)y0 - e, e, 0, x.m - e});
+          need.push_back({(long)y1, e, 0, x.m + (y1 - y0)});
+        }
+      } else {
+        need.push_back({(long)y0 + st.sh[0] - st.mg, (y1 - y0) + 2 * st.mg, 1, 0});
+        if (!st.same_block) need.push_back({(long)y0 + st.sh[2] - st.mg, (y1 - y0) + 2 * st.mg, 2, 0});
+      }
+      for (const Need &nd : need) {
+        int done = 0;
+        while (done < nd.n) {
+          const int g = mod(nd.g + done, H);
+          const int p = owner_of(g, H, world);
+          int p0, p1;
+          strip_rows(H, p, world, p0, p1);
+          const int cnt = std::min(nd.n - done, p1 - g);
+          st.xfers.push_back({p, x.m + (g - p0), cnt, q, nd.buf, nd.row + done});
+          done += cnt;
+        }
+      }
+    }
+  }
+  return x;
+}
+
+void jfa_window(const JfaExchange &x, int t, int rank, int buf[3], int row0[3]) {
+  int y0, y1;
+  strip_rows(x.H, rank, x.world, y0, y1);
+  const JfaExStep &st = x.steps[t];
+  for (int y = 0; y < 3; ++y) {
+    if (st.halo || st.sh[y] == 0) {
+      buf[y] = 0;
+      row0[y] = mod((long)y0 - x.m, x.H);
+    } else {
+      buf[y] = (st.same_block || st.sh[y] < 0) ? 1 : 2;
+      const int sh = st.same_block ? st.sh[0] : st.sh[y];
+      row0[y] = mod((long)y0 + sh - st.mg, x.H);
+    }
+  }
+}
+
+RowSet jfa_mask_rows(int W, int H, int rank, int world) {
+  int y0, y1, sh[3], mg;
+  strip_rows(H, rank, world, y0, y1);
+  jfa_tap_rows(W, H, 0, sh, mg);
+  RowSet r = RowSet::none(H);
+  for (int y = 0; y < 3; ++y) r.add((long)y0 + sh[y] - mg, (long)y1 + sh[y] + mg);
+  return r;
 }
 
 }  // namespace rc2dgi

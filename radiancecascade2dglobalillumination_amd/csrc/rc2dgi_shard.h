@@ -1,13 +1,12 @@
 // Row-strip sharding of one DoRC2DGI() frame over P ranks.
 //
-// Rank r owns screen rows [r*H/P, (r+1)*H/P) of the merged colorRT.  Every rank holds full-size
-// render textures and computes exactly the rows its strip depends on, walking the pass chain
-// backwards (merge <- blur/copy-back <- G_0 <- G_1 ... <- G_{N-1}; DF <- last JFA step <- ... <-
-// first JFA step).  Dependencies that cross strips are small and are computed redundantly
-// (a few probe rows per block per level, the blur halo, the tails of the JFA steps); the early
-// JFA steps, whose taps span the screen, come out full-size.  The one exchange is the 16-bit
-// distance field: rays sample it anywhere, so after the JFA/DF phase each rank's strip is
-// broadcast to the others (RCCL or device copies), then the cascade phase runs.
+// Rank r owns screen rows [r*H/P, (r+1)*H/P) of the merged colorRT.  The JumpFlood steps compute
+// exactly the own strip and exchange the rows their taps reach (plan_jfa_exchange: ring halos for
+// the short steps, strip-sized blocks from the owners at +-offset for the long ones), into
+// strip-sized windows.  The distance field is then all-gathered (rays sample it anywhere), and
+// the cascade phase computes exactly the rows the strip depends on, walking the chain backwards
+// (merge <- blur/copy-back <- G_0 <- G_1 ... <- G_{N-1}); those dependencies cross strips by a
+// few probe rows per block per level and the blur halo, computed redundantly.
 #pragma once
 
 #include <utility>
@@ -52,5 +51,44 @@ void jfa_offsets(int W, int H, int step, float ox[3], float oy[3]);
 void strip_rows(int H, int rank, int world, int &y0, int &y1);
 
 FramePlan plan_frame(const PlanInputs &in);
+
+// ---- JumpFlood exchange (SURVEY §8e "JFA"): with more than one shard every JFA step computes
+// exactly the shard's own strip; before step t the rows of J_{t-1} its taps reach are received
+// from their owners.  Tap rows are j + sh (integer taps of power-of-two screens, exact) or
+// NEAREST of fract(v + off) (other sizes: j + sh +- 1, margin mg = 1).  A step whose offset s
+// (+ mg) stays below the shortest strip is a halo step: the s + mg rows above and below the strip
+// come from the ring neighbours (cyclic) into the halo rows of the shard's window.  A longer step
+// is a block step: the two strip-sized blocks at +-s (cyclic shift; each spans at most two owners)
+// go into two block buffers.  Step 0 reads the ScreenUV mask, which every shard computes itself
+// from the replicated colorRT (only the rows step 0 taps).
+// Buffers of shard q: the window (per JFA ping-pong texture) holds global rows
+// [y0_q - m, y1_q + m) (modulo H) as local rows 0 .. h_q + 2m - 1; blocks A and B hold
+// hmax + 2 mg rows.
+struct JfaXfer {
+  int src, src_row;   // owner shard and the local row of its window (inside its own strip)
+  int rows;
+  int dst, dst_buf;   // receiving shard; 0 its window, 1 block A, 2 block B
+  int dst_row;        // local row in that buffer
+};
+struct JfaExStep {
+  int halo = 1;       // 1 halo step, 0 block step
+  int sh[3] = {0, 0, 0};  // tap row shifts (dy = -1, 0, +1)
+  int mg = 0;         // rounding margin of the tap rows (0 integer taps, 1 float taps)
+  int same_block = 0;  // block step with -s == +s modulo H: both taps read block A
+  std::vector<JfaXfer> xfers;  // every transfer of the step, all shards, in one fixed order
+};
+struct JfaExchange {
+  int world = 1, H = 0;
+  int m = 0;          // halo rows of a window
+  int hmax = 0;       // tallest strip
+  int mg_max = 0;     // largest margin (block buffer rows = hmax + 2 mg_max)
+  std::vector<JfaExStep> steps;  // index t = the step that reads J_{t-1} (steps[0] unused)
+};
+JfaExchange plan_jfa_exchange(int W, int H, int S, int world);
+// where shard `rank` finds the rows tap y of step t reads: buffer (0 window, 1 A, 2 B) and the
+// global row (mod H) of the buffer's local row 0
+void jfa_window(const JfaExchange &x, int t, int rank, int buf[3], int row0[3]);
+// screen rows of the ScreenUV mask step 0 of shard `rank` reads
+RowSet jfa_mask_rows(int W, int H, int rank, int world);
 
 }  // namespace rc2dgi

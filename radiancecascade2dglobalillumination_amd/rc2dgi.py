@@ -108,6 +108,10 @@ def load_library(path: Optional[str] = None):
         "rc2dgi_device_buffer": ([vp, ctypes.c_int, ctypes.POINTER(vp), ip], ctypes.c_int),
         "rc2dgi_plan_rows": ([ctypes.POINTER(_Config), ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip,
                               ctypes.c_int], ctypes.c_int),
+        "rc2dgi_plan_jfa_exchange": ([ctypes.POINTER(_Config), ctypes.c_int, ctypes.c_int, ip, ip, ctypes.c_int],
+                                     ctypes.c_int),
+        "rc2dgi_plan_jfa_window": ([ctypes.POINTER(_Config), ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ip],
+                                   ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -424,5 +428,35 @@ def plan_rows(W: int, H: int, N: int, blur_radius: float, rank: int, world: int,
     return [(buf[2 * k], buf[2 * k + 1]) for k in range(n)]
 
 
+JFA_INFO = ("m", "hmax", "mg_max", "halo", "sh_minus", "sh_zero", "sh_plus", "mg", "same_block")
+
+
+def plan_jfa_exchange(W: int, H: int, N: int, world: int, step: int, render_scale: float = 1.0):
+    """Host-only JumpFlood exchange plan of row-strip shards for JFA step `step` (>= 1): a dict of
+    JFA_INFO and the transfers [(src, src_window_row, rows, dst, dst_buf, dst_row), ...] in the order
+    every shard issues them (rc2dgi_plan_jfa_exchange)."""
+    L = load_library()
+    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, (ctypes.c_int * 5)())
+    info = (ctypes.c_int * 9)()
+    n = L.rc2dgi_plan_jfa_exchange(ctypes.byref(cfg), world, step, info, None, 0)
+    if n < 0:
+        raise RC2DGIError(n, "rc2dgi_plan_jfa_exchange")
+    buf = (ctypes.c_int * max(6 * n, 1))()
+    L.rc2dgi_plan_jfa_exchange(ctypes.byref(cfg), world, step, info, buf, n)
+    return dict(zip(JFA_INFO, list(info))), [tuple(buf[6 * k:6 * k + 6]) for k in range(n)]
+
+
+def plan_jfa_window(W: int, H: int, N: int, rank: int, world: int, step: int, render_scale: float = 1.0):
+    """Where shard `rank` reads tap y of JFA step `step`: ([buffer per tap], [global row of each
+    buffer's local row 0]) (rc2dgi_plan_jfa_window)."""
+    L = load_library()
+    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, (ctypes.c_int * 5)())
+    buf, row0 = (ctypes.c_int * 3)(), (ctypes.c_int * 3)()
+    rc = L.rc2dgi_plan_jfa_window(ctypes.byref(cfg), rank, world, step, buf, row0)
+    if rc < 0:
+        raise RC2DGIError(rc, "rc2dgi_plan_jfa_window")
+    return list(buf), list(row0)
+
+
 __all__ = ["RC2DGI", "RC2DGIError", "load_library", "abi_version", "RT", "PASS_NAMES", "shard_unique_id", "do_group",
-           "plan_rows", "PLAN_JFA", "PLAN_LEVEL", "PLAN_BLUR", "PLAN_MERGE"]
+           "plan_rows", "plan_jfa_exchange", "plan_jfa_window", "PLAN_JFA", "PLAN_LEVEL", "PLAN_BLUR", "PLAN_MERGE"]

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.rc2dgi_abi_version() == 2
+    assert lib.rc2dgi_abi_version() == 3
 
 
 def _cfg(**kw):

@@ -37,7 +37,7 @@ def _full(R, W, H, N, rr, rs, blur, color, emis):
     ctx.set_shader_value("_BlurRadius", blur)
     ctx.frame(color, emis)
     ctx.sync()
-    out = {k: ctx.download(k) for k in ("color", "temp")}
+    out = {k: ctx.download(k) for k in ("color", "temp", "dist", "jump1", "jump2")}
     ctx.close()
     return out
 
@@ -73,10 +73,13 @@ def test_group_shards_match_whole_frame(R, W, H, N, rr, rs, blur, world, scene):
             c.sync()
         for c in ctxs:
             y0, y1 = c.shard_rows()
-            for k in ("color", "temp"):
+            # the merged strip, the JumpFlood textures' own rows (computed on the strip windows with
+            # the row exchange) and the whole distance field (all-gathered)
+            for k in ("color", "temp", "jump1", "jump2"):
                 got = c.download(k)[y0:y1]
                 mism = np.count_nonzero(got != want[k][y0:y1])
                 assert mism == 0, f"shard {c.shard_rows()} {k}: {mism} values differ"
+            assert np.array_equal(c.download("dist"), want["dist"]), f"shard {c.shard_rows()}: distRT"
     for c in ctxs:
         c.close()
 
@@ -87,6 +90,9 @@ def test_sharded_context_needs_an_exchange(R):
     assert c.shard_rows() == (32, 64)
     with pytest.raises(R.RC2DGIError) as e:
         c.do_rc2dgi()
+    assert e.value.code == -6
+    with pytest.raises(R.RC2DGIError) as e:  # its JumpFlood exchanges rows between the steps
+        c.do_phase(1)
     assert e.value.code == -6
     with pytest.raises(R.RC2DGIError):
         c.set_shard(2, 2)

@@ -33,7 +33,13 @@ CLEAR = np.array([0.0, 0.0, 0.0, 1.0], np.float32)  # ClearBackground(Black)
 class Shard:
     """One shard of one frame on the CPU restatement, following the C-ABI plan.  Rows a pass
     writes are first cleared as the reference's ClearAllRTs / per-pass clears leave them; every
-    other row stays NaN, so reading a row the plan did not compute poisons the result."""
+    other row stays NaN, so reading a row the plan did not compute poisons the result.
+
+    JumpFlood (world >= 2, >= 2 steps): every step computes the own strip of a fresh image
+    from J_{t-1}, of which the shard holds its own rows plus exactly the rows the exchange plan
+    (``rc2dgi_plan_jfa_exchange``) delivers -- every other texel is a seed at its own position,
+    which wins wherever a tap reads it; each transfer's source and destination rows are checked
+    against the window / block layout the plan states."""
 
     def __init__(self, p, color, emis, rank, world):
         self.p, self.rank, self.world = p, rank, world
@@ -41,30 +47,92 @@ class Shard:
         self.emis = np.ascontiguousarray(emis, np.float32)
         self.CW, self.CH, self.S = oracle.dims(p)
         self.y0, self.y1 = _strip(p.H, rank, world)
+        self.exchange = world > 1 and self.S >= 2
 
-    def phase1(self):
+    def _nan(self):
+        return np.full((self.p.H, self.p.W, 4), np.nan, np.float32)
+
+    def _self_seeds(self):
+        """JumpFlood poison: every texel a seed at its own position.  NaN taps lose every JFA
+        comparison silently, so a row the exchange failed to deliver would go unnoticed; a texel
+        that is its own seed is as close as a tap can be and wins wherever it is read."""
+        W, H = self.p.W, self.p.H
+        img = np.zeros((H, W, 4), np.float32)
+        img[..., 0] = ((np.arange(W, dtype=np.float32) + np.float32(0.5)) / np.float32(W))[None, :]
+        img[..., 1] = ((np.arange(H, dtype=np.float32) + np.float32(0.5)) / np.float32(H))[:, None]
+        img[..., 3] = 1.0
+        return img
+
+    def jfa_step(self, t):
+        """JumpFlood step t into a fresh image (RC2DGI.cs:296-326): self.prev (J_{t-1}) -> J_t."""
         p, L = self.p, oracle.lib()
         W, H = p.W, p.H
-        nan = lambda: np.full((H, W, 4), np.nan, np.float32)  # noqa: E731
         mx = max(W, H)
         aspx, aspy = np.float32(W) / np.float32(mx), np.float32(H) / np.float32(mx)
-        j1, j2 = oracle.screen_uv(self.color), nan()  # ScreenUV runs whole on every shard
-        j1final, step = True, np.float32(1.0)
-        for s in range(self.S):
+        step = np.float32(1.0)
+        for _ in range(t + 1):
             step = np.float32(step * np.float32(0.5))
-            src, dst = (j1, j2) if j1final else (j2, j1)
-            for a, b in _rows(p, self.rank, self.world, R.PLAN_JFA + s):
-                if s < 2:  # jumpRT2 / the J0 rows in jumpRT1 are cleared texels before their first step
-                    dst[a:b] = CLEAR
-                L.orc_set_rows(a, b)
-                L.orc_jfa_step(oracle._p(src), oracle._p(dst), W, H, float(step), float(aspx), float(aspy), None)
-            j1final = not j1final
-        self.dist = nan()
+        if t == 0:
+            self.prev = oracle.screen_uv(self.color)  # ScreenUV: every shard computes the mask rows it taps
+        if self.exchange and t >= 1:  # every row the step's taps read was computed or delivered
+            missing = self.tap_rows(t) - self.held
+            assert not missing, f"step {t} shard {self.rank}: rows {sorted(missing)[:8]} never delivered"
+        dst = self._self_seeds() if self.exchange else self._nan()
+        for a, b in _rows(p, self.rank, self.world, R.PLAN_JFA + t):
+            dst[a:b] = CLEAR  # finite texels under the step's blend (alpha 1: their value never shows)
+            L.orc_set_rows(a, b)
+            L.orc_jfa_step(oracle._p(self.prev), oracle._p(dst), W, H, float(step), float(aspx), float(aspy), None)
+        L.orc_set_rows(-1, -1)
+        self.prev = dst
+        self.held = set(range(self.y0, self.y1))
+
+    def tap_rows(self, t):
+        """rows of J_{t-1} the own strip's taps read at step t, as JumpFlood.fs computes them:
+        NEAREST + REPEAT of v + offset (float32; exact integer rows at power-of-two sizes)"""
+        W, H = self.p.W, self.p.H
+        mx = max(W, H)
+        aspx = np.float32(W) / np.float32(mx)
+        step = np.float32(1.0)
+        for _ in range(t + 1):
+            step = np.float32(step * np.float32(0.5))
+        v = (np.arange(self.y0, self.y1, dtype=np.float32) + np.float32(0.5)) / np.float32(H)
+        rows = set()
+        for k in (-1, 0, 1):
+            off = np.float32(np.float32(np.float32(k) * aspx) * step)
+            x = (v + off).astype(np.float32)
+            if H & (H - 1) == 0:
+                r = np.floor(x * np.float32(H)).astype(np.int64) % H
+            else:
+                f = (x - np.floor(x)).astype(np.float32)
+                r = np.minimum(np.floor(f * np.float32(H)).astype(np.int64), H - 1)
+            rows |= set(int(q) for q in r)
+        return rows
+
+    def jfa_window_rows(self, t, buf, local_row):
+        """global row held by local row `local_row` of this shard's buffer `buf` at step t"""
+        p = self.p
+        info, _ = R.plan_jfa_exchange(p.W, p.H, p.N, self.world, t, p.render_scale)
+        if buf == 0:
+            return (self.y0 - info["m"] + local_row) % p.H
+        bufs, row0 = R.plan_jfa_window(p.W, p.H, p.N, self.rank, self.world, t, p.render_scale)
+        return (row0[bufs.index(buf)] + local_row) % p.H
+
+    def phase1(self):
+        for t in range(self.S):
+            self.jfa_step(t)
+            if self.exchange and t + 1 < self.S:
+                raise RuntimeError("a sharded JumpFlood needs the exchange: use run_phase1")
+        return self.finish_phase1()
+
+    def finish_phase1(self):
+        p, L = self.p, oracle.lib()
+        self.dist = self._nan()
         self.dist[self.y0:self.y1] = CLEAR
         L.orc_set_rows(self.y0, self.y1)
-        L.orc_distance_field(oracle._p(j1 if j1final else j2), oracle._p(self.dist), W, H, None)
+        L.orc_distance_field(oracle._p(self.prev), oracle._p(self.dist), p.W, p.H, None)
         L.orc_set_rows(-1, -1)
         return self.dist[self.y0:self.y1].copy()
+
 
     def phase2(self):
         p, L = self.p, oracle.lib()
@@ -107,6 +175,37 @@ class Shard:
         return out[self.y0:self.y1], temp[self.y0:self.y1]
 
 
+def deliver(shards_by_rank, t, xfers, me=None):
+    """Apply the JumpFlood transfers of step t: copy rows of J_{t-1} from their owner into the
+    receiving shard's image at the same global rows, after checking that the plan's source row
+    (owner's window) and destination row (receiver's window / block) denote those global rows.
+    me = None: every shard is local; else only transfers whose both ends are local."""
+    for (src, src_row, rows, dst, dst_buf, dst_row) in xfers:
+        if src not in shards_by_rank or dst not in shards_by_rank:
+            continue
+        a, b = shards_by_rank[src], shards_by_rank[dst]
+        H = a.p.H
+        for k in range(rows):
+            g = a.jfa_window_rows(t, 0, src_row + k)
+            assert a.y0 <= g < a.y1, f"step {t}: row {g} sent by shard {src} is not its own"
+            assert b.jfa_window_rows(t, dst_buf, dst_row + k) == g, f"step {t}: transfer lands on the wrong row"
+            b.prev[g] = a.prev[g] if a is not b else b.prev[g]
+            b.held.add(g)
+        del H
+
+
+def run_phase1(shards):
+    """phase 1 of every (local) shard, in lockstep over the JFA steps with the exchange"""
+    by = {s.rank: s for s in shards}
+    s0 = shards[0]
+    for t in range(s0.S):
+        if t >= 1 and s0.exchange:
+            _, xf = R.plan_jfa_exchange(s0.p.W, s0.p.H, s0.p.N, s0.world, t, s0.p.render_scale)
+            deliver(by, t, xf)
+        for s in shards:
+            s.jfa_step(t)
+    return [s.finish_phase1() for s in shards]
+
 CASES = [
     # W, H, N, rayRange, renderScale, blur, world, scene
     (64, 64, 3, 4.0, 1.0, 1.5, 2, "rand:1"),
@@ -131,7 +230,7 @@ def test_oracle_strips_reproduce_the_frame(W, H, N, rr, rs, blur, world, scene):
     color, emis = _scene(scene, W, H)
     full = oracle.frame(p, color, emis)
     shards = [Shard(p, color, emis, r, world) for r in range(world)]
-    strips = [s.phase1() for s in shards]
+    strips = run_phase1(shards)
     for s in shards:  # the exchange: every distRT strip to every shard
         for q, st in enumerate(strips):
             a, b = _strip(H, q, world)
@@ -151,8 +250,8 @@ def test_plan_shape():
         assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
     S = 10
     assert all(R.plan_rows(W, H, 6, 1.5, 0, 1, R.PLAN_JFA + s) == [(0, H)] for s in range(S))
-    sizes = [sum(b - a for a, b in R.plan_rows(W, H, 6, 1.5, 3, 8, R.PLAN_JFA + s)) for s in range(S)]
-    assert sizes[0] == H and sizes[-1] == H // 8 and sizes == sorted(sizes, reverse=True)
+    # sharded: every JumpFlood step computes the own strip (the exchange delivers the taps' rows)
+    assert all(R.plan_rows(W, H, 6, 1.5, 3, 8, R.PLAN_JFA + s) == [(3 * H // 8, 4 * H // 8)] for s in range(S))
     with pytest.raises(R.RC2DGIError):
         R.plan_rows(W, H, 6, 1.5, 8, 8, R.PLAN_MERGE)
 
@@ -181,7 +280,31 @@ def _worker(rank, world, port, q):
     p = oracle.Params(W=W, H=H, N=N, ray_range=rr, render_scale=rs, blur_radius=blur)
     color, emis = _scene(scene, W, H)
     sh = Shard(p, color, emis, rank, world)
-    mine = sh.phase1()
+    # phase 1 with the JumpFlood exchange as point-to-point messages (the RCCL path's ncclSend /
+    # ncclRecv pattern), every transfer in the plan's order
+    import torch
+
+    for t in range(sh.S):
+        if t >= 1:
+            _, xf = R.plan_jfa_exchange(W, H, N, world, t, rs)
+            reqs, inbox = [], []
+            for tag, (src, src_row, rows, dst, dst_buf, dst_row) in enumerate(xf):
+                if src == rank and dst != rank:
+                    g = [sh.jfa_window_rows(t, 0, src_row + k) for k in range(rows)]
+                    reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(sh.prev[g])), dst, tag=tag))
+                elif dst == rank and src != rank:
+                    buf = torch.empty((rows, W, 4), dtype=torch.float32)
+                    reqs.append(dist.irecv(buf, src, tag=tag))
+                    inbox.append((buf, dst_buf, dst_row, rows))
+            deliver({rank: sh}, t, xf)  # transfers within this shard
+            for r in reqs:
+                r.wait()
+            for buf, dst_buf, dst_row, rows in inbox:
+                g = [sh.jfa_window_rows(t, dst_buf, dst_row + k) for k in range(rows)]
+                sh.prev[g] = buf.numpy()
+                sh.held.update(g)
+        sh.jfa_step(t)
+    mine = sh.finish_phase1()
     strips = [None] * world
     dist.all_gather_object(strips, mine)  # the distRT exchange
     for r, st in enumerate(strips):
@@ -213,3 +336,25 @@ def test_two_ranks_gloo_strips():
     p = oracle.Params(W=W, H=H, N=N, ray_range=rr, render_scale=rs, blur_radius=blur)
     color, emis = _scene(scene, W, H)
     assert np.array_equal(got, oracle.frame(p, color, emis).color_out)
+
+
+def test_missing_exchange_row_is_detected():
+    """An incomplete JumpFlood exchange is caught: dropping one row of one transfer leaves a row
+    the step's taps read undelivered (so the passing cases above are not vacuous)."""
+    W, H, N, world = 256, 256, 5, 8
+    p = oracle.Params(W=W, H=H, N=N, ray_range=3.0)
+    color, emis = scenes.demo(W, H)
+    full = oracle.frame(p, color, emis)
+    shards = [Shard(p, color, emis, r, world) for r in range(world)]
+    by = {s.rank: s for s in shards}
+    with pytest.raises(AssertionError, match="never delivered"):
+        for t in range(shards[0].S):
+            if t >= 1:
+                _, xf = R.plan_jfa_exchange(W, H, N, world, t)
+                if t == 3:  # one row short in the first transfer of this step
+                    src, src_row, rows, dst, dst_buf, dst_row = xf[0]
+                    xf[0] = (src, src_row, rows - 1, dst, dst_buf, dst_row)
+                deliver(by, t, xf)
+            for s in shards:
+                s.jfa_step(t)
+    del full
