@@ -154,6 +154,12 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     probe tiles x groups of dg direction blocks (0: tile-major, the default)
  *   "poison"          debug: fill the intermediate render textures with 0xFF bytes before each
  *                     frame (rows a sharded frame never computes then read as NaN)
+ *   "rc_skip"         march exit proofs from a coarse lower bound of distRT (the last sample of a
+ *                     ray that misses is not read when the bound already proves the miss):
+ *                     0 off, 1 auto (screens >= 2048), 2 interval only, 3 interval + screen edge
+ *   "rc_wgproof"      1 (default): a workgroup whose first samples all provably miss skips the march
+ *   "rc_tail" / "rc_tail_L<n>"  rays still marching after this many lockstep iterations finish one
+ *                     per lane in a compacted queue (0 off; default 6)
  * rc2dgi_get_tuning also answers "rc_variant_count". */
 int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
 /* time `frames` frames per candidate workgroup order x march variant ("rc_variant" 0 / 13 / 14 / 15) on

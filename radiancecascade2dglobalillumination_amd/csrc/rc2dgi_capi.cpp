@@ -136,6 +136,7 @@ struct rc2dgi_ctx {
   hipEvent_t ev_frame = nullptr;    // end of the last group frame (peers copy from our distRT)
   hipEvent_t ev_jfa[2] = {nullptr, nullptr};  // end of the last even / odd JFA step (group exchange)
   bool gi1final = false;            // phase 1 -> phase 2 state
+  bool broken = false;              // a reallocation failed: the device buffers are gone (destroy it)
   std::string err;
 };
 
@@ -152,6 +153,13 @@ int fail(rc2dgi_ctx *c, int code, const std::string &msg) {
   if (c) c->err = msg;
   return code;
 }
+
+// a context whose reallocation failed holds freed / null device buffers: refuse to touch them
+#define RC2DGI_USABLE(ctx)                                                                                   \
+  do {                                                                                                       \
+    if ((ctx)->broken)                                                                                       \
+      return fail((ctx), RC2DGI_E_STATE, "the context lost its render textures (a reallocation failed): destroy it"); \
+  } while (0)
 
 int hip_fail(rc2dgi_ctx *c, hipError_t e, const char *what) {
   std::string m = std::string(what) + ": " + hipGetErrorString(e);
@@ -581,7 +589,10 @@ int rc2dgi_set_uniform_i(rc2dgi_ctx *c, const char *name, int v) {
   HIPCHK(c, hipMemcpy(em.data(), c->emissive, em.size() * sizeof(float4), hipMemcpyDeviceToHost));
   c->sky_override.clear();
   int rc = allocate(c);
-  if (rc != RC2DGI_OK) return rc;
+  if (rc != RC2DGI_OK) {
+    c->broken = true;  // no half-allocated context runs a frame: every later call reports it
+    return rc;
+  }
   for (auto &ev : c->ev_level) (void)hipEventCreate(&ev);
   HIPCHK(c, hipMemcpy(c->color_in, col.data(), col.size() * sizeof(float4), hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->emissive, em.data(), em.size() * sizeof(float4), hipMemcpyHostToDevice));
@@ -590,6 +601,7 @@ int rc2dgi_set_uniform_i(rc2dgi_ctx *c, const char *name, int v) {
 
 int rc2dgi_upload(rc2dgi_ctx *c, int which, const void *host, int pitch_bytes, int format) {
   if (!c || !host) return fail(c, RC2DGI_E_ARG, "null argument");
+  RC2DGI_USABLE(c);
   if (which != RC2DGI_RT_COLOR && which != RC2DGI_RT_EMISSIVE)
     return fail(c, RC2DGI_E_ARG, "only COLOR and EMISSIVE are inputs");
   const int W = c->W, H = c->H;
@@ -626,6 +638,7 @@ int rc2dgi_upload(rc2dgi_ctx *c, int which, const void *host, int pitch_bytes, i
 
 int rc2dgi_paint(rc2dgi_ctx *c, int which, const unsigned char *clear_rgba, const rc2dgi_prim *prims, int n) {
   if (!c) return RC2DGI_E_ARG;
+  RC2DGI_USABLE(c);
   if (which != RC2DGI_RT_COLOR && which != RC2DGI_RT_EMISSIVE)
     return fail(c, RC2DGI_E_ARG, "only COLOR and EMISSIVE are painted");
   if (n < 0 || (n > 0 && !prims)) return fail(c, RC2DGI_E_ARG, "bad primitive list");
@@ -651,6 +664,7 @@ int rc2dgi_paint(rc2dgi_ctx *c, int which, const unsigned char *clear_rgba, cons
 
 int rc2dgi_upload_device(rc2dgi_ctx *c, int which, const void *dev, int pitch_bytes, int format) {
   if (!c || !dev) return fail(c, RC2DGI_E_ARG, "null argument");
+  RC2DGI_USABLE(c);
   if (which != RC2DGI_RT_COLOR && which != RC2DGI_RT_EMISSIVE)
     return fail(c, RC2DGI_E_ARG, "only COLOR and EMISSIVE are inputs");
   const int W = c->W, H = c->H;
@@ -866,16 +880,24 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     bool fused = false;
     BlurTaps bt;
     const bool mrg = c->sd.W == c->CW && c->sd.H == c->CH;
+    // a fused kernel writes the copied-back GI into gi_spare, which then becomes finalGI: only when
+    // every launch of it ran (a refused launch -- shapes it does not take -- falls back before any
+    // launch ran, since the shapes are the same for every row interval)
     if (c->blur_path == 0 && blur_rows_plan(c->cd, c->blur_radius, &bt) >= 0) {
+      bool ok = true;
       for (auto &r : plan.blur.iv)
-        launch_blur_rows(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, c->color_in, c->temp, c->color_out,
-                         c->sd, mrg, st, r.first, r.second);
-      fused = true;
-      merged = mrg;
-    } else if (c->blur_path <= 1 && blur_fused_ok(c->cd, c->blur_radius)) {
+        ok = ok && launch_blur_rows(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, c->color_in, c->temp,
+                                    c->color_out, c->sd, mrg, st, r.first, r.second);
+      if (!ok && plan.blur.iv.size() > 1) return fail(c, RC2DGI_E_HIP, "fixed-tap blur refused a row interval");
+      fused = ok;
+      merged = ok && mrg;
+    }
+    if (!fused && c->blur_path <= 1 && blur_fused_ok(c->cd, c->blur_radius)) {
+      bool ok = true;
       for (auto &r : plan.blur.iv)
-        launch_blur_fused(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, st, r.first, r.second);
-      fused = true;
+        ok = ok && launch_blur_fused(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, st, r.first, r.second);
+      if (!ok && plan.blur.iv.size() > 1) return fail(c, RC2DGI_E_HIP, "LDS-tiled blur refused a row interval");
+      fused = ok;
     }
     if (fused) {
       HIPCHK(c, hipGetLastError());
@@ -907,6 +929,7 @@ void dist_strip(const rc2dgi_ctx *c, int q, unsigned short **p, size_t *bytes) {
 
 int rc2dgi_do(rc2dgi_ctx *c) {
   if (!c) return RC2DGI_E_ARG;
+  RC2DGI_USABLE(c);
   if (c->world > 1 && !c->comm)
     return fail(c, RC2DGI_E_STATE, "sharded context: use rc2dgi_shard_connect, rc2dgi_do_group or rc2dgi_do_phase");
   const FramePlan plan = make_plan(c);
@@ -930,6 +953,7 @@ int rc2dgi_do(rc2dgi_ctx *c) {
 
 int rc2dgi_do_phase(rc2dgi_ctx *c, int phase) {
   if (!c) return RC2DGI_E_ARG;
+  RC2DGI_USABLE(c);
   if (phase != 1 && phase != 2) return fail(c, RC2DGI_E_ARG, "phase is 1 or 2");
   if (phase == 1 && c->strip)
     return fail(c, RC2DGI_E_STATE,
@@ -941,6 +965,7 @@ int rc2dgi_do_phase(rc2dgi_ctx *c, int phase) {
 
 int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   if (!c) return RC2DGI_E_ARG;
+  RC2DGI_USABLE(c);
   if (c->world > 1) return fail(c, RC2DGI_E_STATE, "autotune an unsharded context (the orders carry over)");
   if (frames < 1) frames = 1;
   const bool timing = c->timing;
@@ -989,6 +1014,7 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
   if (!cs || n < 1) return RC2DGI_E_ARG;
   for (int k = 0; k < n; ++k) {
     if (!cs[k]) return RC2DGI_E_ARG;
+    RC2DGI_USABLE(cs[k]);
     const rc2dgi_ctx *c = cs[k];
     if (c->rank != k || c->world != n || c->W != cs[0]->W || c->H != cs[0]->H || c->N != cs[0]->N ||
         c->CW != cs[0]->CW || c->CH != cs[0]->CH)
@@ -1072,7 +1098,9 @@ int rc2dgi_set_shard(rc2dgi_ctx *c, int rank, int world) {
   c->frame_done = c->have_frame = false;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  return jfa_buffers(c);  // strip windows (world > 1) or full-size jumpRT1 / jumpRT2
+  const int rc = jfa_buffers(c);  // strip windows (world > 1) or full-size jumpRT1 / jumpRT2
+  if (rc != RC2DGI_OK) c->broken = true;
+  return rc;
 }
 
 int rc2dgi_shard_rows(rc2dgi_ctx *c, int *y0, int *y1) {
@@ -1112,6 +1140,7 @@ int rc2dgi_shard_connect(rc2dgi_ctx *c, const void *id, int nbytes) {
 
 int rc2dgi_device_buffer(rc2dgi_ctx *c, int which, void **dev, int *pitch_bytes) {
   if (!c || !dev || !pitch_bytes) return RC2DGI_E_ARG;
+  RC2DGI_USABLE(c);
   if (which == RC2DGI_RT_FINAL_GI) which = c->final_gi == 2 ? RC2DGI_RT_GI2 : RC2DGI_RT_GI1;
   const int sp = c->sd.pitch, cp = c->cd.pitch;
   switch (which) {
@@ -1217,6 +1246,7 @@ int rc2dgi_set_timing(rc2dgi_ctx *c, int enable) {
 
 int rc2dgi_pass_times(rc2dgi_ctx *c, float *pass_ms, int n_pass, float *level_ms, int n_level) {
   if (!c) return RC2DGI_E_ARG;
+  RC2DGI_USABLE(c);
   if (!c->timing || !c->have_frame) return fail(c, RC2DGI_E_STATE, "enable timing and run a frame first");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipEventSynchronize(c->ev[5]));
@@ -1377,6 +1407,7 @@ int rc2dgi_set_keep_levels(rc2dgi_ctx *c, int enable) {
 
 int rc2dgi_download_level(rc2dgi_ctx *c, int level, void *host, int pitch_bytes, int format) {
   if (!c || !host) return fail(c, RC2DGI_E_ARG, "null argument");
+  RC2DGI_USABLE(c);
   if (!c->keep_levels || !c->have_frame) return fail(c, RC2DGI_E_STATE, "enable keep_levels and run a frame first");
   if (level < 0 || level >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
   if (format != RC2DGI_FMT_RGBA32F) return fail(c, RC2DGI_E_UNSUPPORTED, "levels download as RGBA32F");
@@ -1400,6 +1431,7 @@ int rc2dgi_download_level(rc2dgi_ctx *c, int level, void *host, int pitch_bytes,
 
 int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int format) {
   if (!c || !host) return fail(c, RC2DGI_E_ARG, "null argument");
+  RC2DGI_USABLE(c);
   if (which == RC2DGI_RT_FINAL_GI) which = (c->N % 2 == 0) ? RC2DGI_RT_GI2 : RC2DGI_RT_GI1;
   if (which < RC2DGI_RT_COLOR || which > RC2DGI_RT_BLUR) return fail(c, RC2DGI_E_ARG, "bad render texture id");
   if (format != RC2DGI_FMT_RGBA32F && format != RC2DGI_FMT_RGBA8) return fail(c, RC2DGI_E_ARG, "bad format");

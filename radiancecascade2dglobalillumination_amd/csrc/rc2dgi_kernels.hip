@@ -785,34 +785,6 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
   return hipGetLastError();
 }
 
-// Integer taps for k_jfa_p2: power-of-two W, H <= 16384 (the no-seed value must stay at least
-// max(W,H) away), and every fragTexCoord + offset exactly representable: (i + 0.5) / n has its
-// lowest bit at 2^-(log2 n + 1) and a nonzero offset is a power of two 2^-m (aspect ratio and step
-// size are powers of two), so the sum, below 2 in magnitude, is exact when both exponents are
-// within 23 bits.
-bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp) {
-  if (!(s.powW && s.powH) || s.W > 16384 || s.H > 16384) return false;
-  auto axis = [](int n, const float off[3], int out[3]) {
-    const int q = __builtin_ctz((unsigned)n);
-    if (q + 1 > 23) return false;
-    for (int k = 0; k < 3; ++k) {
-      if (off[k] != 0.0f) {
-        int e;
-        const float m = frexpf(fabsf(off[k]), &e);  // |off| = m * 2^e
-        if (m != 0.5f || 1 - e > 23) return false;
-      }
-      out[k] = (int)floorf(0.5f + off[k] * (float)n);  // exact: off * n is a power of two or 0
-    }
-    return true;
-  };
-  if (!axis(s.W, off_x, tp->dx) || !axis(s.H, off_y, tp->dy)) return false;
-  const int mx = s.W > s.H ? s.W : s.H;
-  tp->scx = (float)(mx / s.W);
-  tp->scy = (float)(mx / s.H);
-  tp->dinit = (float)mx * (float)mx;
-  return true;
-}
-
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0,
                            int row1, const JfaSrc *window, int dst_row0) {

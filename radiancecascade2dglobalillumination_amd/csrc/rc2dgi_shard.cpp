@@ -65,6 +65,35 @@ bool RowSet::contains(int r) const {
   return false;
 }
 
+// Integer taps for k_jfa_p2: power-of-two W, H <= 16384 (the no-seed value must stay at least
+// max(W,H) away), and every fragTexCoord + offset exactly representable: (i + 0.5) / n has its
+// lowest bit at 2^-(log2 n + 1) and a nonzero offset is a power of two 2^-m (aspect ratio and step
+// size are powers of two), so the sum, below 2 in magnitude, is exact when both exponents are
+// within 23 bits.
+// (host code; also used by launch_jfa_step)
+bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp) {
+  if (!(s.powW && s.powH) || s.W > 16384 || s.H > 16384) return false;
+  auto axis = [](int n, const float off[3], int out[3]) {
+    const int q = __builtin_ctz((unsigned)n);
+    if (q + 1 > 23) return false;
+    for (int k = 0; k < 3; ++k) {
+      if (off[k] != 0.0f) {
+        int e;
+        const float m = frexpf(fabsf(off[k]), &e);  // |off| = m * 2^e
+        if (m != 0.5f || 1 - e > 23) return false;
+      }
+      out[k] = (int)floorf(0.5f + off[k] * (float)n);  // exact: off * n is a power of two or 0
+    }
+    return true;
+  };
+  if (!axis(s.W, off_x, tp->dx) || !axis(s.H, off_y, tp->dy)) return false;
+  const int mx = s.W > s.H ? s.W : s.H;
+  tp->scx = (float)(mx / s.W);
+  tp->scy = (float)(mx / s.H);
+  tp->dinit = (float)mx * (float)mx;
+  return true;
+}
+
 void jfa_offsets(int W, int H, int step, float ox[3], float oy[3]) {
   const int mx = W > H ? W : H;
   const float aspx = (float)W / (float)mx, aspy = (float)H / (float)mx;  // RC2DGI.cs:273
@@ -212,8 +241,9 @@ JfaExchange plan_jfa_exchange(int W, int H, int S, int world) {
     jfa_tap_rows(W, H, t, st.sh, st.mg);
     const int s = std::max(std::abs(st.sh[0]), std::abs(st.sh[2]));
     st.halo = s + st.mg < hmin;
-    if (st.halo) x.m = std::max(x.m, s + st.mg);
-    else x.mg_max = std::max(x.mg_max, st.mg);
+    // a halo step reads s + mg rows beyond the strip; a block step's unshifted tap its mg rows
+    x.m = std::max(x.m, st.halo ? s + st.mg : st.mg);
+    if (!st.halo) x.mg_max = std::max(x.mg_max, st.mg);
     st.same_block = !st.halo && mod((long)st.sh[2] - st.sh[0], H) == 0;
   }
   for (int t = 1; t < S; ++t) {
@@ -231,8 +261,12 @@ JfaExchange plan_jfa_exchange(int W, int H, int S, int world) {
           need.push_back({(long)y1, e, 0, x.m + (y1 - y0)});
         }
       } else {
-        need.push_back({(long)y0 + st.sh[0] - st.mg, (y1 - y0) + 2 * st.mg, 1, 0});
-        if (!st.same_block) need.push_back({(long)y0 + st.sh[2] - st.mg, (y1 - y0) + 2 * st.mg, 2, 0});
+        if (st.mg > 0) {  // the unshifted tap's rounding rows, into the window's halo
+          need.push_back({(long)y0 - st.mg, st.mg, 0, x.m - st.mg});
+          need.push_back({(long)y1, st.mg, 0, x.m + (y1 - y0)});
+        }
+        if (st.sh[0] != 0) need.push_back({(long)y0 + st.sh[0] - st.mg, (y1 - y0) + 2 * st.mg, 1, 0});
+        if (st.sh[2] != 0 && !st.same_block) need.push_back({(long)y0 + st.sh[2] - st.mg, (y1 - y0) + 2 * st.mg, 2, 0});
       }
       for (const Need &nd : need) {
         int done = 0;
