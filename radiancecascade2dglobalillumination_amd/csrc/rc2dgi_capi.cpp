@@ -124,6 +124,7 @@ struct rc2dgi_ctx {
                                  // only, 3 interval and screen edge
   std::vector<int> rc_tail;      // per level: tail compaction after this many lockstep iterations (tuning rc_tail_L<n>)
   int rc_wgproof = 1;            // tuning "rc_wgproof": workgroup-wide exit proof of the first samples
+  int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
@@ -704,7 +705,7 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
     const unsigned *src = t == 0 ? c->occ : jfa_out(c, t - 1);
     for (auto &r : plan.jfa[t].iv)
       HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, jfa_out(c, t), dist, c->sd, ox, oy, st,
-                                r.first, r.second));
+                                r.first, r.second, nullptr, 0, c->jfa_lds));
     return RC2DGI_OK;
   }
   // row-strip shard: the own strip, into its window (global row y0 - m = local row 0)
@@ -1327,6 +1328,10 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_wgproof = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "jfa_lds") {
+    c->jfa_lds = value != 0;
+    return RC2DGI_OK;
+  }
   if (k == "rc_tail" || k.rfind("rc_tail_L", 0) == 0) {
     if (value < 0 || value > 32) return fail(c, RC2DGI_E_ARG, "rc_tail is 0 (off) .. 32 lockstep iterations");
     if (k == "rc_tail") {
@@ -1375,6 +1380,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "rc_wgproof") {
     *value = c->rc_wgproof;
+    return RC2DGI_OK;
+  }
+  if (k == "jfa_lds") {
+    *value = c->jfa_lds;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_tail_L", 0) == 0) {

@@ -57,7 +57,8 @@ struct JfaSrc {
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0 = 0,
                            int row1 = -1,  // output rows [row0, row1) (-1 = H)
-                           const JfaSrc *window = nullptr, int dst_row0 = 0);
+                           const JfaSrc *window = nullptr, int dst_row0 = 0,
+                           int lds = 0);  // LDS-staged taps for short power-of-two steps (tuning jfa_lds)
 // integer taps of the power-of-two JFA kernel (false: the float path runs); also used by the
 // row-strip planner
 bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp);

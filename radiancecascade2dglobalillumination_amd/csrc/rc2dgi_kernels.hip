@@ -197,7 +197,11 @@ __host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
 
 // U8: RGBA8 jumpRT (quantized seed uv, pack_seed_u8): the same integer taps, the float distance of
 // k_jfa_step's U8 path (the seed's uv is k * (1/255), not its texel centre).
-template <bool FIRST, bool IKEY, bool U8 = false>
+// LDS: a short step (offset s <= 8 texels on both axes): the workgroup stages its 64 x 16 tile and
+// an s-texel ring of the previous step in LDS (each texel loaded once, rows wrapped), then reads the
+// 9 taps of every texel from LDS (tuning "jfa_lds"; same seeds, same bits).
+constexpr int kJfaLdsMax = 8;
+template <bool FIRST, bool IKEY, bool U8 = false, bool LDS = false>
 __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src, int src_pitch,
                                                 unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                 ScreenDims s, JfaTaps o, int row0, int row1, int lattice,
@@ -226,6 +230,40 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
   unsigned qx[3];  // U8 first step: the quantized u of each tap column (pack_seed_u8's low half)
 #pragma unroll
   for (int x = 0; x < 3; ++x) qx[x] = (FIRST && U8) ? pack_seed_u8((int)ti[x], 0, Axis{s.W, 1}, Axis{s.H, 1}) & 0xFFFFu : 0u;
+  if constexpr (LDS && !FIRST) {
+    constexpr int TWM = 64 + 2 * kJfaLdsMax, THM = 4 * JT + 2 * kJfaLdsMax;
+    __shared__ unsigned tile[THM * TWM];
+    const int sh = o.dy[2], TW = 64 + 2 * sh, TH = 4 * JT + 2 * sh;  // host: dx[2] == dy[2] = sh <= 8
+    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
+    const int jb = row0 + by * (4 * JT) - sh, ib = bx * 64 - sh;
+    // wave w stages rows w, w + 4, ...; a lane two columns; every load issued before the first store
+    constexpr int RPW = THM / 4;
+    unsigned va[RPW], vb[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int r = min(wv + 4 * q, TH - 1);
+      const unsigned *row = src + (size_t)((unsigned)(jb + r) & (unsigned)(s.H - 1)) * src_pitch;
+      va[q] = row[(unsigned)(ib + lane) & (unsigned)(s.W - 1)];
+      vb[q] = row[(unsigned)(ib + 64 + min(lane, TW - 65)) & (unsigned)(s.W - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int r = wv + 4 * q;
+      if (r < TH) {
+        tile[r * TWM + lane] = va[q];
+        if (lane < TW - 64) tile[r * TWM + 64 + lane] = vb[q];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const int rl = wv + 4 * t + sh;  // the texel's tile row (clamped rows are computed, not stored)
+#pragma unroll
+      for (int y = 0; y < 3; ++y)
+#pragma unroll
+        for (int x = 0; x < 3; ++x) seed[t][y * 3 + x] = tile[(rl + o.dy[y]) * TWM + lane + sh + o.dx[x]];
+    }
+  } else {
 #pragma unroll
   for (int t = 0; t < JT; ++t) {
     const int j = min(j0 + 4 * t, row1 - 1);  // clamped rows are computed but not stored
@@ -250,6 +288,7 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
         }
       }
     }
+  }
   }
   typedef short v2s __attribute__((ext_vector_type(2)));
 #pragma unroll
@@ -787,7 +826,7 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
 
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0,
-                           int row1, const JfaSrc *window, int dst_row0) {
+                           int row1, const JfaSrc *window, int dst_row0, int lds) {
   JfaSrc win{};
   if (window && !first) win = *window;
   if (row1 < 0 || row1 > s.H) row1 = s.H;
@@ -820,6 +859,15 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     else
       hipLaunchKernelGGL((k_jfa_step<false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
                          row1, win, dst_row0);
+  } else if (p2 && lds && !first && !win.on && tp.dx[2] == tp.dy[2] && tp.dy[2] >= 1 && tp.dy[2] <= kJfaLdsMax &&
+             (row1 - row0) % (4 * JT) == 0 && s.W % 64 == 0) {
+    const bool ikey = s.W == s.H && s.W <= 4096;
+    if (ikey)
+      hipLaunchKernelGGL((k_jfa_p2<false, true, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp,
+                         row0, row1, 0, win, dst_row0);
+    else
+      hipLaunchKernelGGL((k_jfa_p2<false, false, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s,
+                         tp, row0, row1, 0, win, dst_row0);
   } else if (p2) {
     const bool ikey = s.W == s.H && s.W <= 4096;
 #define RC2DGI_JFA(F, K)                                                                                      \

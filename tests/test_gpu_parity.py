@@ -492,3 +492,24 @@ def test_exit_proofs_and_tail_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene):
                 assert np.array_equal(g, fr.gi_levels[L]), \
                     f"variant {v} rc_skip {skip} rc_tail {tail} level {L}: {np.count_nonzero(g != fr.gi_levels[L])}"
     ctx.close()
+
+
+@pytest.mark.parametrize("W,H,N,storage", [(256, 256, 4, "f32"), (1024, 1024, 5, "f32"), (512, 512, 4, "rgba8"),
+                                           (512, 256, 4, "f32"), (4096, 4096, 6, "f32")])
+def test_jfa_lds_staging_is_bit_identical(RC2DGI, W, H, N, storage):
+    """The LDS-staged taps of the short JumpFlood steps (tuning jfa_lds) load the same seeds: every
+    JFA output and the distance field are unchanged (non-square screens keep the plain kernel)."""
+    color, emis = make_scene("demo", W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for lds in (0, 1):
+        ctx.set_tuning("jfa_lds", lds)
+        assert ctx.get_tuning("jfa_lds") == lds
+        ctx.do_rc2dgi()
+        ctx.sync()
+        out[lds] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
+    for k in out[0]:
+        assert np.array_equal(out[0][k], out[1][k]), f"{k}: {np.count_nonzero(out[0][k] != out[1][k])}"
+    ctx.close()
