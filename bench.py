@@ -109,6 +109,26 @@ def gather_roofline(rec, N, level_ms):
             "source": "profiles/rc_level_pmc.json (TCC_HIT+TCC_MISS per launch), profiles/r01/gather_ceiling.txt"}
 
 
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 VALU instruction occupies a 16-lane SIMD 4 cycles
+# (MI355X_MICROARCH.md), at the 2.4 GHz peak engine clock
+VALU_PEAK_GINSTS = 256 * 4 * 2.4 / 4.0
+
+
+def valu_roofline(rec, N, level_ms):
+    """The RC pass against the VALU issue rate: wave instructions per frame
+    (PMC SQ_INSTS_VALU per level launch from the committed profile) over this run's level times."""
+    lv = rec.get("per_level", {})
+    ins = [lv.get(f"k_rc_level L{L}", {}).get("valu_insts") for L in range(N)]
+    if any(x is None for x in ins):
+        return None
+    t = sum(level_ms) / 1e3
+    achieved = sum(ins) / t / 1e9
+    return {"kernel": "k_rc_level (all levels)", "achieved": round(achieved, 1), "peak": round(VALU_PEAK_GINSTS, 1),
+            "unit": "G VALU wave-instructions/s", "frac": round(achieved / VALU_PEAK_GINSTS, 4),
+            "floor_ms": round(sum(ins) / VALU_PEAK_GINSTS / 1e6, 4),
+            "source": "profiles/rc_level_pmc.json (SQ_INSTS_VALU per launch)"}
+
+
 def input_costs(ctx, W, H, color, emis, reps=5):
     """Per-frame cost of producing the painted inputs (outside the timed frames): painting the
     demo scene on the device (rc2dgi_paint) vs uploading both textures from host
@@ -432,7 +452,7 @@ def main():
     bytes_launch = b_rc(W, H, CW, CH, N, {"f32": 16, "f16": 8, "rgba8": 4}[a.storage]) / N
     avg_launch_s = (t_rc / 1e3) / (a.steps * N)
     achieved = bytes_launch / avg_launch_s / 1e9
-    traffic, gather = None, None
+    traffic, gather, valu = None, None, None
     pmc = os.path.join(ROOT, "profiles", "rc_level_pmc.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
@@ -440,6 +460,7 @@ def main():
         if rec.get("config") == f"{W}x{H}_N{N}" and a.storage == "f32":
             traffic = rec.get("hbm_bytes_per_launch")
             gather = gather_roofline(rec, N, lvl_ms / a.steps)
+            valu = valu_roofline(rec, N, lvl_ms / a.steps)
     line = {
         "metric": (f"Mpixel*cascades/s (RC pass) at {W}^2, cascadeCount={N}" if W == H else
                    f"Mpixel*cascades/s (RC pass) at {W}x{H}, cascadeCount={N}"),
@@ -473,6 +494,8 @@ def main():
     }
     if gather:
         line["gather_roofline"] = gather
+    if valu:
+        line["valu_roofline"] = valu
     line["inputs"] = input_costs(ctx, W, H, color, emis)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the CPU leg: rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(W, H, N, a.ray_range, a.cpu_budget)

@@ -93,6 +93,7 @@ def main():
                                  "l2_requests": (v["TCC_HIT_sum"] + v["TCC_MISS_sum"]) if "TCC_HIT_sum" in v else None,
                                  "l2_hit": (v["TCC_HIT_sum"] / max(v["TCC_HIT_sum"] + v["TCC_MISS_sum"], 1))
                                  if "TCC_HIT_sum" in v else None,
+                                 "valu_insts": v.get("SQ_INSTS_VALU"),
                                  "dur_us": v["_dur_ns"] / 1e3} for k, v in lv.items()}}
         if all(x is not None for x in fetch + write) and lv:
             rec["hbm_bytes_per_launch"] = sum(2 * f * 1024 + w * 1024 for f, w in zip(fetch, write)) / len(lv)

@@ -2,7 +2,8 @@
 # Round-end evidence on one GPU, for the schedule the bench times (the committed per-config
 # schedule in radiancecascade2dglobalillumination_amd/tuning/, or TUNE=1: autotune and save it):
 #   1. rocprofv3 --kernel-trace --stats of the bench;
-#   2. PMC FETCH/WRITE/TCC passes of the same -> profiles/rc_level_pmc.json (HBM traffic per launch);
+#   2. PMC FETCH/WRITE/TCC/SQ_INSTS_VALU passes of the same -> profiles/rc_level_pmc.json (HBM traffic and
+#      VALU wave instructions per launch);
 #   3. the final bench line (with cpu_baseline), reading the fresh traffic;
 #   4. optional batch-mode line (BATCH=<scenes per GPU>).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -20,7 +21,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   -- python3 bench.py --no-cpu-baseline $SCHED > gpurun_out/prof.log 2>&1 || exit $?
 tail -1 gpurun_out/prof.log | cut -c1-200
 echo "== pmc"
-GROUPS_OVERRIDE="FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum" STEPS=5 BENCH_ARGS="$SCHED" \
+GROUPS_OVERRIDE="FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;SQ_INSTS_VALU SQ_WAVES" STEPS=5 BENCH_ARGS="$SCHED" \
   bash scripts/profile_pmc.sh || exit $?
 python3 scripts/pmc_summary.py gpurun_out/pmc --json gpurun_out/rc_level_pmc.json > gpurun_out/pmc_summary.txt
 cut -c1-160 gpurun_out/pmc_summary.txt

@@ -51,3 +51,12 @@ def test_committed_pmc_record_has_the_gather_fields():
     for L in range(6):
         lv = rec["per_level"][f"k_rc_level L{L}"]
         assert lv["l2_requests"] > 0 and 0.0 < lv["l2_hit"] < 1.0 and lv["dur_us"] > 0
+
+
+def test_valu_roofline_is_issue_time_over_level_time(bench):
+    """valu_roofline: wave instructions per frame over the level times, against 256 CUs x 4 SIMDs at
+    one wave64 instruction per 4 cycles."""
+    rec = {"per_level": {f"k_rc_level L{L}": {"valu_insts": 614.4e6 / 4} for L in range(4)}}
+    v = bench.valu_roofline(rec, 4, [0.25] * 4)  # 614.4 M instructions in 1 ms
+    assert abs(v["achieved"] - 614.4) < 0.1 and abs(v["frac"] - 1.0) < 1e-3 and abs(v["floor_ms"] - 1.0) < 1e-3
+    assert bench.valu_roofline({"per_level": {}}, 4, [0.1] * 4) is None
