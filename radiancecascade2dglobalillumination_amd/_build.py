@@ -91,6 +91,10 @@ if __name__ == "__main__":
         # join (WRONG, run-to-run different results on gfx950).  Extra flags after the mode are passed on.
         print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_ESC_PLAIN"] + sys.argv[2:],
                     out=os.path.join(ROOT, "build", "diag", "librc2dgi_escplain.so")))
+    elif len(sys.argv) > 2 and sys.argv[1] == "exp":
+        # A/B build of an experiment: build/ab/librc2dgi_<name>.so with the flags given (scripts/ab_lib.sh)
+        print(build(force=True, verbose=True, extra=sys.argv[3:],
+                    out=os.path.join(ROOT, "build", "ab", f"librc2dgi_{sys.argv[2]}.so")))
     elif len(sys.argv) > 1 and sys.argv[1] == "stats":
         # diagnostic build: march statistics per level (rc2dgi_diag_stats; atomics, slower)
         print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_STATS"], out=os.path.join(ROOT, "build", "diag", "librc2dgi_stats.so")))

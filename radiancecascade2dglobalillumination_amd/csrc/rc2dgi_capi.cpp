@@ -106,6 +106,7 @@ struct rc2dgi_ctx {
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
+  float4 *dexit = nullptr;  // screen-exit terms of dirs (rc_exit_terms), same layout
   float4 *sky = nullptr;
   // state
   bool tables_dirty = true;
@@ -209,7 +210,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
-                  c->cmin};
+                  c->cmin,     c->dexit};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -226,6 +227,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->cmin = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
+  c->dexit = nullptr;
   c->sky = nullptr;
 }
 
@@ -322,6 +324,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->gi_spare, nc * gsz));
   HIPCHK(c, alloc(&c->dirs, dir_table_len(c->N) * sizeof(float2)));
+  HIPCHK(c, alloc(&c->dexit, dir_table_len(c->N) * sizeof(float4)));
   HIPCHK(c, alloc(&c->sky, ((size_t)4 << (2 * (c->N - 1))) * sizeof(float4)));
   // initial contents: ClearAllRTs (RC2DGI.cs:109) -> (0,0,0,1) is implied by the frame
   // itself; zero everything so never-written texels (cascadeBlurRT with blur off) read as a
@@ -348,7 +351,8 @@ int allocate(rc2dgi_ctx *c) {
 }
 
 // correctly rounded tables for RadianceCascades.fs:117-121 and :48-57/:150-154
-void build_tables(const rc2dgi_ctx *c, std::vector<float2> &dirs, std::vector<float4> &sky) {
+void build_tables(const rc2dgi_ctx *c, std::vector<float2> &dirs, std::vector<float4> &dexit,
+                  std::vector<float4> &sky) {
   dirs.resize(dir_table_len(c->N));
   for (int L = 0; L < c->N; ++L) {
     const int b = 1 << L, n = 4 * b * b;
@@ -362,6 +366,14 @@ void build_tables(const rc2dgi_ctx *c, std::vector<float2> &dirs, std::vector<fl
       const float angle = ((float)a + 0.5f) * angleStep;
       dirs[off + a] = make_float2((float)std::cos((double)angle), (float)std::sin((double)angle));
     }
+  }
+  float aspx, aspy;
+  rc_aspect(c->W, c->H, aspx, aspy);
+  dexit.resize(dirs.size());
+  for (size_t i = 0; i < dirs.size(); ++i) {
+    float e[4];
+    rc_exit_terms(dirs[i].x, dirs[i].y, aspx, aspy, e);
+    dexit[i] = make_float4(e[0], e[1], e[2], e[3]);
   }
   const int b = 1 << (c->N - 1), n = 4 * b * b;
   sky.resize(n);
@@ -395,9 +407,10 @@ void build_tables(const rc2dgi_ctx *c, std::vector<float2> &dirs, std::vector<fl
 int upload_tables(rc2dgi_ctx *c) {
   if (!c->tables_dirty) return RC2DGI_OK;
   std::vector<float2> dirs;
-  std::vector<float4> sky;
-  build_tables(c, dirs, sky);
+  std::vector<float4> dexit, sky;
+  build_tables(c, dirs, dexit, sky);
   HIPCHK(c, hipMemcpyAsync(c->dirs, dirs.data(), dirs.size() * sizeof(float2), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->dexit, dexit.data(), dexit.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->sky, sky.data(), sky.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   // the host vectors die here: make the pageable copies complete first
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -840,6 +853,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.dist = c->dist;
     a.shade = c->shade;
     a.dirs = c->dirs + dir_table_offset(L);
+    a.dexit = c->dexit + dir_table_offset(L);
     a.sky = c->sky;
     a.level = L;
     a.N = c->N;

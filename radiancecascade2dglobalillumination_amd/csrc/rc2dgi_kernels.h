@@ -81,6 +81,7 @@ struct RcLevelArgs {
   const unsigned short *dist;  // 16-bit distance q (screen)
   const float4 *shade;   // surface records of the hittable texels (launch_shade)
   const float2 *dirs;    // 4^(L+1) (cos, sin)
+  const float4 *dexit = nullptr;  // 4^(L+1) screen-exit terms of the directions (rc_exit_terms), with cmin
   const float4 *sky;     // 4^N sky terms (top level)
   int level, N;
   float ray_range, reflectivity;
@@ -132,6 +133,30 @@ hipError_t launch_shade(const unsigned short *dist, const float4 *color, const f
                         ScreenDims s, float reflectivity, hipStream_t st);
 
 // CalculateRayRange's end of level L (RadianceCascades.fs:38-46), as k_rc_level computes it
+// _Aspect (RC2DGI.cs:273): screen size over its larger side
+inline void rc_aspect(int W, int H, float &aspx, float &aspy) {
+  const int mx = W > H ? W : H;
+  aspx = (float)W / (float)mx;
+  aspy = (float)H / (float)mx;
+}
+
+// Screen-exit terms of one ray direction (dx, dy) for the exit proof of k_rc_level: {ix, iy, ex,
+// ey} such that T = min((ex - ox) * ix, (ey - oy) * iy) is, for any origin o in (0, 1)^2, a t whose
+// sample position o + (t d) asp lies off screen (then every t >= T does: each coordinate is
+// monotone in t).  ex is the line 2^-19 outside the edge the ray heads for and ix = 1 / (dx aspy),
+// each rounded once (u = 2^-24): T carries a relative error below 4u, the position's offset
+// (T dx) aspy then below 6u of |ex - ox| <= 1 + 2^-19, and the final add u -- under 2^-21 in all,
+// a quarter of the margin.  A component too small for that (|v| < 2^-100, denormal products lose the
+// relative bound) never exits: ix = +inf with ex = 2 gives T = +inf.
+inline void rc_exit_terms(float dx, float dy, float aspx, float aspy, float out[4]) {
+  const float v[2] = {dx * aspy, dy * aspx};
+  for (int a = 0; a < 2; ++a) {
+    const bool dead = !(v[a] > 0x1p-100f || v[a] < -0x1p-100f);
+    out[a] = dead ? __builtin_inff() : 1.0f / v[a];
+    out[2 + a] = dead ? 2.0f : (v[a] > 0.0f ? 1.0f + 0x1p-19f : -0x1p-19f);
+  }
+}
+
 inline float rc_ray_end(int level, int N, float ray_range) {
   return ((float)((1 << (level * 2 + 2)) - 1) / (float)((1 << (N * 2)) - 1)) * ray_range;
 }

@@ -1022,9 +1022,7 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.bdxf = P.CRx / (float)P.bsc;  // blockDim = _CascadeResolution / float(blockSqrtCount)
   P.bdyf = P.CRy / (float)P.bsc;
   P.bs2 = (float)(P.bsc * 2);
-  const int mx = s.W > s.H ? s.W : s.H;
-  P.aspx = (float)s.W / (float)mx;  // RC2DGI.cs:273
-  P.aspy = (float)s.H / (float)mx;
+  rc_aspect(s.W, s.H, P.aspx, P.aspy);  // RC2DGI.cs:273
   // CalculateRayRange (RadianceCascades.fs:38-46)
   const int maxValue = (1 << (a.N * 2)) - 1;
   const int start = (1 << (a.level * 2)) - 1;

@@ -26,6 +26,7 @@ struct RcParams {
   const uint2 *wg_map;  // workgroup -> (tile x | y << 16, direction group), host-built (XCD remap + order)
   int tpr;              // 8x8 tiles per row of the tiled distance field (TILED)
   const float4 *cmin;   // coarse lower bound of the field (kCminDim^2 floats as float4), nullptr: off
+  const float4 *dexit;  // screen-exit terms per direction of the level (rc_exit_terms)
   int csh;              // its cells are 2^csh texels square
   int cscr;             // the exit proof tests the screen edge too
   int tailk;            // tail compaction after this many lockstep iterations (0: off)
@@ -139,6 +140,15 @@ template <bool P2S>
 __device__ __forceinline__ bool on_screen(float px, float py) {
   if constexpr (P2S) return __float_as_uint(px) <= 0x3f800000u && __float_as_uint(py) <= 0x3f800000u;
   return !(px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+}
+
+// Exit bound of one ray for the exit proof (k_rc_level): a te with t + dl >= te proving that the
+// sample at t ends its ray (dl > 0 a lower bound of its distance, see s_cm).  t1n = the successor
+// of t1, so tl >= t1n <=> tl > t1.  With scr, also the screen exit T of the direction's terms e
+// (rc_exit_terms: every t >= T samples off screen).  A live sample has t < te (t <= t1 and on
+// screen), so dl = 0 never proves anything.
+__device__ __forceinline__ float exit_bound(float t1n, bool scr, float4 e, float ox, float oy) {
+  return scr ? fminf(t1n, fminf((e.z - ox) * e.x, (e.w - oy) * e.y)) : t1n;
 }
 
 // floor(x) as an int in one instruction (x finite, within int range)
@@ -504,6 +514,17 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     diag_slots += NR;
 #endif
   }
+  // exit bounds of the rays (exit_bound): the proof of a sample is then one add and one compare
+  const float t1n = __uint_as_float(__float_as_uint(P.t1) + 1u);  // t1 >= 0
+  // (per ray in the one-probe-per-lane tiles; the many-ray tiles have no registers to spare for
+  // them and test the screen at t + dl instead)
+  float tend[TLC ? NR : 1];
+  if constexpr (TLC) {
+    if (cm) {
+#pragma unroll
+      for (int k = 0; k < NR; ++k) tend[k] = exit_bound(t1n, P.cscr, P.dexit[bi0 * 4 + k % ND], ox, oy[k / ND]);
+    }
+  }
   bool more = false;  // a ray of this lane still marches
 #pragma unroll
   for (int k = 0; k < NR; ++k) more |= act[k];
@@ -514,6 +535,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     unsigned didx[NR];  // distance-field index (tiled or linear) or packet (packed)
     unsigned psub[PACKED ? NR : 1];  // packed: byte of the texel in its packet
     bool live[NR];
+    int cix[NR], ciy[NR];
     bool any_live = false;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
@@ -530,13 +552,30 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         ix = wrap_nearest(px, sax);
         iy = wrap_nearest(py, say);
       }
-      if (cm) {  // exit proof (see s_cm); ix, iy are in range for every lane
-        const float dl = s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)];
-        const float tl = t[k] + dl;
-        bool ex = tl > P.t1;
-        if (P.cscr) ex = ex || !on_screen<P2S>(ox + (tl * rdx[r]) * P.aspy, oy[p] + (tl * rdy[r]) * P.aspx);
-        live[k] = live[k] && !(dl > 0.0f && ex);
+      if constexpr (!TLC) {
+        if (cm) {  // exit proof (see s_cm); ix, iy are in range for every lane
+          const float tl = t[k] + s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)];
+          // a live sample is on screen, and t + 0 is t: no dl > 0 test needed
+          const bool ex = tl >= t1n || (P.cscr && !on_screen<P2S>(ox + (tl * rdx[r]) * P.aspy,
+                                                                   oy[p] + (tl * rdy[r]) * P.aspx));
+          live[k] = live[k] && !ex;
+        }
       }
+      cix[k] = ix;
+      ciy[k] = iy;
+    }
+    if constexpr (TLC) {
+      if (cm) {  // exit proof (see s_cm, exit_bound): the table reads together, one wait
+        float dl[NR];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) dl[k] = s_cm[((ciy[k] >> P.csh) * kCminDim) + (cix[k] >> P.csh)];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) live[k] = live[k] && !(t[k] + dl[k] >= tend[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      int ix = cix[k], iy = ciy[k];
       if (!live[k]) ix = iy = 0;
       idx[k] = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;  // < 2^24 operands
       if constexpr (TILED) {
@@ -642,6 +681,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         qdy = r == q2 ? rdy[q2] : qdy;
       }
       float tt = __uint_as_float(e.x);
+      const float qte = cm ? exit_bound(t1n, P.cscr, P.dexit[bi0 * 4 + r], qox, qoy) : 0.0f;
       int hit = -1;
       for (int it = itend; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
         const float px = qox + (tt * qdx) * P.aspy;
@@ -657,13 +697,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
           ix = wrap_nearest(px, sax);
           iy = wrap_nearest(py, say);
         }
-        if (cm) {
-          const float dl = s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)];
-          const float tq = tt + dl;
-          bool ex = tq > P.t1;
-          if (P.cscr) ex = ex || !on_screen<P2S>(qox + (tq * qdx) * P.aspy, qoy + (tq * qdy) * P.aspx);
-          live = live && !(dl > 0.0f && ex);
-        }
+        if (cm) live = live && !(tt + s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)] >= qte);
         if (!live) break;
         const int idx = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
         const float d = decode_dist(fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx));
@@ -836,6 +870,8 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   P.cmin = reinterpret_cast<const float4 *>(a.cmin);
   P.csh = dist_cmin_shift(P.s.W, P.s.H);
   P.cscr = a.cmin_screen;
+  P.dexit = a.dexit;
+  if (P.cmin && P.cscr && !P.dexit) return hipErrorInvalidValue;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
 #define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \

@@ -8,7 +8,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["RC2DGI_LIB"] = os.path.join(ROOT, "build", "diag", "librc2dgi_stats.so")
+os.environ.setdefault("RC2DGI_LIB", os.path.join(ROOT, "build", "diag", "librc2dgi_stats.so"))
 
 
 def main():

@@ -213,3 +213,48 @@ def test_nibble_packets_round_trip():
         assert esc <= W
     # the smooth row mostly fits
     assert sum(int(np.count_nonzero(n == 15)) for _, _, n in _nib_encode(rows[1], len(rows[1]))) < 60
+
+
+def _exit_terms(dx, dy, aspx, aspy):
+    """rc_exit_terms (csrc/rc2dgi_kernels.h), float32 step by step."""
+    f = np.float32
+    v = [f(dx) * f(aspy), f(dy) * f(aspx)]
+    inv, edge = [], []
+    for a in range(2):
+        dead = not (v[a] > f(2.0 ** -100) or v[a] < f(-(2.0 ** -100)))
+        inv.append(f(np.inf) if dead else f(1.0) / v[a])
+        edge.append(f(2.0) if dead else (f(1.0 + 2.0 ** -19) if v[a] > 0 else f(-(2.0 ** -19))))
+    return inv + edge
+
+
+def test_screen_exit_terms_put_the_sample_off_screen():
+    """The exit proof of k_rc_level (exit_bound) treats every t >= T as off screen, with
+    T = min((ex - ox) * ix, (ey - oy) * iy) from the per-direction terms.  Each coordinate of
+    o + (t dir) asp is monotone in t, so that holds iff the position at T itself is off screen
+    (outside [0, 1] on some axis) -- checked here in float32 for origins right at the edges,
+    directions near the axes, and the aspect ratios of non-square screens."""
+    f = np.float32
+    rng = np.random.default_rng(7)
+    edge_o = [f(0.5 / 16384), f(1 - 0.5 / 16384), f(0.5 / 4096), f(1 - 0.5 / 4096), f(0.5)]
+    checked = 0
+    for W, H in [(4096, 4096), (1200, 900), (900, 1200), (16384, 128), (333, 16384)]:
+        mx = max(W, H)
+        aspx, aspy = f(W) / f(mx), f(H) / f(mx)
+        angles = np.concatenate([rng.uniform(0, 2 * np.pi, 400),
+                                 (np.array([0, np.pi / 2, np.pi, 3 * np.pi / 2]) + rng.normal(0, 1e-6, (50, 4))).ravel()])
+        dirs = [(f(np.cos(a)), f(np.sin(a))) for a in angles] + [(f(1), f(0)), (f(0), f(-1)), (f(1e-38), f(1))]
+        origins = [(a, b) for a in edge_o for b in edge_o] + [tuple(f(x) for x in rng.uniform(0, 1, 2))
+                                                              for _ in range(20)]
+        for dx, dy in dirs:
+            ix, iy, ex, ey = _exit_terms(dx, dy, aspx, aspy)
+            for ox, oy in origins:
+                with np.errstate(invalid="ignore", over="ignore"):
+                    T = min((ex - ox) * ix, (ey - oy) * iy)
+                assert T > 0
+                if T == np.inf:
+                    continue
+                px = ox + (T * dx) * aspy
+                py = oy + (T * dy) * aspx
+                assert px < 0 or px > 1 or py < 0 or py > 1, (W, H, dx, dy, ox, oy, T, px, py)
+                checked += 1
+    assert checked > 50000, checked
