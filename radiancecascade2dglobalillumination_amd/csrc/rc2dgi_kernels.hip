@@ -1017,7 +1017,7 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.p1 = (a.p1 < 0 || a.p1 > P.bdy) ? P.bdy : a.p1;
   P.CRx = (float)c.CW;
   P.CRy = (float)c.CH;
-  P.invCRx = 1.0f / P.CRx;  // used only when CW / CH are powers of two (then exact)
+  P.invCRx = 1.0f / P.CRx;  // exact divisions when CW / CH are powers of two; else only the approximate WG-proof box
   P.invCRy = 1.0f / P.CRy;
   P.bdxf = P.CRx / (float)P.bsc;  // blockDim = _CascadeResolution / float(blockSqrtCount)
   P.bdyf = P.CRy / (float)P.bsc;

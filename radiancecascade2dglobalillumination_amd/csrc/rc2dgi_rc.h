@@ -276,6 +276,9 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                      const uint4 *__restrict__ dpk) {
   constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
   constexpr bool TILED = DL == 1, PACKED = DL == 2 || DL == 3;
+  // plain 16-bit field: the march carries byte offsets into it (twice the texel index; the
+  // P2S column comes out of the floor doubled), hit records too (halved at the shading load)
+  constexpr bool BOFF = !TILED && !PACKED;
   static_assert(!PACKED || P2S, "packed distance field: power-of-two screens only");
   // staged footprint: taps of c in [c0, c0+T) lie in [c0/2 - 1, c0/2 + T/2]
   constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
@@ -450,10 +453,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // long-ray levels the box spans many cells and the unused test alone cost 3 % (measured).
   constexpr bool WGC = !Z0 && !TLC;
   if (WGC && cm && P.wgp && !(P.t0 > P.t1)) {
-    const float bx0 = ((((float)cx0 + 0.5f) * (float)P.bsc) / P.CRx - P.t0) * P.sWf - 2.0f;
-    const float bx1 = ((((float)(cx0 + TX) - 0.5f) * (float)P.bsc) / P.CRx + P.t0) * P.sWf + 2.0f;
-    const float by0 = ((((float)cy0 + 0.5f) * (float)P.bsc) / P.CRy - P.t0) * P.sHf - 2.0f;
-    const float by1 = ((((float)(cy0 + THY) - 0.5f) * (float)P.bsc) / P.CRy + P.t0) * P.sHf + 2.0f;
+    // (reciprocal multiplies: the slack covers their rounding, and IEEE divisions cost ~10 VALU each)
+    const float bx0 = ((((float)cx0 + 0.5f) * (float)P.bsc) * P.invCRx - P.t0) * P.sWf - 2.0f;
+    const float bx1 = ((((float)(cx0 + TX) - 0.5f) * (float)P.bsc) * P.invCRx + P.t0) * P.sWf + 2.0f;
+    const float by0 = ((((float)cy0 + 0.5f) * (float)P.bsc) * P.invCRy - P.t0) * P.sHf - 2.0f;
+    const float by1 = ((((float)(cy0 + THY) - 0.5f) * (float)P.bsc) * P.invCRy + P.t0) * P.sHf + 2.0f;
     if (bx1 < P.sWf - 1.0f && by1 < P.sHf - 1.0f) {
       const int c0 = __builtin_amdgcn_readfirstlane(max(0, (int)bx0) >> P.csh);
       const int c1 = __builtin_amdgcn_readfirstlane((int)bx1 >> P.csh);
@@ -502,7 +506,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
       for (int r = 0; r < ND; ++r) {
         const int k = p * ND + r;
-        hit_idx[k] = hit ? idx : -1;
+        hit_idx[k] = hit ? (BOFF ? 2 * idx : idx) : -1;
         t[k] = live && !hit ? P.t0 + d : P.t0;
         act[k] = live && !hit && !(t[k] > P.t1);
       }
@@ -529,6 +533,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
   for (int k = 0; k < NR; ++k) more |= act[k];
   const int itend = tl ? min(P.tailk, RC2DGI_DIAG_MAX_ITERS) : RC2DGI_DIAG_MAX_ITERS;
+  // BOFF with P2S: floor(p * 2W) & (2W - 2) = 2 (floor(p W) & (W - 1)) (p W and p 2W are exact)
+  const float sWx = (BOFF && P2S) ? 2.0f * P.sWf : P.sWf;
+  const int wmask = (BOFF && P2S) ? 2 * P.s.W - 2 : P.s.W - 1;
+  const int xsh = BOFF ? P.csh + 1 : P.csh;  // column -> bound-table cell
 #pragma unroll UNR
   for (int it = it0; more && it < itend; ++it) {
     int idx[NR];
@@ -545,16 +553,18 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       int ix, iy;
       if constexpr (P2S) {
         live[k] = act[k] && __float_as_uint(px) <= 0x3f800000u && __float_as_uint(py) <= 0x3f800000u;
-        ix = cvt_floor(px * P.sWf) & (P.s.W - 1);
-        iy = cvt_floor(py * P.sHf) & (P.s.H - 1);
+        const f2v_t sc = f2v_t{px, py} * f2v_t{sWx, P.sHf};  // one packed multiply, same roundings
+        ix = cvt_floor(sc.x) & wmask;
+        iy = cvt_floor(sc.y) & (P.s.H - 1);
       } else {
         live[k] = act[k] && !(px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
         ix = wrap_nearest(px, sax);
         iy = wrap_nearest(py, say);
+        if constexpr (BOFF) ix <<= 1;
       }
       if constexpr (!TLC) {
         if (cm) {  // exit proof (see s_cm); ix, iy are in range for every lane
-          const float tl = t[k] + s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)];
+          const float tl = t[k] + s_cm[((iy >> P.csh) * kCminDim) + (ix >> xsh)];
           // a live sample is on screen, and t + 0 is t: no dl > 0 test needed
           const bool ex = tl >= t1n || (P.cscr && !on_screen<P2S>(ox + (tl * rdx[r]) * P.aspy,
                                                                    oy[p] + (tl * rdy[r]) * P.aspx));
@@ -568,7 +578,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       if (cm) {  // exit proof (see s_cm, exit_bound): the table reads together, one wait
         float dl[NR];
 #pragma unroll
-        for (int k = 0; k < NR; ++k) dl[k] = s_cm[((ciy[k] >> P.csh) * kCminDim) + (cix[k] >> P.csh)];
+        for (int k = 0; k < NR; ++k) dl[k] = s_cm[((ciy[k] >> P.csh) * kCminDim) + (cix[k] >> xsh)];
 #pragma unroll
         for (int k = 0; k < NR; ++k) live[k] = live[k] && !(t[k] + dl[k] >= tend[k]);
       }
@@ -576,6 +586,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       int ix = cix[k], iy = ciy[k];
+      if constexpr (BOFF) {  // byte offset; dead rays re-read texel 0 (one cached line)
+        const int off = (int)__umul24((unsigned)iy, (unsigned)(2 * P.s.pitch)) + ix;  // < 2^25
+        idx[k] = live[k] ? off : 0;
+        act[k] = live[k];
+        any_live |= live[k];
+        continue;
+      }
       if (!live[k]) ix = iy = 0;
       idx[k] = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;  // < 2^24 operands
       if constexpr (TILED) {
@@ -616,7 +633,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     } else {
 #pragma unroll
       for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
-        q[k] = ld_dist(dist, didx[k] << 1);
+        q[k] = ld_dist(dist, BOFF ? (unsigned)idx[k] : didx[k] << 1);
     }
     bool any = false;
 #pragma unroll
@@ -702,7 +719,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         const int idx = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
         const float d = decode_dist(fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx));
         if (d < 0.001f) {
-          hit = idx;
+          hit = BOFF ? 2 * idx : idx;  // the owner's convention
           break;
         }
         tt = tt + d;
@@ -770,7 +787,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     for (int r = 0; r < ND; ++r) {
       const int k = p * ND + r;
       hr[r] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-      if (hit_idx[k] >= 0) hr[r] = shade[hit_idx[k]];
+      if (hit_idx[k] >= 0) hr[r] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
     }
 #pragma unroll
     for (int dblk = 0; dblk < PD; ++dblk) {
