@@ -433,6 +433,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     const float2 d = dirs[bi0 * 4 + r];
     rdx[r] = d.x;
     rdy[r] = d.y;
+    if constexpr (TLC) {  // VGPR copies: the wave-uniform directions otherwise pin 8 SGPRs over the march
+      asm("v_mov_b32 %0, %1" : "=v"(rdx[r]) : "s"(d.x));
+      asm("v_mov_b32 %0, %1" : "=v"(rdy[r]) : "s"(d.y));
+    }
   }
   float t[NR];
   int hit_idx[NR];
