@@ -440,12 +440,16 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   float t[NR];
   int hit_idx[NR];
-  bool act[NR];
+  // A ray that takes no more samples (ended, or never started) holds t = +inf: its positions are
+  // then off screen (+-inf, or NaN for a zero direction component: P2S's unsigned test rejects
+  // both) and its proof passes.  The march state is t and hit_idx alone -- no per-ray booleans
+  // carried across iterations (the compiler keeps those as lane masks merged with several scalar
+  // instructions each per iteration).
+  constexpr float kDone = __builtin_inff();
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
-    t[k] = P.t0;
+    t[k] = pok[k / ND] && !(P.t0 > P.t1) ? P.t0 : kDone;
     hit_idx[k] = -1;
-    act[k] = pok[k / ND] && !(P.t0 > P.t1);  // act: the ray takes another sample (t <= t1 folded in)
   }
   // Workgroup-wide exit proof: a ray's first sample o + (t0 dir) asp lies within t0 (uv) of its
   // probe on each axis, so inside the tile's probe box grown by t0.  When every bound-table cell
@@ -473,7 +477,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
           for (int cc = c0; cc <= c1; ++cc) m = fminf(m, s_cm[rr * kCminDim + cc]);
         if (m > 0.0f && P.t0 + m > P.t1) {
 #pragma unroll
-          for (int k = 0; k < NR; ++k) act[k] = false;
+          for (int k = 0; k < NR; ++k) t[k] = kDone;
         }
       }
     }
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     unsigned zq[PY];
 #pragma unroll
     for (int p = 0; p < PY; ++p) {
-      zlive[p] = act[p * ND] && __float_as_uint(ox) <= 0x3f800000u && __float_as_uint(oy[p]) <= 0x3f800000u;
+      zlive[p] = t[p * ND] < kDone && __float_as_uint(ox) <= 0x3f800000u && __float_as_uint(oy[p]) <= 0x3f800000u;
       int ix = cvt_floor(ox * P.sWf) & (P.s.W - 1);
       int iy = cvt_floor(oy[p] * P.sHf) & (P.s.H - 1);
       if (!zlive[p]) ix = iy = 0;
@@ -511,8 +515,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       for (int r = 0; r < ND; ++r) {
         const int k = p * ND + r;
         hit_idx[k] = hit ? (BOFF ? 2 * idx : idx) : -1;
-        t[k] = live && !hit ? P.t0 + d : P.t0;
-        act[k] = live && !hit && !(t[k] > P.t1);
+        const float tz = P.t0 + d;
+        t[k] = live && !hit && !(tz > P.t1) ? tz : kDone;
       }
 #ifdef RC2DGI_DIAG_STATS
       diag_samples += live ? (unsigned)ND : 0u;
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   bool more = false;  // a ray of this lane still marches
 #pragma unroll
-  for (int k = 0; k < NR; ++k) more |= act[k];
+  for (int k = 0; k < NR; ++k) more |= t[k] < kDone;
   const int itend = tl ? min(P.tailk, RC2DGI_DIAG_MAX_ITERS) : RC2DGI_DIAG_MAX_ITERS;
   // BOFF with P2S: floor(p * 2W) & (2W - 2) = 2 (floor(p W) & (W - 1)) (p W and p 2W are exact)
   const float sWx = (BOFF && P2S) ? 2.0f * P.sWf : P.sWf;
@@ -552,16 +556,17 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       const int r = k % ND, p = k / ND;
-      const float px = ox + (t[k] * rdx[r]) * P.aspy;
-      const float py = oy[p] + (t[k] * rdy[r]) * P.aspx;
+      // o + (t dir) asp as one (x, y) pair per ray: packed ops, same IEEE roundings per component
+      const f2v_t pxy = f2v_t{ox, oy[p]} + (f2v_t{t[k], t[k]} * f2v_t{rdx[r], rdy[r]}) * f2v_t{P.aspy, P.aspx};
+      const float px = pxy.x, py = pxy.y;
       int ix, iy;
       if constexpr (P2S) {
-        live[k] = act[k] && __float_as_uint(px) <= 0x3f800000u && __float_as_uint(py) <= 0x3f800000u;
-        const f2v_t sc = f2v_t{px, py} * f2v_t{sWx, P.sHf};  // one packed multiply, same roundings
+        live[k] = __float_as_uint(px) <= 0x3f800000u && __float_as_uint(py) <= 0x3f800000u;  // t = inf: off
+        const f2v_t sc = pxy * f2v_t{sWx, P.sHf};  // one packed multiply, same roundings
         ix = cvt_floor(sc.x) & wmask;
         iy = cvt_floor(sc.y) & (P.s.H - 1);
       } else {
-        live[k] = act[k] && !(px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
+        live[k] = t[k] < kDone && !(px < 0.0f || py < 0.0f || px > 1.0f || py > 1.0f);
         ix = wrap_nearest(px, sax);
         iy = wrap_nearest(py, say);
         if constexpr (BOFF) ix <<= 1;
@@ -593,7 +598,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       if constexpr (BOFF) {  // byte offset; dead rays re-read texel 0 (one cached line)
         const int off = (int)__umul24((unsigned)iy, (unsigned)(2 * P.s.pitch)) + ix;  // < 2^25
         idx[k] = live[k] ? off : 0;
-        act[k] = live[k];
         any_live |= live[k];
         continue;
       }
@@ -609,10 +613,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       } else {
         didx[k] = (unsigned)idx[k];
       }
-      act[k] = live[k];
       any_live |= live[k];
     }
-    if (!any_live) break;  // every ray left its interval or the screen: no more samples
+    if (!any_live) {  // every ray left its interval or the screen: no more samples
+#pragma unroll
+      for (int k = 0; k < NR; ++k) t[k] = kDone;
+      break;
+    }
 #ifdef RC2DGI_DIAG_STATS
     diag_slots += NR;
     for (int k = 0; k < NR; ++k) diag_samples += live[k] ? 1u : 0u;
@@ -638,6 +645,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
       for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
         q[k] = ld_dist(dist, BOFF ? (unsigned)idx[k] : didx[k] << 1);
+      if constexpr (NR == 4) {
+        // all four gathers in flight before the first is consumed (left alone, the scheduler waits
+        // for the first pair before issuing the second: two round trips per iteration)
+        asm volatile("" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]));
+      }
     }
     bool any = false;
 #pragma unroll
@@ -645,9 +657,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       const float d = decode_dist(q[k]);
       const bool hit = live[k] && d < 0.001f;
       hit_idx[k] = hit ? idx[k] : hit_idx[k];
-      t[k] = live[k] && !hit ? t[k] + d : t[k];
-      act[k] = live[k] && !hit && !(t[k] > P.t1);  // the next iteration's interval test, done now
-      any |= act[k];
+      const float tn = t[k] + d;
+      const bool go = live[k] && !hit && !(tn > P.t1);  // the next iteration's interval test, done now
+      t[k] = go ? tn : kDone;
+      any |= go;
     }
     if (!any) break;
   }
@@ -664,7 +677,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     // pending rays (still marching after itend iterations) -> LDS queue, wave-contiguous ranges
     unsigned n = 0;
 #pragma unroll
-    for (int k = 0; k < NR; ++k) n += act[k] ? 1u : 0u;
+    for (int k = 0; k < NR; ++k) n += t[k] < kDone ? 1u : 0u;
     unsigned excl = 0, tot = 0;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {  // n <= NR <= 8: exclusive prefix over the wave, bit by bit
@@ -681,7 +694,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       qpos[k] = (int)pos;
-      if (act[k]) s_q[pos++] = make_uint2(__float_as_uint(t[k]), (threadIdx.x << 3) | (unsigned)k);
+      if (t[k] < kDone) s_q[pos++] = make_uint2(__float_as_uint(t[k]), (threadIdx.x << 3) | (unsigned)k);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
@@ -755,7 +768,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   if (tl) {  // hit texels of this lane's rays that finished in the tail
 #pragma unroll
     for (int k = 0; k < NR; ++k)
-      if (act[k]) hit_idx[k] = (int)s_q[qpos[k]].x;
+      if (t[k] < kDone) hit_idx[k] = (int)s_q[qpos[k]].x;
   }
 
   // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
