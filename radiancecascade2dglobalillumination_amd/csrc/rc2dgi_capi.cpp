@@ -185,7 +185,7 @@ void derive_sizes(int W, int H, int N, float rs, int &CW, int &CH, int &S) {
 }
 
 // tail compaction default: rays still marching after 6 lockstep iterations finish one per lane
-constexpr int kDefaultTail = 6;
+constexpr int kDefaultTail = 10;
 
 size_t dir_table_len(int N) {  // sum over levels of 4^(L+1)
   size_t n = 0;
