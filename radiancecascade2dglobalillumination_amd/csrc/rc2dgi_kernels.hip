@@ -381,27 +381,39 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
 // every texel a ray can stop on (decode_dist(q) < 0.001, the march's own test) the record is
 // (emission, 1) when length(emission) > 0, else (albedo, _Reflectivity).  The march then needs
 // one load per hit instead of an emissive load plus, for albedo hits, a second dependent one.
-// Texels no ray can stop on are not written (and never read).  One thread per 4 texels of a row.
+// Texels no ray can stop on are not written (and never read).  A wave covers 256 texels of a row
+// in four 64-texel passes (every load and store instruction of the wave is one contiguous run);
+// the emission and the albedo of every hittable texel are loaded together (one round trip after
+// the field, not a second, dependent one for the albedo hits).
 __global__ __launch_bounds__(256) void k_shade(const unsigned short *__restrict__ dist, const float4 *__restrict__ color,
                                                const float4 *__restrict__ emis, float4 *__restrict__ shade,
                                                ScreenDims s, float reflectivity) {
-  const int i0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+  const int lane = threadIdx.x & 63;
+  const int i0 = blockIdx.x * 256 + lane;
   const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (i0 >= s.W || j >= s.H) return;
+  if (j >= s.H) return;
   const size_t row = (size_t)j * s.pitch;
-  const uint2 q4 = *reinterpret_cast<const uint2 *>(dist + row + i0);  // pitch is a multiple of 64 texels
-  const unsigned q[4] = {q4.x & 0xFFFFu, q4.x >> 16, q4.y & 0xFFFFu, q4.y >> 16};
+  unsigned q[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) q[t] = i0 + 64 * t < s.W ? dist[row + i0 + 64 * t] : 0xFFFFu;
+  bool h[4];
+  float4 e[4], c[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int i = i0 + t;
-    if (i < s.W && decode_dist(q[t]) < 0.001f) {
-      const float4 e = emis[row + i];
-      float4 r = make_float4(e.x, e.y, e.z, 1.0f);
-      if (!(sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f)) {
-        const float4 c = color[row + i];
-        r = make_float4(c.x, c.y, c.z, reflectivity);
-      }
-      shade[row + i] = r;
+    h[t] = decode_dist(q[t]) < 0.001f;  // q = 0xFFFF (beyond the row) decodes to 1
+    e[t] = c[t] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (h[t]) {
+      e[t] = emis[row + i0 + 64 * t];
+      c[t] = color[row + i0 + 64 * t];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (h[t]) {
+      float4 r = make_float4(e[t].x, e[t].y, e[t].z, 1.0f);
+      if (!(sqrtf(e[t].x * e[t].x + e[t].y * e[t].y + e[t].z * e[t].z) > 0.0f))
+        r = make_float4(c[t].x, c[t].y, c[t].z, reflectivity);
+      shade[row + i0 + 64 * t] = r;
     }
   }
 }
