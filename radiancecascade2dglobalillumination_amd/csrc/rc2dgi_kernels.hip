@@ -431,18 +431,32 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
   const bool in = x0 < W && y0 < H;
   if (in) {
     const int x1 = min(W, x0 + (1 << csh)), y1 = min(H, y0 + (1 << csh));
-    const int n4 = (x1 - x0 + 3) >> 2;  // 4-texel groups per row of the cell
-    const int tot = n4 * (y1 - y0);
-    for (int e = (int)threadIdx.x; e < tot; e += 256) {
-      const int r = e / n4;
-      const int xx = x0 + 4 * (e - r * n4);
-      const unsigned short *p = dist + (size_t)(y0 + r) * pitch + xx;
-      if (csh >= 2 && xx + 3 < x1) {  // 8-byte aligned: x0 is a multiple of 4, rows of 64-texel pitch
-        const uint2 v = *reinterpret_cast<const uint2 *>(p);
-        m = min(m, min(min(v.x & 0xFFFFu, v.x >> 16), min(v.y & 0xFFFFu, v.y >> 16)));
-      } else {
-        for (int t = 0; t < 4; ++t)
-          if (xx + t < x1) m = min(m, (unsigned)p[t]);
+    if (csh >= 3 && x1 - x0 == (1 << csh) && y1 - y0 == (1 << csh)) {
+      // whole cell: 16-byte loads of 8 texels (rows of 64-texel pitch keep them aligned), shifts
+      // instead of the general path's integer division, several loads in flight
+      const int sh = csh - 3, tot = 1 << (2 * csh - 3);
+#pragma unroll 4
+      for (int e = (int)threadIdx.x; e < tot; e += 256) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(dist + (size_t)(y0 + (e >> sh)) * pitch + x0 +
+                                                          ((e & ((1 << sh) - 1)) << 3));
+        const unsigned a = min(min(v.x & 0xFFFFu, v.x >> 16), min(v.y & 0xFFFFu, v.y >> 16));
+        const unsigned b = min(min(v.z & 0xFFFFu, v.z >> 16), min(v.w & 0xFFFFu, v.w >> 16));
+        m = min(m, min(a, b));
+      }
+    } else {
+      const int n4 = (x1 - x0 + 3) >> 2;  // 4-texel groups per row of the cell
+      const int tot = n4 * (y1 - y0);
+      for (int e = (int)threadIdx.x; e < tot; e += 256) {
+        const int r = e / n4;
+        const int xx = x0 + 4 * (e - r * n4);
+        const unsigned short *p = dist + (size_t)(y0 + r) * pitch + xx;
+        if (csh >= 2 && xx + 3 < x1) {  // 8-byte aligned: x0 is a multiple of 4, rows of 64-texel pitch
+          const uint2 v = *reinterpret_cast<const uint2 *>(p);
+          m = min(m, min(min(v.x & 0xFFFFu, v.x >> 16), min(v.y & 0xFFFFu, v.y >> 16)));
+        } else {
+          for (int t = 0; t < 4; ++t)
+            if (xx + t < x1) m = min(m, (unsigned)p[t]);
+        }
       }
     }
   }
