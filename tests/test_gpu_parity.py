@@ -513,3 +513,43 @@ def test_jfa_lds_staging_is_bit_identical(RC2DGI, W, H, N, storage):
     for k in out[0]:
         assert np.array_equal(out[0][k], out[1][k]), f"{k}: {np.count_nonzero(out[0][k] != out[1][k])}"
     ctx.close()
+
+
+@pytest.mark.parametrize("W,H,N", [(256, 256, 4), (512, 256, 4), (240, 180, 3)])
+def test_degenerate_direction_tables(RC2DGI, W, H, N):
+    """Direction tables with exact zero components, unit axes, components below the exit table's
+    2^-100 guard (csrc/rc2dgi_kernels.h rc_exit_terms), denormals and tiny ones: an ended ray holds
+    t = +inf, so a zero component makes its position NaN (rejected by the screen test), and the
+    screen-exit term of a vanishing component must never prove an exit.  Every level is bit-exact
+    with the oracle under every exit-proof setting."""
+    color, emis = make_scene("demo", W, H)
+    specials = np.array([[1, 0], [0, 1], [-1, 0], [0, -1], [1e-35, 1], [-1e-40, -1], [1, 1e-38], [-1, -2e-7],
+                         [0.6, -0.8], [-0.0, 1], [1, -0.0], [0.7071068, 0.7071068]], np.float32)
+    rng = np.random.default_rng(11)
+    tabs = []
+    for L in range(N):
+        n = 4 << (2 * L)
+        tabs.append(specials[rng.integers(0, len(specials), n)])
+    dir_tabs = np.concatenate(tabs).astype(np.float32)  # (directions, 2) as the fixtures hold them
+    p = oracle.Params(W=W, H=H, N=N, ray_range=2.0)
+    fr = oracle.frame(p, color, emis, dir_tabs=dir_tabs, keep_levels=True)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0)
+    ctx.set_keep_levels(True)
+    off = 0
+    for L in range(N):
+        n = 4 << (2 * L)
+        ctx.set_direction_table(L, dir_tabs[off:off + n])
+        off += n
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    for v in (0, 6, 13):
+        ctx.set_tuning("rc_variant", v)
+        for skip in (0, 2, 3):
+            ctx.set_tuning("rc_skip", skip)
+            ctx.do_rc2dgi()
+            ctx.sync()
+            for L in range(N):
+                g = ctx.download_level(L)
+                assert np.array_equal(g, fr.gi_levels[L]), \
+                    f"variant {v} rc_skip {skip} level {L}: {np.count_nonzero(g != fr.gi_levels[L])}"
+    ctx.close()
