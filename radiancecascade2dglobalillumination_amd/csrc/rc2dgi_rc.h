@@ -451,6 +451,20 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     t[k] = pok[k / ND] && !(P.t0 > P.t1) ? P.t0 : kDone;
     hit_idx[k] = -1;
   }
+  // Far intervals (t0 >= 1/4: the top levels, where most rays start beyond the screen edge): a ray
+  // whose first position is off screen takes no sample at all (RadianceCascades.fs:65-69), so it
+  // ends here -- and a wave whose rays all start off screen skips the march.  The position is the
+  // march's own expression.
+  if constexpr (TLC) {
+    if (P.t0 >= 0.25f) {
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        const f2v_t pxy =
+            f2v_t{ox, oy[k / ND]} + (f2v_t{t[k], t[k]} * f2v_t{rdx[k % ND], rdy[k % ND]}) * f2v_t{P.aspy, P.aspx};
+        if (!on_screen<P2S>(pxy.x, pxy.y)) t[k] = kDone;
+      }
+    }
+  }
   // Workgroup-wide exit proof: a ray's first sample o + (t0 dir) asp lies within t0 (uv) of its
   // probe on each axis, so inside the tile's probe box grown by t0.  When every bound-table cell
   // under that box proves exit for a first sample (dl > 0 and t0 + dl > t1: every sample there
