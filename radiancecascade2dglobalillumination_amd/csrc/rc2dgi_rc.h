@@ -468,9 +468,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // Workgroup-wide exit proof: a ray's first sample o + (t0 dir) asp lies within t0 (uv) of its
   // probe on each axis, so inside the tile's probe box grown by t0.  When every bound-table cell
   // under that box proves exit for a first sample (dl > 0 and t0 + dl > t1: every sample there
-  // misses and ends its ray), no ray of the workgroup samples at all: the march is skipped.  The
-  // box carries two texels of slack for its approximate float arithmetic; a box touching the far
-  // screen edge (where p = 1 wraps to texel 0) is not tried.  Compiled into the kernels without
+  // misses and ends its ray), no ray of the workgroup samples at all: the march is skipped.  Boxes
+  // of up to 8 x 8 cells are tried.  The box carries two texels of slack for its approximate float
+  // arithmetic; a box touching the far screen edge (where p = 1 wraps to texel 0) is not tried.
+  // Compiled into the kernels without
   // tail compaction (the several-probes-per-lane tiles that serve the short-ray levels): at the
   // long-ray levels the box spans many cells and the unused test alone cost 3 % (measured).
   constexpr bool WGC = !Z0 && !TLC;
@@ -485,11 +486,16 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       const int c1 = __builtin_amdgcn_readfirstlane((int)bx1 >> P.csh);
       const int r0 = __builtin_amdgcn_readfirstlane(max(0, (int)by0) >> P.csh);
       const int r1 = __builtin_amdgcn_readfirstlane((int)by1 >> P.csh);
-      if ((c1 - c0 + 1) * (r1 - r0 + 1) <= 16) {
-        float m = 3.0e38f;
-        for (int rr = r0; rr <= r1; ++rr)
-          for (int cc = c0; cc <= c1; ++cc) m = fminf(m, s_cm[rr * kCminDim + cc]);
-        if (m > 0.0f && P.t0 + m > P.t1) {
+      if (c1 - c0 < 8 && r1 - r0 < 8) {
+        // every cell of the box at once, one per lane of an 8 x 8 window, and one vote (the old
+        // uniform loop over the cells cost a dependent LDS round trip and ~4 VALU per cell)
+        const int dr = lane >> 3, dc = lane & 7;
+        bool ok = true;
+        if (dr <= r1 - r0 && dc <= c1 - c0) {
+          const float v = s_cm[(r0 + dr) * kCminDim + c0 + dc];
+          ok = v > 0.0f && P.t0 + v > P.t1;
+        }
+        if (__all(ok)) {
 #pragma unroll
           for (int k = 0; k < NR; ++k) t[k] = kDone;
         }
