@@ -100,7 +100,10 @@ struct RcLevelArgs {
 
 // coarse lower bound of the distance field: kCminDim x kCminDim cells of 2^dist_cmin_shift texels,
 // float per cell (row-major, kCminDim per row) = decode_dist(min q) or 0 where a texel is a hit
-constexpr int kCminDim = 32;
+#ifndef RC2DGI_CMIN_DIM
+#define RC2DGI_CMIN_DIM 32  // experiment builds may override it (_build.py exp)
+#endif
+constexpr int kCminDim = RC2DGI_CMIN_DIM;
 int dist_cmin_shift(int W, int H);
 hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, float *cmin, int W, int H, hipStream_t st);
 
