@@ -102,7 +102,7 @@ struct rc2dgi_ctx {
   uint4 *dist_p = nullptr;           // packed copy for the "p" RC variants (k_dist_pack)
   uint4 *dist_n = nullptr;           // nibble-predicted copy for the "n" RC variants (k_dist_nib)
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
-  float *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
+  CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
@@ -317,7 +317,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
   HIPCHK(c, alloc(&c->dist_n, dist_nib_bytes(c->W, c->H)));
   HIPCHK(c, alloc(&c->shade, ns * sizeof(float4)));
-  HIPCHK(c, alloc(&c->cmin, (size_t)kCminDim * kCminDim * sizeof(float)));
+  HIPCHK(c, alloc(&c->cmin, (size_t)kCminDim * kCminDim * sizeof(CminT)));
   const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
   HIPCHK(c, alloc(&c->gi1, nc * gsz));
   HIPCHK(c, alloc(&c->gi2, nc * gsz));

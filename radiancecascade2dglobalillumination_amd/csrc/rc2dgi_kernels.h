@@ -75,6 +75,35 @@ struct RcMapCache {
   ~RcMapCache();
 };
 
+// coarse lower bound of the distance field: kCminDim x kCminDim cells of 2^dist_cmin_shift texels
+// (row-major, kCminDim per row).  Default: 64 x 64 byte entries (4 KB of LDS per workgroup, as the
+// round-2 32 x 32 float table): entry k stands for the lower bound k / 512 = floor(512 d) / 512 <= d
+// of the cell's smallest decode_dist(q), 0 where a texel is a hit.  -DRC2DGI_CMIN_F32 builds the
+// older 32 x 32 float table (A/B: the finer cells cut RC 1.717 -> 1.707 ms on one box).
+#ifndef RC2DGI_CMIN_F32
+#define RC2DGI_CMIN_U8 1
+#endif
+#ifdef RC2DGI_CMIN_U8
+using CminT = unsigned char;
+#ifndef RC2DGI_CMIN_DIM
+#define RC2DGI_CMIN_DIM 64
+#endif
+#else
+using CminT = float;
+#ifndef RC2DGI_CMIN_DIM
+#define RC2DGI_CMIN_DIM 32
+#endif
+#endif
+constexpr int kCminDim = RC2DGI_CMIN_DIM;
+constexpr float kCminStep = 1.0f / 512.0f;
+__host__ __device__ __forceinline__ float cmin_value(CminT v) {
+#ifdef RC2DGI_CMIN_U8
+  return (float)v * kCminStep;  // exact: k < 2^8, power-of-two step
+#else
+  return v;
+#endif
+}
+
 struct RcLevelArgs {
   const float4 *upper;   // G_{L+1} (nullptr at the top level)
   float4 *out;           // G_L
@@ -92,20 +121,14 @@ struct RcLevelArgs {
   const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
   const uint4 *dist_nib = nullptr;             // nibble-predicted distance field (variants "n", k_dist_nib)
-  const float *cmin = nullptr;  // coarse lower bound of the field (launch_dist_cmin); nullptr: no exit proofs
+  const CminT *cmin = nullptr;  // coarse lower bound of the field (launch_dist_cmin); nullptr: no exit proofs
   int cmin_screen = 0;          // the exit proof also tests the screen edge (worth it for long rays)
   int tail_k = 0;               // tail compaction after this many lockstep march iterations (0: off)
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
 };
 
-// coarse lower bound of the distance field: kCminDim x kCminDim cells of 2^dist_cmin_shift texels,
-// float per cell (row-major, kCminDim per row) = decode_dist(min q) or 0 where a texel is a hit
-#ifndef RC2DGI_CMIN_DIM
-#define RC2DGI_CMIN_DIM 32  // experiment builds may override it (_build.py exp)
-#endif
-constexpr int kCminDim = RC2DGI_CMIN_DIM;
 int dist_cmin_shift(int W, int H);
-hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, float *cmin, int W, int H, hipStream_t st);
+hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st);
 
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,

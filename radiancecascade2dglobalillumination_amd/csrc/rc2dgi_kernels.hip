@@ -419,13 +419,13 @@ __global__ __launch_bounds__(256) void k_shade(const unsigned short *__restrict_
 }
 
 // ---------------------------------------------------------------- coarse lower bound of the field
-// One workgroup per cell of 2^csh x 2^csh texels (a 32 x 32 grid covers the screen): the cell's
+// One workgroup per cell of 2^csh x 2^csh texels (a kCminDim x kCminDim grid covers the screen): the cell's
 // smallest distance decode_dist(min q), or 0 when some texel of the cell passes the march's hit
 // test.  decode_dist is monotone, so the value bounds every texel of the cell from below: a ray
 // whose sample lies in the cell advances by at least that much and does not stop there
 // (k_rc_level's exit proof, kCminDim).
 __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restrict__ dist, int pitch,
-                                                   float *__restrict__ cmin, int W, int H, int csh) {
+                                                   CminT *__restrict__ cmin, int W, int H, int csh) {
   const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
   unsigned m = 0xFFFFu;
   const bool in = x0 < W && y0 < H;
@@ -468,7 +468,12 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
   if (threadIdx.x == 0) {
     m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
     const float d = decode_dist(m);
+#ifdef RC2DGI_CMIN_U8
+    // floor(d * 512) / 512 <= d (power-of-two scaling and floor are exact); 0 where a texel hits
+    cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? (CminT)fminf(floorf(d * 512.0f), 255.0f) : (CminT)0;
+#else
     cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? d : 0.0f;
+#endif
   }
 }
 
@@ -1232,7 +1237,7 @@ int dist_cmin_shift(int W, int H) {
   return s;
 }
 
-hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, float *cmin, int W, int H, hipStream_t st) {
+hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st) {
   hipLaunchKernelGGL(k_dist_cmin, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, pitch, cmin, W, H,
                      dist_cmin_shift(W, H));
   return hipGetLastError();

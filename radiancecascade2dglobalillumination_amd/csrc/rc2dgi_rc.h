@@ -25,7 +25,7 @@ struct RcParams {
   float sWf, sHf;  // screen size as floats (power-of-two screen path)
   const uint2 *wg_map;  // workgroup -> (tile x | y << 16, direction group), host-built (XCD remap + order)
   int tpr;              // 8x8 tiles per row of the tiled distance field (TILED)
-  const float4 *cmin;   // coarse lower bound of the field (kCminDim^2 floats as float4), nullptr: off
+  const float4 *cmin;   // coarse lower bound of the field (kCminDim^2 CminT entries as float4), nullptr: off
   const float4 *dexit;  // screen-exit terms per direction of the level (rc_exit_terms)
   int csh;              // its cells are 2^csh texels square
   int cscr;             // the exit proof tests the screen edge too
@@ -304,14 +304,15 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // the staging loads and hides under them, so Z0 kernels keep the plain march.
   constexpr bool CMS = !Z0;
   constexpr int CMN = kCminDim * kCminDim;
-  __shared__ float s_cm[CMS ? CMN : 1];
+  __shared__ __attribute__((aligned(16))) CminT s_cm[CMS ? CMN : 1];
   const bool cm = CMS && P.cmin != nullptr;
-  constexpr int CPT = CMS ? (CMN / 4 + NT - 1) / NT : 1;  // float4 of the table per thread
+  constexpr int CM4 = CMN * (int)sizeof(CminT) / 16;  // 16-byte pieces of the table
+  constexpr int CPT = CMS ? (CM4 + NT - 1) / NT : 1;  // per thread
   float4 cmv[CPT];
   if (cm) {
 #pragma unroll
     for (int j = 0; j < CPT; ++j)
-      if (CMN / 4 % NT == 0 || (int)threadIdx.x + j * NT < CMN / 4) cmv[j] = P.cmin[threadIdx.x + j * NT];
+      if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4) cmv[j] = P.cmin[threadIdx.x + j * NT];
   }
   // Tail compaction.  A lane marches its NR rays in lockstep and a wave runs until its longest ray
   // ends, so the few rays that pass close to a surface (steps shrink, then grow geometrically) set
@@ -405,7 +406,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     if (cm) {
 #pragma unroll
       for (int j = 0; j < CPT; ++j)
-        if (CMN / 4 % NT == 0 || (int)threadIdx.x + j * NT < CMN / 4)
+        if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4)
           reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
     }
     if (tl && threadIdx.x == 0) s_qn = 0u;
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         const int dr = lane >> 3, dc = lane & 7;
         bool ok = true;
         if (dr <= r1 - r0 && dc <= c1 - c0) {
-          const float v = s_cm[(r0 + dr) * kCminDim + c0 + dc];
+          const float v = cmin_value(s_cm[(r0 + dr) * kCminDim + c0 + dc]);
           ok = v > 0.0f && P.t0 + v > P.t1;
         }
         if (__all(ok)) {
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       }
       if constexpr (!TLC) {
         if (cm) {  // exit proof (see s_cm); ix, iy are in range for every lane
-          const float tl = t[k] + s_cm[((iy >> P.csh) * kCminDim) + (ix >> xsh)];
+          const float tl = t[k] + cmin_value(s_cm[((iy >> P.csh) * kCminDim) + (ix >> xsh)]);
           // a live sample is on screen, and t + 0 is t: no dl > 0 test needed
           const bool ex = tl >= t1n || (P.cscr && !on_screen<P2S>(ox + (tl * rdx[r]) * P.aspy,
                                                                    oy[p] + (tl * rdy[r]) * P.aspx));
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       if (cm) {  // exit proof (see s_cm, exit_bound): the table reads together, one wait
         float dl[NR];
 #pragma unroll
-        for (int k = 0; k < NR; ++k) dl[k] = s_cm[((ciy[k] >> P.csh) * kCminDim) + (cix[k] >> xsh)];
+        for (int k = 0; k < NR; ++k) dl[k] = cmin_value(s_cm[((ciy[k] >> P.csh) * kCminDim) + (cix[k] >> xsh)]);
 #pragma unroll
         for (int k = 0; k < NR; ++k) live[k] = live[k] && !(t[k] + dl[k] >= tend[k]);
       }
@@ -751,7 +752,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
           ix = wrap_nearest(px, sax);
           iy = wrap_nearest(py, say);
         }
-        if (cm) live = live && !(tt + s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)] >= qte);
+        if (cm) live = live && !(tt + cmin_value(s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)]) >= qte);
         if (!live) break;
         const int idx = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
         const float d = decode_dist(fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx));
