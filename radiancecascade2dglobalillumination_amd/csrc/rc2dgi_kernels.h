@@ -95,7 +95,10 @@ using CminT = float;
 #endif
 #endif
 constexpr int kCminDim = RC2DGI_CMIN_DIM;
-constexpr float kCminStep = 1.0f / 512.0f;
+#ifndef RC2DGI_CMIN_SCALE
+#define RC2DGI_CMIN_SCALE 512.0f  // a power of two (experiment builds may override it)
+#endif
+constexpr float kCminScale = RC2DGI_CMIN_SCALE, kCminStep = 1.0f / RC2DGI_CMIN_SCALE;
 __host__ __device__ __forceinline__ float cmin_value(CminT v) {
 #ifdef RC2DGI_CMIN_U8
   return (float)v * kCminStep;  // exact: k < 2^8, power-of-two step

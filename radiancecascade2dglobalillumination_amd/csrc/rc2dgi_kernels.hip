@@ -469,8 +469,8 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
     m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
     const float d = decode_dist(m);
 #ifdef RC2DGI_CMIN_U8
-    // floor(d * 512) / 512 <= d (power-of-two scaling and floor are exact); 0 where a texel hits
-    cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? (CminT)fminf(floorf(d * 512.0f), 255.0f) : (CminT)0;
+    // floor(d * scale) / scale <= d (power-of-two scaling and floor are exact); 0 where a texel hits
+    cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
 #else
     cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? d : 0.0f;
 #endif
