@@ -44,6 +44,25 @@ def test_hit_threshold_monotone():
     assert hits[:k].all() and not hits[k:].any() and k == 66
 
 
+def test_byte_exit_table_entries_are_lower_bounds():
+    """k_dist_cmin's byte entries (CminT, rc2dgi_kernels.h): a cell whose smallest distance d passes
+    the hit test stores k = min(255, floor(d * 512)) and k_rc_level reads k * (1/512).  That value
+    must never exceed d (the exit proof needs a lower bound), and 0 stays 0 (a hit cell proves
+    nothing).  Every q, fp32 arithmetic as on the device."""
+    q = np.arange(65536, dtype=np.float32)
+    d = q / np.float32(65535.0)
+    for scale in (256.0, 512.0, 1024.0):
+        sc = np.float32(scale)
+        k = np.where(d >= np.float32(0.001), np.minimum(np.floor(d * sc), np.float32(255.0)), np.float32(0.0))
+        k = k.astype(np.uint8)
+        bound = k.astype(np.float32) * (np.float32(1.0) / sc)
+        assert (bound <= d).all()
+        assert (bound[d < np.float32(0.001)] == 0).all()
+        # the bound is tight to one step below saturation
+        ok = (d < np.float32(255.0) / sc) & (d >= np.float32(0.001))
+        assert (d[ok] - bound[ok] < np.float32(1.0) / sc).all()
+
+
 def test_pow2_division_is_reciprocal_multiply():
     """div_res(): for n = 2^k, a / n == a * (1/n) bit for bit (exact scaling)."""
     rng = np.random.default_rng(0)
