@@ -249,7 +249,7 @@ def bench_batch(a, rank, local, world):
     if rank == 0:
         print(json.dumps({
             "metric": "Mpixel*cascades/s (whole DoRC2DGI frames, batch of independent scenes)",
-            "value": round(units / wall / 1e6, 1), "unit": "Mpixel*cascades/s", "n_gpus": world,
+            "value": round(units / wall / 1e6, 1), "unit": "Mpixel*cascades/s", "n_gpus": world, "pg_world": pg_world(),
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall * 1e3 / a.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic random scenes resident in HBM",
@@ -330,7 +330,7 @@ def bench_strips(a, rank, local, world):
     if rank == 0:
         print(json.dumps({
             "metric": f"Mpixel*cascades/s (whole DoRC2DGI frame, row strips) at {W}x{H}, cascadeCount={N}",
-            "value": round(units / wall / 1e6, 1), "unit": "Mpixel*cascades/s", "n_gpus": world,
+            "value": round(units / wall / 1e6, 1), "unit": "Mpixel*cascades/s", "n_gpus": world, "pg_world": pg_world(),
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall * 1e3 / a.steps, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
@@ -339,6 +339,34 @@ def bench_strips(a, rank, local, world):
             "frames_per_s": round(a.steps / wall, 2)}), flush=True)
     for g in ctxs:
         g.close()
+
+
+def spawn_ranks(n):
+    """bench.py --gpus N outside torch.distributed.run: run N ranks of this same command line under
+    it (one process per GPU, rendezvous on 127.0.0.1) as a child, and return its exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:  # a free port for the rendezvous
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def pg_world():
+    """World size of the initialised process group (1 without one): what the line's n_gpus is."""
+    import torch.distributed as dist
+
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def finish_pg():
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def main():
@@ -377,13 +405,37 @@ def main():
                     help="extra rc2dgi_set_tuning knob applied after the schedule (e.g. rc_skip=0), repeatable")
     ap.add_argument("--shards", type=int, default=1,
                     help="strips on one process: run this many shards as in-process contexts")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend (nccl = RCCL on the GPU box; gloo only with --launch-check)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="no GPU work: bring up the ranks, print the world size the line would carry")
     a = ap.parse_args()
+
+    # --gpus N is the rank count.  Without a torch.distributed.run environment, spawn it here as a
+    # child process -- before anything touches the GPU -- and exit with its code; inside one, a
+    # world size other than N is an error, never a silent one-GPU line.
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return spawn_ranks(a.gpus)
+    if env_world is not None and int(env_world) != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        return 2
+
+    from radiancecascade2dglobalillumination_amd import dist as rdist
+
+    if a.launch_check:
+        rank, local, world = rdist.init(a.backend)
+        got = rdist.max_over_ranks([float(rank)], device="cpu" if a.backend == "gloo" else "cuda")
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world, "pg_world": pg_world(), "backend": a.backend,
+                              "max_rank": int(got[0])}), flush=True)
+        finish_pg()
+        return 0
 
     import numpy as np
     import torch
 
     from radiancecascade2dglobalillumination_amd import RC2DGI, scenes
-    from radiancecascade2dglobalillumination_amd import dist as rdist
 
     rank, local, world = rdist.init("nccl")
     if a.batch:
@@ -466,7 +518,7 @@ def main():
                    f"Mpixel*cascades/s (RC pass) at {W}x{H}, cascadeCount={N}"),
         "value": round(value, 1),
         "unit": "Mpixel*cascades/s",
-        "n_gpus": world,
+        "n_gpus": world, "pg_world": pg_world(),
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(wall * 1e3 / a.steps, 4),
@@ -502,11 +554,9 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
+    finish_pg()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

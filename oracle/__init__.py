@@ -70,6 +70,9 @@ def lib():
         L.orc_rc_level.restype = None
         L.orc_rc_level.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _f32p,
                                    _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int]
+        L.orc_rc_level_strided.restype = None
+        L.orc_rc_level_strided.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _f32p,
+                                   _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.orc_dir_table.argtypes = [ctypes.c_int, ctypes.c_int, _f32p]
         L.orc_sky_table.argtypes = [ctypes.POINTER(_Cfg), _f32p]
         L.orc_dims.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
@@ -214,6 +217,14 @@ def rc_level(p: Params, level: int, upper, color, emissive, dist, out, dir_table
     _, CH, _ = dims(p)
     lib().orc_rc_level(ctypes.byref(p.c()), level, _p(upper), _p(color), _p(emissive), _p(dist), _p(out),
                        _p(dir_table), _p(sky_tab), None, row0, CH if row1 is None else row1)
+
+
+def rc_level_rows(p: Params, level: int, upper, color, emissive, dist, out, dir_table, sky_tab, row0=0, row1=None,
+                  stride=1):
+    """rc_level over the rows row0, row0 + stride, ... < row1, in parallel (parity tests)."""
+    _, CH, _ = dims(p)
+    lib().orc_rc_level_strided(ctypes.byref(p.c()), level, _p(upper), _p(color), _p(emissive), _p(dist), _p(out),
+                               _p(dir_table), _p(sky_tab), None, row0, CH if row1 is None else row1, stride)
 
 
 def _c(a):

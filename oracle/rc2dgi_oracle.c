@@ -356,6 +356,14 @@ static inline void sample_radiance_sdf(const orc_cfg *c, const float *color, con
 void orc_rc_level(const orc_cfg *c, int level, const float *upper, const float *color,
                   const float *emissive, const float *dist, float *out, const float *dir_table,
                   const float *sky_table, const float *tc, int row0, int row1) {
+  orc_rc_level_strided(c, level, upper, color, emissive, dist, out, dir_table, sky_table, tc, row0, row1, 1);
+}
+
+/* the rows row0, row0 + stride, ... below row1 (parity tests: a spread sample of a large level,
+ * the rows run in parallel) */
+void orc_rc_level_strided(const orc_cfg *c, int level, const float *upper, const float *color,
+                          const float *emissive, const float *dist, float *out, const float *dir_table,
+                          const float *sky_table, const float *tc, int row0, int row1, int stride) {
   int CW, CH;
   orc_dims(c, &CW, &CH, NULL);
   int mx = c->W > c->H ? c->W : c->H;
@@ -374,9 +382,12 @@ void orc_rc_level(const orc_cfg *c, int level, const float *upper, const float *
   float bs2 = (float)(bsc * 2);
   if (row0 < 0) row0 = 0;
   if (row1 > CH) row1 = CH;
+  if (stride < 1) stride = 1;
+  const int nrows = row1 > row0 ? (row1 - row0 + stride - 1) / stride : 0;
 #pragma omp parallel for schedule(dynamic, 4)
-  for (int j = row0; j < row1; ++j)
+  for (int jr = 0; jr < nrows; ++jr)
     for (int i = 0; i < CW; ++i) {
+      const int j = row0 + jr * stride;
       float u, v;
       tc_at(tc, i, j, CW, CH, &u, &v);
       float pix = floorf(u * CRx), piy = floorf(v * CRy);

@@ -76,6 +76,9 @@ void orc_distance_field(const float *jump, float *dist, int W, int H, const floa
 void orc_rc_level(const orc_cfg *c, int level, const float *upper, const float *color,
                   const float *emissive, const float *dist, float *out, const float *dir_table,
                   const float *sky_table, const float *tc, int row0, int row1);
+void orc_rc_level_strided(const orc_cfg *c, int level, const float *upper, const float *color,
+                  const float *emissive, const float *dist, float *out, const float *dir_table,
+                  const float *sky_table, const float *tc, int row0, int row1, int stride);
 void orc_blur(const float *gi, float *blur, int CW, int CH, float radius, const float *tc);
 void orc_blur_copyback(const float *blur, float *gi, int CW, int CH, const float *tc);
 void orc_merge(const float *color, const float *gi, float *temp, float *color_out, int W, int H,

@@ -91,6 +91,12 @@ if __name__ == "__main__":
         # join (WRONG, run-to-run different results on gfx950).  Extra flags after the mode are passed on.
         print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_ESC_PLAIN"] + sys.argv[2:],
                     out=os.path.join(ROOT, "build", "diag", "librc2dgi_escplain.so")))
+    elif len(sys.argv) > 2 and sys.argv[1] == "escform":
+        # diagnostic builds separating the two changes of the §5.3 fix: "vaddr" = compiler-scheduled escape
+        # loads with a 64-bit VGPR address (waited at the join), "saddrwait" = scalar-base form waited at once
+        form = {"vaddr": "RC2DGI_DIAG_ESC_VADDR", "saddrwait": "RC2DGI_DIAG_ESC_SADDR_WAIT"}[sys.argv[2]]
+        print(build(force=True, verbose=True, extra=[f"-D{form}"],
+                    out=os.path.join(ROOT, "build", "diag", f"librc2dgi_esc{sys.argv[2]}.so")))
     elif len(sys.argv) > 2 and sys.argv[1] == "exp":
         # A/B build of an experiment: build/ab/librc2dgi_<name>.so with the flags given (scripts/ab_lib.sh)
         print(build(force=True, verbose=True, extra=sys.argv[3:],

@@ -184,7 +184,7 @@ void derive_sizes(int W, int H, int N, float rs, int &CW, int &CH, int &S) {
   if (S < 1) S = 1;
 }
 
-// tail compaction default: rays still marching after 6 lockstep iterations finish one per lane
+// tail compaction default: rays still marching after kDefaultTail lockstep iterations finish one per lane
 constexpr int kDefaultTail = 10;
 
 size_t dir_table_len(int N) {  // sum over levels of 4^(L+1)
@@ -1057,6 +1057,17 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
       if (c->strip) {
         const size_t rowb = (size_t)c->sd.pitch * sizeof(unsigned);
         std::vector<int> waited(n, 0);
+        // step t overwrites J_{t-2} (ping-pong); the peers that copied rows of J_{t-2} from us
+        // before their step t-1 did so on their own streams, so wait for those steps (the block
+        // partners change from step to step, so they need not be the peers we receive from now)
+        if (t >= 2) {
+          std::vector<int> rd(n, 0);
+          for (const JfaXfer &x : c->jx.steps[t - 1].xfers)
+            if (x.src == k && x.dst != k && !rd[x.dst]) {
+              HIPCHK(c, hipStreamWaitEvent(c->stream, cs[x.dst]->ev_jfa[(t - 1) & 1], 0));
+              rd[x.dst] = 1;
+            }
+        }
         for (const JfaXfer &x : c->jx.steps[t].xfers) {
           if (x.dst != k) continue;
           if (x.src != k && !waited[x.src]) {
@@ -1205,8 +1216,8 @@ int rc2dgi_plan_jfa_exchange(const rc2dgi_config *cfg, int world, int step, int 
 }
 
 int rc2dgi_plan_jfa_window(const rc2dgi_config *cfg, int rank, int world, int step, int *buf, int *row0) {
-  if (!cfg || !buf || !row0 || world < 2 || rank < 0 || rank >= world || world > cfg->screen_height ||
-      cfg->cascade_count < 1 || cfg->cascade_count > 15 || !(cfg->render_scale > 0.0f))
+  if (!cfg || !buf || !row0 || cfg->screen_width < 1 || cfg->screen_height < 1 || world < 2 || rank < 0 ||
+      rank >= world || world > cfg->screen_height || cfg->cascade_count < 1 || cfg->cascade_count > 15 || !(cfg->render_scale > 0.0f))
     return RC2DGI_E_ARG;
   int CW, CH, S;
   derive_sizes(cfg->screen_width, cfg->screen_height, cfg->cascade_count, cfg->render_scale, CW, CH, S);

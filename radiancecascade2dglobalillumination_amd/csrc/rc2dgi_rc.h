@@ -183,6 +183,23 @@ __device__ __forceinline__ unsigned ld_dist_esc(const unsigned short *dist, unsi
 #ifdef RC2DGI_DIAG_ESC_PLAIN  // diagnostic build reproducing the failure: a plain load, waited at the join
   return ld_dist(dist, off);
 #endif
+#ifdef RC2DGI_DIAG_ESC_VADDR  // diagnostic: compiler-scheduled load (waited at the join), 64-bit VGPR address
+  {
+    const unsigned long long b = reinterpret_cast<unsigned long long>(dist);
+    unsigned lo, hi;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "s"((unsigned)b));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(hi) : "s"((unsigned)(b >> 32)));
+    const unsigned long long vb = ((unsigned long long)hi << 32 | lo) + off;
+    return *reinterpret_cast<const __attribute__((address_space(1))) unsigned short *>(vb);
+  }
+#endif
+#ifdef RC2DGI_DIAG_ESC_SADDR_WAIT  // diagnostic: scalar-base + 32-bit offset form, waited right after issue
+  {
+    unsigned v;
+    asm volatile("global_load_ushort %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(off), "s"(dist) : "memory");
+    return v;
+  }
+#endif
   unsigned v;
   const unsigned short *p = reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + off);
   asm volatile("global_load_ushort %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
@@ -263,6 +280,14 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
   }
 }
 
+// ISA section markers (scripts/isa_mix.py builds with -DRC2DGI_ISA_SECTIONS to split the kernel's
+// instruction mix into staging / march / tail / merge; the product build has none)
+#ifdef RC2DGI_ISA_SECTIONS
+#define RC_SECTION(n) asm volatile(";@section " n)
+#else
+#define RC_SECTION(n)
+#endif
+
 // DL: distance-field layout the march reads: 0 pitch-linear uint16, 1 8x8-tiled (TILED), 2 packed
 // 14-texel row packets (`dpk`, see kPackTexels; power-of-two screens <= 16384).
 // Z0: level 0 on a power-of-two screen (t0 = 0): the first march iteration is shared by a probe's rays
@@ -274,6 +299,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                      const float2 *__restrict__ dirs,
                                                      const float4 *__restrict__ sky,
                                                      const uint4 *__restrict__ dpk) {
+  RC_SECTION("setup");
   constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
   constexpr bool TILED = DL == 1, PACKED = DL == 2 || DL == 3;
   // plain 16-bit field: the march carries byte offsets into it (twice the texel index; the
@@ -562,6 +588,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
   for (int k = 0; k < NR; ++k) more |= t[k] < kDone;
   const int itend = tl ? min(P.tailk, RC2DGI_DIAG_MAX_ITERS) : RC2DGI_DIAG_MAX_ITERS;
+  RC_SECTION("march");
   // BOFF with P2S: floor(p * 2W) & (2W - 2) = 2 (floor(p W) & (W - 1)) (p W and p 2W are exact)
   const float sWx = (BOFF && P2S) ? 2.0f * P.sWf : P.sWf;
   const int wmask = (BOFF && P2S) ? 2 * P.s.W - 2 : P.s.W - 1;
@@ -693,6 +720,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
 #endif
 
+  RC_SECTION("tail");
   int qpos[TLC ? NR : 1];  // queue entry of each pending ray of this lane
   if (tl) {
     // pending rays (still marching after itend iterations) -> LDS queue, wave-contiguous ranges
@@ -767,6 +795,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
   }
 
+  RC_SECTION("stage_write");
   if (STG) {
 #pragma unroll
     for (int j = 0; j < DPW; ++j) {
@@ -792,6 +821,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       if (t[k] < kDone) hit_idx[k] = (int)s_q[qpos[k]].x;
   }
 
+  RC_SECTION("merge");
   // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
   const bool pow2c = P2S || (P.c.powW && P.c.powH);  // P2S implies power-of-two cascades
 #pragma unroll

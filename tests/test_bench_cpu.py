@@ -60,3 +60,27 @@ def test_valu_roofline_is_issue_time_over_level_time(bench):
     v = bench.valu_roofline(rec, 4, [0.25] * 4)  # 614.4 M instructions in 1 ms
     assert abs(v["achieved"] - 614.4) < 0.1 and abs(v["frac"] - 1.0) < 1e-3 and abs(v["floor_ms"] - 1.0) < 1e-3
     assert bench.valu_roofline({"per_level": {}}, 4, [0.1] * 4) is None
+
+
+def _run_bench(args, env_extra=None, timeout=180):
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def test_gpus_n_spawns_n_ranks_over_gloo():
+    # bench.py --gpus 2 outside torch.distributed.run launches two ranks itself (before any GPU call)
+    # and the line reports the process group's world size, never a silent one-rank run
+    r = _run_bench(["--gpus", "2", "--launch-check", "--backend", "gloo"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["pg_world"] == 2 and line["max_rank"] == 1
+
+
+def test_world_size_mismatch_is_an_error():
+    r = _run_bench(["--gpus", "4", "--launch-check", "--backend", "gloo"], {"WORLD_SIZE": "2"}, timeout=60)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
