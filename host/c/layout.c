@@ -17,6 +17,7 @@ int main(void) {
   F(rc2dgi_config, ray_range);
   F(rc2dgi_config, storage);
   F(rc2dgi_config, device);
+  F(rc2dgi_config, flags);
   F(rc2dgi_config, reserved);
   printf("rc2dgi_prim %zu\n", sizeof(rc2dgi_prim));
   F(rc2dgi_prim, kind);

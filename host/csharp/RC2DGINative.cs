@@ -25,7 +25,8 @@ static unsafe class RC2DGINative
         public int ScreenWidth, ScreenHeight, CascadeCount;
         public float RenderScale, RayRange;
         public int Storage, Device;
-        public int R0, R1, R2, R3, R4; // reserved, zero
+        public int Flags;              // 1 = Linux merge fallback (Merge.fs not found, RC2DGI.cs:62)
+        public int R0, R1, R2, R3;     // reserved, zero
     }
 
     [DllImport(Lib)] public static extern int rc2dgi_create(ref Config cfg, out IntPtr ctx);

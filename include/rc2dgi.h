@@ -44,7 +44,8 @@
 extern "C" {
 #endif
 
-#define RC2DGI_ABI_VERSION 3  /* 2: row-strip sharding entry points; 3: JumpFlood exchange planner */
+#define RC2DGI_ABI_VERSION 4  /* 2: row-strip sharding entry points; 3: JumpFlood exchange planner;
+                                 4: rc2dgi_config.flags (Linux merge fallback) */
 
 typedef struct rc2dgi_ctx rc2dgi_ctx;
 
@@ -78,6 +79,15 @@ typedef enum rc2dgi_rt {
   RC2DGI_RT_FINAL_GI = 9   /* alias of giRT1 / giRT2 per RC2DGI.cs:365          (CW x CH) */
 } rc2dgi_rt;
 
+/* rc2dgi_config.flags */
+typedef enum rc2dgi_flag {
+  /* The literal app on a case-sensitive filesystem: LoadShader(null,
+   * "shaders/Merge.fs") (RC2DGI.cs:62) finds no such file (it is merge.fs on disk), raylib substitutes
+   * its default shader, and the merge pass (RC2DGI.cs:389-397) draws colorRT into tempRT unchanged:
+   * colorRT gets no GI added.  finalGI and every other render texture are unaffected. */
+  RC2DGI_FLAG_LINUX_MERGE_FALLBACK = 1
+} rc2dgi_flag;
+
 typedef enum rc2dgi_format {
   RC2DGI_FMT_RGBA8 = 0,    /* 4 x uint8, unorm (k/255) */
   RC2DGI_FMT_RGBA32F = 1   /* 4 x float32 */
@@ -91,7 +101,8 @@ typedef struct rc2dgi_config {
   float ray_range;         /* rayRange     (RC2DGI.cs:68) -> _RayRange */
   int storage;             /* rc2dgi_storage */
   int device;              /* HIP device ordinal */
-  int reserved[5];         /* must be zero */
+  int flags;               /* rc2dgi_flag bits, 0 = the Windows behaviour (merge.fs) */
+  int reserved[4];         /* must be zero */
 } rc2dgi_config;
 
 /* ---- lifetime (RC2DGI.cs:57-109) */

@@ -35,7 +35,7 @@ class _Cfg(ctypes.Structure):
         ("sky_radiance", ctypes.c_float), ("sky_color", ctypes.c_float * 3),
         ("sun_color", ctypes.c_float * 3), ("sun_angle", ctypes.c_float),
         ("reflectivity", ctypes.c_float), ("blur_radius", ctypes.c_float), ("gi_f16", ctypes.c_int),
-        ("rgba8", ctypes.c_int),
+        ("rgba8", ctypes.c_int), ("linux_merge", ctypes.c_int),
     ]
 
 
@@ -85,6 +85,8 @@ def lib():
         L.orc_blur_copyback.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
         L.orc_merge.argtypes = [_f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 _f32p]
+        L.orc_merge_ex.argtypes = [_f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   _f32p, ctypes.c_int]
         L.orc_set_rows.argtypes = [ctypes.c_int, ctypes.c_int]
         L.orc_set_gi_f16.argtypes = [ctypes.c_int]
         L.orc_set_rgba8.argtypes = [ctypes.c_int]
@@ -112,12 +114,13 @@ class Params:
     blur_radius: float = 1.5
     gi_f16: bool = False  # giRT1/2 stored as RGBA16F (RC2DGI.cs:105-106)
     rgba8: bool = False   # every render texture RGBA8 (the literal app): texels k*(1/255)
+    linux_merge: bool = False  # Merge.fs not found on Linux (RC2DGI.cs:62): merge adds no GI
 
     def c(self) -> _Cfg:
         return _Cfg(self.W, self.H, self.N, self.render_scale, self.ray_range, self.sky_radiance,
                     (ctypes.c_float * 3)(*self.sky_color), (ctypes.c_float * 3)(*self.sun_color),
                     self.sun_angle, self.reflectivity, self.blur_radius, int(self.gi_f16),
-                    int(self.rgba8))
+                    int(self.rgba8), int(self.linux_merge))
 
 
 INV255 = np.float32(1.0) / np.float32(255.0)
@@ -289,13 +292,14 @@ def blur_copyback(blur_img, gi, tc=None):
     return g
 
 
-def merge(color, gi, tc=None):
+def merge(color, gi, tc=None, linux_merge=False):
     color, gi = _c(color), _c(gi)
     H, W = color.shape[:2]
     CH, CW = gi.shape[:2]
     temp = np.empty_like(color)
     out = np.empty_like(color)
-    lib().orc_merge(_p(color), _p(gi), _p(temp), _p(out), W, H, CW, CH, _p(None if tc is None else _c(tc)))
+    lib().orc_merge_ex(_p(color), _p(gi), _p(temp), _p(out), W, H, CW, CH, _p(None if tc is None else _c(tc)),
+                       int(linux_merge))
     return temp, out
 
 

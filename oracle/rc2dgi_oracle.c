@@ -485,6 +485,13 @@ void orc_blur_copyback(const float *blur, float *gi, int CW, int CH, const float
  * DoRC2DGI), then tempRT -> colorRT with the default shader (RC2DGI.cs:389-404). */
 void orc_merge(const float *color, const float *gi, float *temp, float *color_out, int W, int H,
                int CW, int CH, const float *tc) {
+  orc_merge_ex(color, gi, temp, color_out, W, H, CW, CH, tc, 0);
+}
+
+/* linux_merge: raylib's default shader instead of merge.fs: fragColor = texel *
+ * colDiffuse (1,1,1,1) * fragColor (white vertex colour) = the colorRT texel, exactly */
+void orc_merge_ex(const float *color, const float *gi, float *temp, float *color_out, int W, int H,
+                  int CW, int CH, const float *tc, int linux_merge) {
 #pragma omp parallel for schedule(static)
   for (int j = row_lo(); j < row_hi(H); ++j)
     for (int i = 0; i < W; ++i) {
@@ -495,6 +502,9 @@ void orc_merge(const float *color, const float *gi, float *temp, float *color_ou
       sample_bilinear(gi, CW, CH, u, v, g);
       float s[4] = {fminf(c[0] + g[0], 1.0f), fminf(c[1] + g[1], 1.0f), fminf(c[2] + g[2], 1.0f),
                     c[3]};
+      if (linux_merge) {
+        s[0] = c[0]; s[1] = c[1]; s[2] = c[2];
+      }
       float *t = temp + ((size_t)j * W + i) * 4;
       t[0] = 0.0f; t[1] = 0.0f; t[2] = 0.0f; t[3] = 1.0f; /* ClearAllRTs */
       blend_store(t, s);
@@ -591,7 +601,7 @@ int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,
     }
   }
   /* 6. merge + copy back */
-  orc_merge(color_in, finalGI, out->temp, out->color_out, c->W, c->H, CW, CH, tcs);
+  orc_merge_ex(color_in, finalGI, out->temp, out->color_out, c->W, c->H, CW, CH, tcs, c->linux_merge);
   free(dirs);
   free(sky);
   g_gi_f16 = 0; /* the per-pass API defaults to RGBA32F again */

@@ -38,6 +38,8 @@ typedef struct orc_cfg {
   int gi_f16;           /* giRT1/2 as RGBA16F (RC2DGI.cs:105-106): stores round toward zero */
   int rgba8;            /* every render texture RGBA8 (the literal app): texels hold
                            k*(1/255); inputs must already be such values */
+  int linux_merge;      /* "shaders/Merge.fs" not found on a case-sensitive filesystem (RC2DGI.cs:62,
+                           SURVEY A.8): the merge pass runs raylib's default shader (colorRT texel) */
 } orc_cfg;
 
 /* Optional overrides used only to pin the restatement against llvmpipe goldens:
@@ -83,6 +85,8 @@ void orc_blur(const float *gi, float *blur, int CW, int CH, float radius, const 
 void orc_blur_copyback(const float *blur, float *gi, int CW, int CH, const float *tc);
 void orc_merge(const float *color, const float *gi, float *temp, float *color_out, int W, int H,
                int CW, int CH, const float *tc);
+void orc_merge_ex(const float *color, const float *gi, float *temp, float *color_out, int W, int H,
+               int CW, int CH, const float *tc, int linux_merge);
 
 /* whole frame = ClearAllRTs + DoRC2DGI on the given painted inputs. returns 0 on success */
 int orc_frame(const orc_cfg *c, const float *color_in, const float *emissive,

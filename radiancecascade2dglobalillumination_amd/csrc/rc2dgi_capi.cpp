@@ -80,6 +80,7 @@ struct rc2dgi_ctx {
   int W = 0, H = 0, N = 0;
   float render_scale = 1.0f;
   int storage = RC2DGI_STORAGE_F32;
+  bool linux_merge = false;  // RC2DGI_FLAG_LINUX_MERGE_FALLBACK: the merge pass runs raylib's default shader
   float ray_range = 2.0f;
   float sky_radiance = 1.0f, sky_color[3] = {0.5f, 0.6f, 0.8f}, sun_color[3] = {1.0f, 0.9f, 0.6f};
   float sun_angle = 0.3f, reflectivity = 0.0f, blur_radius = 1.5f;
@@ -482,6 +483,7 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
     return RC2DGI_E_ARG;
   for (int r : cfg->reserved)
     if (r != 0) return RC2DGI_E_ARG;
+  if (cfg->flags & ~RC2DGI_FLAG_LINUX_MERGE_FALLBACK) return RC2DGI_E_ARG;
   if (cfg->storage != RC2DGI_STORAGE_F32 && cfg->storage != RC2DGI_STORAGE_F16 &&
       cfg->storage != RC2DGI_STORAGE_RGBA8_COMPAT)
     return RC2DGI_E_ARG;
@@ -494,6 +496,7 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
   c->render_scale = cfg->render_scale;
   c->storage = cfg->storage;
   c->ray_range = cfg->ray_range;
+  c->linux_merge = (cfg->flags & RC2DGI_FLAG_LINUX_MERGE_FALLBACK) != 0;
   int rc = RC2DGI_OK;
   hipError_t e = hipSetDevice(c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
@@ -894,7 +897,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   if (c->blur_radius > 0.0f) {
     bool fused = false;
     BlurTaps bt;
-    const bool mrg = c->sd.W == c->CW && c->sd.H == c->CH;
+    const bool mrg = c->sd.W == c->CW && c->sd.H == c->CH && !c->linux_merge;
     // a fused kernel writes the copied-back GI into gi_spare, which then becomes finalGI: only when
     // every launch of it ran (a refused launch -- shapes it does not take -- falls back before any
     // launch ran, since the shapes are the same for every row interval)
@@ -925,7 +928,8 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   if (T) HIPCHK(c, hipEventRecord(c->ev[4], st));
   if (!merged)
     for (auto &r : plan.merge.iv)
-      HIPCHK(c, launch_merge(c->color_in, finalGI, c->temp, c->color_out, c->sd, c->cd, st, r.first, r.second));
+      HIPCHK(c, launch_merge(c->color_in, finalGI, c->temp, c->color_out, c->sd, c->cd, st, r.first, r.second,
+                             c->linux_merge));
   if (T) HIPCHK(c, hipEventRecord(c->ev[5], st));
   c->frame_done = true;
   c->have_frame = true;

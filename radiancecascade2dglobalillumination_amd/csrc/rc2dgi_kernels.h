@@ -211,10 +211,10 @@ bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Cas
                       const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
                       hipStream_t st, int row0 = 0, int row1 = -1);
 
-// merge.fs into temp, then tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
+// merge.fs into temp, then tempRT -> colorRT copy-back (RC2DGI.cs:389-404); linux_merge: raylib's default
+// shader in place of merge.fs (RC2DGI_FLAG_LINUX_MERGE_FALLBACK)
 hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,
-                        CascadeDims c, hipStream_t st, int row0 = 0,
-                        int row1 = -1);
+                        CascadeDims c, hipStream_t st, int row0 = 0, int row1 = -1, bool linux_merge = false);
 
 // format conversion for uploads from device memory: RGBA8 unorm -> float4 (k/255; u8: k*(1/255),
 // the value an RGBA8 texture fetch returns)

@@ -803,15 +803,18 @@ __global__ __launch_bounds__(256) void k_blur_copyback(const typename GI::RT::T 
 template <class GI>
 __global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_in, const typename GI::T *__restrict__ gi,
                                                float4 *__restrict__ temp, float4 *__restrict__ color_out,
-                                               ScreenDims s, CascadeDims c, int row0, int row1) {
+                                               ScreenDims s, CascadeDims c, int row0, int row1, int linux_merge) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= row1) return;
   const float u = texcoord(i, Axis{s.W, s.powW}), v = texcoord(j, Axis{s.H, s.powH});
   const size_t o = (size_t)j * s.pitch + i;
   const float4 col = color_in[o];
-  const float4 g = sample_bilinear_gi<GI>(gi, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
-  const float4 src = make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
+  float4 src = col;  // Linux: raylib's default shader, texel * colDiffuse (1) * vertex colour (1) = the texel
+  if (!linux_merge) {
+    const float4 g = sample_bilinear_gi<GI>(gi, c.pitch, Axis{c.CW, c.powW}, Axis{c.CH, c.powH}, u, v);
+    src = make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
+  }
   const float4 t = GI::RT::blend_black(src);  // tempRT as cleared by ClearAllRTs
   temp[o] = t;
   color_out[o] = GI::RT::blend(t, col);       // tempRT -> colorRT, default shader, blended
@@ -1181,18 +1184,18 @@ hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, h
 }
 
 hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,
-                        CascadeDims c, hipStream_t st, int row0, int row1) {
+                        CascadeDims c, hipStream_t st, int row0, int row1, bool linux_merge) {
   clamp_rows(s.H, row0, row1);
   if (row0 >= row1) return hipSuccess;
   if (c.gi_u8)
     hipLaunchKernelGGL(k_merge<GiU8>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in,
-                       reinterpret_cast<const GiU8::T *>(gi), temp, color_out, s, c, row0, row1);
+                       reinterpret_cast<const GiU8::T *>(gi), temp, color_out, s, c, row0, row1, (int)linux_merge);
   else if (c.gi_f16)
     hipLaunchKernelGGL(k_merge<GiF16>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in,
-                       reinterpret_cast<const GiF16::T *>(gi), temp, color_out, s, c, row0, row1);
+                       reinterpret_cast<const GiF16::T *>(gi), temp, color_out, s, c, row0, row1, (int)linux_merge);
   else
     hipLaunchKernelGGL(k_merge<GiF32>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in, gi, temp, color_out, s,
-                       c, row0, row1);
+                       c, row0, row1, (int)linux_merge);
   return hipGetLastError();
 }
 

@@ -51,7 +51,7 @@ class Prim(ctypes.Structure):
 class _Config(ctypes.Structure):
     _fields_ = [("screen_width", ctypes.c_int), ("screen_height", ctypes.c_int), ("cascade_count", ctypes.c_int),
                 ("render_scale", ctypes.c_float), ("ray_range", ctypes.c_float), ("storage", ctypes.c_int),
-                ("device", ctypes.c_int), ("reserved", ctypes.c_int * 5)]
+                ("device", ctypes.c_int), ("flags", ctypes.c_int), ("reserved", ctypes.c_int * 4)]
 
 
 _lib = None
@@ -131,13 +131,16 @@ class RC2DGI:
     """One GI context = the reference's render-texture set + DoRC2DGI() on one GPU."""
 
     def __init__(self, screen_width: int = 1200, screen_height: int = 900, cascade_count: int = 6,
-                 render_scale: float = 1.0, ray_range: float = 2.0, device: int = 0, storage: str = "f32"):
+                 render_scale: float = 1.0, ray_range: float = 2.0, device: int = 0, storage: str = "f32",
+                 linux_merge_fallback: bool = False):
         """storage: "f32" (RGBA32F render textures), "f16" (giRT1/2 as RGBA16F, RC2DGI.cs:105-106) or
-        "rgba8" (every render texture RGBA8 with GL unorm8 arithmetic -- the literal app)."""
+        "rgba8" (every render texture RGBA8 with GL unorm8 arithmetic -- the literal app).
+        linux_merge_fallback: the app on a case-sensitive filesystem, where "shaders/Merge.fs" is not
+        found (RC2DGI.cs:62) and the merge pass adds no GI to colorRT."""
         self._L = load_library()
         st = {"f32": 0, "rgba8": 1, "f16": 2}[storage]
         cfg = _Config(screen_width, screen_height, cascade_count, render_scale, ray_range, st, device,
-                      (ctypes.c_int * 5)())
+                      1 if linux_merge_fallback else 0, (ctypes.c_int * 4)())
         h = ctypes.c_void_p()
         rc = self._L.rc2dgi_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:
@@ -417,7 +420,7 @@ def plan_rows(W: int, H: int, N: int, blur_radius: float, rank: int, world: int,
     """Host-only planner: [(begin, end), ...] rows shard `rank` of `world` computes for a pass
     (PLAN_JFA + step, PLAN_LEVEL + level, PLAN_BLUR, PLAN_MERGE)."""
     L = load_library()
-    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, (ctypes.c_int * 5)())
+    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, 0, (ctypes.c_int * 4)())
     buf = (ctypes.c_int * 64)()
     n = L.rc2dgi_plan_rows(ctypes.byref(cfg), float(blur_radius), rank, world, pass_id, buf, 32)
     if n < 0:
@@ -436,7 +439,7 @@ def plan_jfa_exchange(W: int, H: int, N: int, world: int, step: int, render_scal
     JFA_INFO and the transfers [(src, src_window_row, rows, dst, dst_buf, dst_row), ...] in the order
     every shard issues them (rc2dgi_plan_jfa_exchange)."""
     L = load_library()
-    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, (ctypes.c_int * 5)())
+    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, 0, (ctypes.c_int * 4)())
     info = (ctypes.c_int * 9)()
     n = L.rc2dgi_plan_jfa_exchange(ctypes.byref(cfg), world, step, info, None, 0)
     if n < 0:
@@ -450,7 +453,7 @@ def plan_jfa_window(W: int, H: int, N: int, rank: int, world: int, step: int, re
     """Where shard `rank` reads tap y of JFA step `step`: ([buffer per tap], [global row of each
     buffer's local row 0]) (rc2dgi_plan_jfa_window)."""
     L = load_library()
-    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, (ctypes.c_int * 5)())
+    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, 0, (ctypes.c_int * 4)())
     buf, row0 = (ctypes.c_int * 3)(), (ctypes.c_int * 3)()
     rc = L.rc2dgi_plan_jfa_window(ctypes.byref(cfg), rank, world, step, buf, row0)
     if rc < 0:

@@ -33,7 +33,8 @@ def params_of(m: dict):
                          sky_radiance=m["sky_radiance"], sky_color=tuple(m["sky_color"]),
                          sun_color=tuple(m["sun_color"]), sun_angle=m["sun_angle"],
                          reflectivity=m["reflectivity"], blur_radius=m["blur_radius"],
-                         gi_f16=bool(m.get("gi_f16", False)), rgba8=bool(m.get("rgba8", False)))
+                         gi_f16=bool(m.get("gi_f16", False)), rgba8=bool(m.get("rgba8", False)),
+                         linux_merge=bool(m.get("linux_merge", False)))
 
 
 def rel_err(got: np.ndarray, want: np.ndarray, floor: float = 1e-3) -> np.ndarray:

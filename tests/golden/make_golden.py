@@ -57,6 +57,9 @@ FIXTURES = [
     ("rand128_n4_rgba8", 128, 128, 4, 2.0, "rand:6", dict(rgba8=True, blur_radius=2.5), True),
     ("rand96x64_n3_rgba8", 96, 64, 3, 4.0, "rand:7", dict(rgba8=True, reflectivity=0.4), True),
     ("rand128x64_n2_rgba8_noblur", 128, 64, 2, 4.0, "rand:8", dict(rgba8=True, blur_radius=0.0), True),
+    # the app on Linux: "shaders/Merge.fs" is not found (RC2DGI.cs:62), raylib's default
+    # shader runs the merge pass (glref --linux-merge-fallback); bright colours (> 1) show the missing clamp
+    ("rand96x64_n3_linuxmerge", 96, 64, 3, 4.0, "rand:9", dict(linux_merge=True), False),
 ]
 
 
@@ -75,6 +78,7 @@ def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
     u.update(over)
     gi_f16 = bool(u.pop("gi_f16", False))
     rgba8 = bool(u.pop("rgba8", False))
+    linux_merge = bool(u.pop("linux_merge", False))
     color, emis = make_scene(scene, W, H)
     with tempfile.TemporaryDirectory() as d:
         color.tofile(os.path.join(d, "c.f32"))
@@ -85,7 +89,8 @@ def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
         base = ["--w", str(W), "--h", str(H), "--n", str(N), "--out", d]
         subprocess.run([GLREF, "--ref-shaders", shaders, "--ray-range", str(rr), "--in-color", d + "/c.f32",
                         "--in-emissive", d + "/e.f32", "--dump", "all"] + base + uargs + (["--gi-f16"] if gi_f16 else [])
-                       + (["--mode", "rgba8", "--dump-u8"] if rgba8 else []),
+                       + (["--mode", "rgba8", "--dump-u8"] if rgba8 else [])
+                       + (["--linux-merge-fallback"] if linux_merge else []),
                        check=True)
         subprocess.run([GLREF, "--capture-tables"] + base + uargs + (["--mode", "rgba8"] if rgba8 else []), check=True)
         meta = json.load(open(os.path.join(d, "glref.json")))
@@ -116,6 +121,8 @@ def run(name, W, H, N, rr, scene, over, keep_steps, shaders):
     entry = dict(name=name, W=W, H=H, N=N, ray_range=rr, render_scale=1.0, scene=scene, CW=CW, CH=CH,
                  jfa_steps=meta["jfa_steps"], final_gi=meta["final_gi"], renderer=meta["renderer"],
                  gl_version=meta["version"], mode=meta["mode"], gi_f16=gi_f16, rgba8=rgba8, **u)
+    if linux_merge:
+        entry["linux_merge"] = True
     entry["sky_color"] = list(u["sky_color"])
     entry["sun_color"] = list(u["sun_color"])
     return entry

@@ -20,7 +20,7 @@ CS = os.path.join(ROOT, "host", "csharp", "RC2DGINative.cs")
 # to its own size, the struct to its largest field
 CS_SIZES = {"int": 4, "float": 4, "byte": 1}
 C_NAMES = {"Config": ("rc2dgi_config", ["screen_width", "screen_height", "cascade_count", "render_scale",
-                                        "ray_range", "storage", "device", "reserved"]),
+                                        "ray_range", "storage", "device", "flags", "reserved"]),
            "Prim": ("rc2dgi_prim", ["kind", "x", "y", "w", "h", "r", "g", "b", "a"])}
 
 
@@ -63,7 +63,7 @@ def test_csharp_structs_match_the_c_abi(struct):
     sizes, fields = c_layout()
     cs, cs_size = cs_layout(struct)
     assert cs_size == sizes[cname], f"{struct}: C# {cs_size} bytes, C {sizes[cname]}"
-    # the C# mirror spells the reserved array as R0..R4: fold trailing fields onto the array
+    # the C# mirror spells the reserved array as R0..R3: fold trailing fields onto the array
     i = 0
     for cf in cfields:
         off, size = fields[(cname, cf)]
