@@ -104,6 +104,8 @@ struct rc2dgi_ctx {
   uint4 *dist_n = nullptr;           // nibble-predicted copy for the "n" RC variants (k_dist_nib)
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
+  unsigned char *hitc = nullptr;     // per bound-table cell: holds a texel that passes the hit test
+  unsigned char *cdt = nullptr;      // cell distance table of the miss proofs (k_cell_dt)
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
@@ -126,6 +128,7 @@ struct rc2dgi_ctx {
                                  // only, 3 interval and screen edge
   std::vector<int> rc_tail;      // per level: tail compaction after this many lockstep iterations (tuning rc_tail_L<n>)
   int rc_wgproof = 1;            // tuning "rc_wgproof": workgroup-wide exit proof of the first samples
+  std::vector<int> rc_mp;        // per level: miss proofs in the one-probe tiles (tuning rc_mp_L<n>)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
@@ -211,7 +214,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
-                  c->cmin,     c->dexit};
+                  c->cmin,     c->dexit, c->hitc, c->cdt};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -226,6 +229,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->dist_n = nullptr;
   c->shade = nullptr;
   c->cmin = nullptr;
+  c->hitc = c->cdt = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
   c->dexit = nullptr;
@@ -319,6 +323,8 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->dist_n, dist_nib_bytes(c->W, c->H)));
   HIPCHK(c, alloc(&c->shade, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->cmin, (size_t)kCminDim * kCminDim * sizeof(CminT)));
+  HIPCHK(c, alloc(&c->hitc, (size_t)kCminDim * kCminDim));
+  HIPCHK(c, alloc(&c->cdt, (size_t)kCminDim * kCminDim));
   const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
   HIPCHK(c, alloc(&c->gi1, nc * gsz));
   HIPCHK(c, alloc(&c->gi2, nc * gsz));
@@ -343,6 +349,7 @@ int allocate(rc2dgi_ctx *c) {
   c->rc_order.resize(c->N);
   for (int L = 0; L < c->N; ++L) c->rc_order[L] = default_rc_order(L);
   c->rc_tail.assign(c->N, kDefaultTail);
+  c->rc_mp.assign(c->N, 0);
   if (int rc = jfa_buffers(c)) return rc;
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
@@ -844,7 +851,11 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   // exit proofs: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
   // staging and barrier cost more than the skipped samples save (RC 0.338 vs 0.376 ms, measured)
   const bool proofs = c->rc_skip > 1 || (c->rc_skip == 1 && std::max(c->W, c->H) >= 2048);
-  if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st));
+  bool mps = false;
+  for (int v : c->rc_mp) mps |= v != 0;
+  mps = mps && proofs;
+  if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
+  if (mps) HIPCHK(c, launch_cell_dt(c->hitc, c->cdt, st));
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
@@ -869,6 +880,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.dist_packed = c->dist_p;
     a.dist_nib = c->dist_n;
     a.cmin = proofs ? c->cmin : nullptr;
+    a.cdt = (mps && c->rc_mp[L]) ? c->cdt : nullptr;
     // the screen-edge test pays where rays are long (t1 >= 1/8 of the screen: L4 / L5 at N = 6)
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
@@ -1361,8 +1373,19 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->jfa_lds = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "rc_mp" || k.rfind("rc_mp_L", 0) == 0) {
+    if (k == "rc_mp") {
+      for (int &v : c->rc_mp) v = value != 0;
+      return RC2DGI_OK;
+    }
+    const int L = std::atoi(k.c_str() + 7);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    c->rc_mp[L] = value != 0;
+    return RC2DGI_OK;
+  }
   if (k == "rc_tail" || k.rfind("rc_tail_L", 0) == 0) {
-    if (value < 0 || value > 32) return fail(c, RC2DGI_E_ARG, "rc_tail is 0 (off) .. 32 lockstep iterations");
+    if (value < -1 || value > 32)
+      return fail(c, RC2DGI_E_ARG, "rc_tail is -1 (queue every ray) .. 0 (off) .. 32 lockstep iterations");
     if (k == "rc_tail") {
       for (int &v : c->rc_tail) v = value;
       return RC2DGI_OK;
@@ -1419,6 +1442,12 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
     const int L = std::atoi(k.c_str() + 9);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
     *value = c->rc_tail[L];
+    return RC2DGI_OK;
+  }
+  if (k.rfind("rc_mp_L", 0) == 0) {
+    const int L = std::atoi(k.c_str() + 7);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    *value = c->rc_mp[L];
     return RC2DGI_OK;
   }
   if (k.rfind("rc_order_L", 0) == 0) {

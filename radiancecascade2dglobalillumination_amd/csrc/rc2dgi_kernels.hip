@@ -425,7 +425,8 @@ __global__ __launch_bounds__(256) void k_shade(const unsigned short *__restrict_
 // whose sample lies in the cell advances by at least that much and does not stop there
 // (k_rc_level's exit proof, kCminDim).
 __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restrict__ dist, int pitch,
-                                                   CminT *__restrict__ cmin, int W, int H, int csh) {
+                                                   CminT *__restrict__ cmin, int W, int H, int csh,
+                                                   unsigned char *__restrict__ hitc) {
   const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
   unsigned m = 0xFFFFu;
   const bool in = x0 < W && y0 < H;
@@ -460,6 +461,16 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
       }
     }
   }
+  if (in) {
+    // REPEAT wrap: a march sample at u = 1 reads column 0 of its row, at v = 1 row 0 of its column, at
+    // (1, 1) texel (0, 0) -- those texels belong to the bound of the last cell column / row too
+    const int x1 = min(W, x0 + (1 << csh)), y1 = min(H, y0 + (1 << csh));
+    if (x1 == W)
+      for (int e = (int)threadIdx.x; e < y1 - y0; e += 256) m = min(m, (unsigned)dist[(size_t)(y0 + e) * pitch]);
+    if (y1 == H)
+      for (int e = (int)threadIdx.x; e < x1 - x0; e += 256) m = min(m, (unsigned)dist[x0 + e]);
+    if (x1 == W && y1 == H && threadIdx.x == 0) m = min(m, (unsigned)dist[0]);
+  }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, o, 64));
   __shared__ unsigned s_m[4];
@@ -468,12 +479,43 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
   if (threadIdx.x == 0) {
     m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
     const float d = decode_dist(m);
+    if (hitc) hitc[blockIdx.y * kCminDim + blockIdx.x] = (in && d < 0.001f) ? 1 : 0;
 #ifdef RC2DGI_CMIN_U8
     // floor(d * scale) / scale <= d (power-of-two scaling and floor are exact); 0 where a texel hits
     cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
 #else
     cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? d : 0.0f;
 #endif
+  }
+}
+
+// ---------------------------------------------------------------- cell distance table of the miss proof
+// cdt[c] = min over cells f with hitc[f] = 1 of max(|fx - cx|, |fy - cy|) (Chebyshev distance in cells, 255
+// when no cell is flagged): every cell within Chebyshev distance cdt[c] - 1 of c holds no texel a march sample
+// could hit.  Separable: the column distance h(x, y) = min |y - y'| over flagged (x, y'), then
+// cdt(x, y) = min over x' of max(|x - x'|, h(x', y)).  One workgroup, 4 KB tables in LDS.
+__global__ __launch_bounds__(1024) void k_cell_dt(const unsigned char *__restrict__ hitc,
+                                                  unsigned char *__restrict__ cdt) {
+  constexpr int D = kCminDim, NC = D * D;
+  __shared__ unsigned char f[NC], h[NC];
+  for (int i = (int)threadIdx.x; i < NC; i += 1024) f[i] = hitc[i];
+  __syncthreads();
+  for (int i = (int)threadIdx.x; i < NC; i += 1024) {
+    const int x = i % D, y = i / D;
+    int best = 255;
+    for (int yy = 0; yy < D; ++yy)
+      if (f[yy * D + x]) best = min(best, abs(y - yy));
+    h[i] = (unsigned char)best;
+  }
+  __syncthreads();
+  for (int i = (int)threadIdx.x; i < NC; i += 1024) {
+    const int x = i % D, y = i / D;
+    int best = 255;
+    for (int xx = 0; xx < D; ++xx) {
+      const int hv = h[y * D + xx];
+      if (hv != 255) best = min(best, max(abs(x - xx), hv));
+    }
+    cdt[i] = (unsigned char)best;
   }
 }
 
@@ -1199,6 +1241,11 @@ hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, 
   return hipGetLastError();
 }
 
+hipError_t launch_cell_dt(const unsigned char *hitc, unsigned char *cdt, hipStream_t st) {
+  hipLaunchKernelGGL(k_cell_dt, dim3(1), dim3(1024), 0, st, hitc, cdt);
+  return hipGetLastError();
+}
+
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,
                             hipStream_t st) {
   const int tpr = (W + 7) / 8;
@@ -1240,9 +1287,10 @@ int dist_cmin_shift(int W, int H) {
   return s;
 }
 
-hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st) {
+hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st,
+                            unsigned char *hitc) {
   hipLaunchKernelGGL(k_dist_cmin, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, pitch, cmin, W, H,
-                     dist_cmin_shift(W, H));
+                     dist_cmin_shift(W, H), hitc);
   return hipGetLastError();
 }
 

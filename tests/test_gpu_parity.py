@@ -573,3 +573,39 @@ def test_linux_merge_fallback_at_the_fused_blur_size(RC2DGI):
             g = ctx.download(k)
             assert np.array_equal(g, w), f"linux_merge={flag} {k}: {np.count_nonzero(g != w)} differ"
         ctx.close()
+
+
+@pytest.mark.parametrize("W,H,N,rr,rs,scene,storage", [
+    (512, 512, 6, 2.0, 1.0, "demo", "f32"), (333, 200, 4, 8.0, 1.0, "demo", "f32"),
+    (256, 128, 5, 64.0, 1.0, "rand:12", "f32"), (256, 256, 4, 2.0, 0.5, "rand:3", "f16"),
+    (17, 5, 2, 8.0, 1.0, "rand:9", "f32"), (1024, 1024, 6, 2.0, 1.0, "rand:5", "f32"),
+    (512, 512, 6, 2.0, 1.0, "rand:6", "rgba8"), (2048, 2048, 6, 2.0, 1.0, "demo", "f32"),
+    (64, 64, 3, 2.0, 1.0, "empty", "f32")])
+def test_miss_proofs_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene, storage):
+    """Miss proofs (tuning rc_mp: a ray whose path provably holds no texel that passes the hit test is
+    not marched; k_dist_cmin's hit cells + k_cell_dt's Chebyshev cell distances) with every tail
+    setting (-1: every unproved ray queued at once, 0 off, 10 the default) in the one-probe tile
+    variants, and the variants without them (the flag must leave those alone): every level bit-exact
+    vs the oracle (RadianceCascades.fs:60-92: a miss returns (0,0,0,1) however it ends)."""
+    color, emis = make_scene(scene, W, H)
+    if storage == "rgba8":
+        color, emis = oracle.from_u8(np.rint(np.clip(color, 0, 1) * 255)), oracle.from_u8(np.rint(np.clip(emis, 0, 1) * 255))
+    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr, render_scale=rs, **mode_params(storage)), color, emis,
+                      keep_levels=True)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr, render_scale=rs, storage=storage)
+    ctx.set_keep_levels(True)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    ctx.set_tuning("rc_skip", 2)  # bound tables at every size
+    ctx.set_tuning("rc_mp", 1)
+    for v in (0, 3, 4, 13, 18, 19, 6):
+        ctx.set_tuning("rc_variant", v)
+        for tail in (-1, 0, 10):
+            ctx.set_tuning("rc_tail", tail)
+            ctx.do_rc2dgi()
+            ctx.sync()
+            for L in range(N):
+                g = ctx.download_level(L)
+                assert np.array_equal(g, fr.gi_levels[L]), \
+                    f"variant {v} tail {tail} level {L}: {np.count_nonzero(np.any(g != fr.gi_levels[L], axis=-1))} differ"
+    ctx.close()
