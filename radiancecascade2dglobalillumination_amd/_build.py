@@ -86,21 +86,14 @@ if __name__ == "__main__":
     elif len(sys.argv) > 1 and sys.argv[1] == "nomerge":
         # timing-only ablation build: RC levels without the upper-cascade staging and merge (WRONG results)
         print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_NOMERGE"], out=os.path.join(ROOT, "build", "diag", "librc2dgi_nomerge.so")))
-    elif len(sys.argv) > 1 and sys.argv[1] == "escplain":
-        # diagnostic build reproducing DESIGN.md §5.3: packed-field escape loads waited for at the branch
-        # join (WRONG, run-to-run different results on gfx950).  Extra flags after the mode are passed on.
-        print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_ESC_PLAIN"] + sys.argv[2:],
-                    out=os.path.join(ROOT, "build", "diag", "librc2dgi_escplain.so")))
-    elif len(sys.argv) > 2 and sys.argv[1] == "escform":
-        # diagnostic builds separating the two changes of the §5.3 fix: "vaddr" = compiler-scheduled escape
-        # loads with a 64-bit VGPR address (waited at the join), "saddrwait" = scalar-base form waited at once
-        form = {"vaddr": "RC2DGI_DIAG_ESC_VADDR", "saddrwait": "RC2DGI_DIAG_ESC_SADDR_WAIT"}[sys.argv[2]]
-        print(build(force=True, verbose=True, extra=[f"-D{form}"],
-                    out=os.path.join(ROOT, "build", "diag", f"librc2dgi_esc{sys.argv[2]}.so")))
     elif len(sys.argv) > 2 and sys.argv[1] == "exp":
         # A/B build of an experiment: build/ab/librc2dgi_<name>.so with the flags given (scripts/ab_lib.sh)
         print(build(force=True, verbose=True, extra=sys.argv[3:],
                     out=os.path.join(ROOT, "build", "ab", f"librc2dgi_{sys.argv[2]}.so")))
+    elif len(sys.argv) > 1 and sys.argv[1] == "timing":
+        # diagnostic build: k_rc_level wave-lifetime split by section (s_memtime; scripts/rc_timing.py)
+        print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_TIMING"] + sys.argv[2:],
+                    out=os.path.join(ROOT, "build", "diag", "librc2dgi_timing.so")))
     elif len(sys.argv) > 1 and sys.argv[1] == "stats":
         # diagnostic build: march statistics per level (rc2dgi_diag_stats; atomics, slower)
         print(build(force=True, verbose=True, extra=["-DRC2DGI_DIAG_STATS"], out=os.path.join(ROOT, "build", "diag", "librc2dgi_stats.so")))

@@ -105,7 +105,7 @@ struct rc2dgi_ctx {
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
   unsigned char *hitc = nullptr;     // per bound-table cell: holds a texel that passes the hit test
-  unsigned char *cdt = nullptr;      // cell distance table of the miss proofs (k_cell_dt)
+  unsigned char *dclr = nullptr;     // directional clear distances of the miss proofs (k_dir_clear)
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
@@ -128,7 +128,7 @@ struct rc2dgi_ctx {
                                  // only, 3 interval and screen edge
   std::vector<int> rc_tail;      // per level: tail compaction after this many lockstep iterations (tuning rc_tail_L<n>)
   int rc_wgproof = 1;            // tuning "rc_wgproof": workgroup-wide exit proof of the first samples
-  std::vector<int> rc_mp;        // per level: miss proofs in the one-probe tiles (tuning rc_mp_L<n>)
+  std::vector<int> rc_mp;        // per level: directional miss proofs in the one-probe tiles (tuning rc_mp_L<n>)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
@@ -214,7 +214,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
-                  c->cmin,     c->dexit, c->hitc, c->cdt};
+                  c->cmin,     c->dexit, c->hitc, c->dclr};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -229,7 +229,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->dist_n = nullptr;
   c->shade = nullptr;
   c->cmin = nullptr;
-  c->hitc = c->cdt = nullptr;
+  c->hitc = c->dclr = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
   c->dexit = nullptr;
@@ -324,7 +324,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->shade, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->cmin, (size_t)kCminDim * kCminDim * sizeof(CminT)));
   HIPCHK(c, alloc(&c->hitc, (size_t)kCminDim * kCminDim));
-  HIPCHK(c, alloc(&c->cdt, (size_t)kCminDim * kCminDim));
+  HIPCHK(c, alloc(&c->dclr, (size_t)kDirBins * kCminDim * kCminDim));
   const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
   HIPCHK(c, alloc(&c->gi1, nc * gsz));
   HIPCHK(c, alloc(&c->gi2, nc * gsz));
@@ -349,7 +349,7 @@ int allocate(rc2dgi_ctx *c) {
   c->rc_order.resize(c->N);
   for (int L = 0; L < c->N; ++L) c->rc_order[L] = default_rc_order(L);
   c->rc_tail.assign(c->N, kDefaultTail);
-  c->rc_mp.assign(c->N, 0);
+  c->rc_mp.assign(c->N, 1);  // directional miss proofs wherever they apply (one-probe tiles, 4^L >= kDirBins)
   if (int rc = jfa_buffers(c)) return rc;
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
@@ -855,7 +855,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   for (int v : c->rc_mp) mps |= v != 0;
   mps = mps && proofs;
   if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
-  if (mps) HIPCHK(c, launch_cell_dt(c->hitc, c->cdt, st));
+  if (mps) HIPCHK(c, launch_dir_clear(c->hitc, c->dclr, c->W, c->H, st));
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
@@ -880,7 +880,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.dist_packed = c->dist_p;
     a.dist_nib = c->dist_n;
     a.cmin = proofs ? c->cmin : nullptr;
-    a.cdt = (mps && c->rc_mp[L]) ? c->cdt : nullptr;
+    a.dclr = (mps && c->rc_mp[L]) ? c->dclr : nullptr;
     // the screen-edge test pays where rays are long (t1 >= 1/8 of the screen: L4 / L5 at N = 6)
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];

@@ -125,7 +125,8 @@ struct RcLevelArgs {
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
   const uint4 *dist_nib = nullptr;             // nibble-predicted distance field (variants "n", k_dist_nib)
   const CminT *cmin = nullptr;  // coarse lower bound of the field (launch_dist_cmin); nullptr: no exit proofs
-  const unsigned char *cdt = nullptr;  // cell distance table (launch_cell_dt); non-null: miss proofs (one-probe tiles)
+  const unsigned char *dclr = nullptr;  // directional clear distances (launch_dir_clear): the one-probe tiles prove
+                                       // misses with them instead of cmin (levels with 4^L >= kDirBins)
   int cmin_screen = 0;          // the exit proof also tests the screen edge (worth it for long rays)
   int tail_k = 0;               // tail compaction after this many lockstep march iterations (0: off)
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
@@ -136,9 +137,10 @@ int dist_cmin_shift(int W, int H);
 // u = 1 / v = 1 onto column / row 0 included in the last cell column / row), else 0
 hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st,
                             unsigned char *hitc = nullptr);
-// Miss proofs (k_rc_level): cdt[c] = Chebyshev distance, in cells, from cell c to the nearest cell with
-// hitc = 1 (255: none), kCminDim x kCminDim bytes
-hipError_t launch_cell_dt(const unsigned char *hitc, unsigned char *cdt, hipStream_t st);
+// Directional clear distances of the march proofs (k_rc_level, one-probe tiles): kDirBins angular bins x
+// kCminDim^2 cells, bytes (k_dir_clear)
+constexpr int kDirBins = 64;
+hipError_t launch_dir_clear(const unsigned char *hitc, unsigned char *dclr, int W, int H, hipStream_t st);
 
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,

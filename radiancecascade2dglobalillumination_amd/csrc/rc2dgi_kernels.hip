@@ -489,34 +489,75 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
   }
 }
 
-// ---------------------------------------------------------------- cell distance table of the miss proof
-// cdt[c] = min over cells f with hitc[f] = 1 of max(|fx - cx|, |fy - cy|) (Chebyshev distance in cells, 255
-// when no cell is flagged): every cell within Chebyshev distance cdt[c] - 1 of c holds no texel a march sample
-// could hit.  Separable: the column distance h(x, y) = min |y - y'| over flagged (x, y'), then
-// cdt(x, y) = min over x' of max(|x - x'|, h(x', y)).  One workgroup, 4 KB tables in LDS.
-__global__ __launch_bounds__(1024) void k_cell_dt(const unsigned char *__restrict__ hitc,
-                                                  unsigned char *__restrict__ cdt) {
-  constexpr int D = kCminDim, NC = D * D;
-  __shared__ unsigned char f[NC], h[NC];
-  for (int i = (int)threadIdx.x; i < NC; i += 1024) f[i] = hitc[i];
-  __syncthreads();
-  for (int i = (int)threadIdx.x; i < NC; i += 1024) {
-    const int x = i % D, y = i / D;
-    int best = 255;
-    for (int yy = 0; yy < D; ++yy)
-      if (f[yy * D + x]) best = min(best, abs(y - yy));
-    h[i] = (unsigned char)best;
+// ---------------------------------------------------------------- directional clear distances (march proofs)
+// dclr[j][c] = s: from any point of cell c (kCminDim x kCminDim cells of 2^csh texels, k_dist_cmin's grid) and
+// for every direction of angular bin j (angles [2 pi j / kDirBins, 2 pi (j + 1) / kDirBins)), the ray stays
+// clear of the cells holding a texel that passes the hit test (hitc, REPEAT wrap included) for s cells of
+// distance (s * 2^csh texels); 255: the whole grid.  Step s covers radii [s C, (s + 1) C) texels: the points
+// u + d r (u in the cell, d in the bin, r in the step) lie in the box of the four chord corners grown by
+// the sagitta r (1 - cos(dtheta / 2)) and one texel (the fp32 rounding of positions and directions), and
+// the step's cells are the cells that box touches.  Cells off the grid are off screen: never sampled.
+// One thread per (bin, cell): kDirBins x 16 workgroups of 256 cells (a quarter of the grid rows each); the
+// flag grid as one 64-bit word per row in LDS.
+__global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restrict__ hitc,
+                                                   unsigned char *__restrict__ dclr, int csh) {
+  constexpr int D = kCminDim, NS = kCminDim;
+  static_assert(D == 64, "one 64-bit word per row");
+  __shared__ unsigned short part[D * 4];      // 16-cell pieces of the rows
+  __shared__ int box[NS][4];                   // per step: cell offsets x0, x1, y0, y1 relative to the start cell
+  const int j = blockIdx.x >> 4, c = (int)((blockIdx.x & 15) * 256 + threadIdx.x);
+  {  // thread t packs cells 16 t .. 16 t + 15 (row t / 4, piece t % 4)
+    const uint4 v = reinterpret_cast<const uint4 *>(hitc)[threadIdx.x];
+    unsigned m = 0;
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) m |= ((w[q >> 2] >> (8 * (q & 3))) & 0xFFu) ? 1u << q : 0u;
+    part[threadIdx.x] = (unsigned short)m;
+  }
+  if (threadIdx.x < NS) {
+    const double C = (double)(1 << csh), PI2 = 6.283185307179586;
+    const double ta = PI2 * j / kDirBins, tb = PI2 * (j + 1) / kDirBins;
+    const double sag = 1.0 - cos(0.5 * (tb - ta));
+    const double r0 = threadIdx.x * C, r1 = (threadIdx.x + 1) * C;
+    double lox = 1e30, hix = -1e30, loy = 1e30, hiy = -1e30;
+    const double ds[2][2] = {{cos(ta), sin(ta)}, {cos(tb), sin(tb)}};
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b) {
+        const double r = b ? r1 : r0;
+        lox = fmin(lox, ds[a][0] * r);
+        hix = fmax(hix, ds[a][0] * r);
+        loy = fmin(loy, ds[a][1] * r);
+        hiy = fmax(hiy, ds[a][1] * r);
+      }
+    const double m = r1 * sag + 1.0;
+    box[threadIdx.x][0] = (int)floor((lox - m) / C);
+    box[threadIdx.x][1] = (int)floor((hix + m + C - 1e-6) / C);
+    box[threadIdx.x][2] = (int)floor((loy - m) / C);
+    box[threadIdx.x][3] = (int)floor((hiy + m + C - 1e-6) / C);
   }
   __syncthreads();
-  for (int i = (int)threadIdx.x; i < NC; i += 1024) {
-    const int x = i % D, y = i / D;
-    int best = 255;
-    for (int xx = 0; xx < D; ++xx) {
-      const int hv = h[y * D + xx];
-      if (hv != 255) best = min(best, max(abs(x - xx), hv));
+  __shared__ unsigned long long rows[D];
+  if (threadIdx.x < D)
+    rows[threadIdx.x] = (unsigned long long)part[4 * threadIdx.x] | (unsigned long long)part[4 * threadIdx.x + 1] << 16 |
+                        (unsigned long long)part[4 * threadIdx.x + 2] << 32 |
+                        (unsigned long long)part[4 * threadIdx.x + 3] << 48;
+  __syncthreads();
+  const int cx = c % D, cy = c / D;
+  int clear = 255;
+  for (int s = 0; s < NS; ++s) {
+    const int bx0 = cx + box[s][0], bx1 = cx + box[s][1], by0 = cy + box[s][2], by1 = cy + box[s][3];
+    // the boxes move outwards along the bin's directions: once one lies wholly off the grid, so do the next
+    if (bx1 < 0 || bx0 > D - 1 || by1 < 0 || by0 > D - 1) break;
+    const int x0 = max(0, bx0), x1 = min(D - 1, bx1), y0 = max(0, by0), y1 = min(D - 1, by1);
+    const unsigned long long mask = (x1 - x0 == 63 ? ~0ull : ((1ull << (x1 - x0 + 1)) - 1ull)) << x0;
+    bool hit = false;
+    for (int y = y0; y <= y1 && !hit; ++y) hit = (rows[y] & mask) != 0;
+    if (hit) {
+      clear = s;
+      break;
     }
-    cdt[i] = (unsigned char)best;
   }
+  dclr[(size_t)j * D * D + c] = (unsigned char)clear;
 }
 
 // ---------------------------------------------------------------- tiled distance field
@@ -1068,19 +1109,25 @@ bool rc_variant_packed(int v) { return v == 16 || v == 18; }
 bool rc_variant_nib(int v) { return v == 17 || v == 19; }
 const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
-#ifdef RC2DGI_DIAG_STATS
-// the diagnostic counters (one device buffer per process, zeroed when made)
+#if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
+// the diagnostic counters (one device buffer per process, zeroed when made): [16 levels][16], then (timing
+// builds) kDiagSlots copies of it that rc2dgi_diag_stats sums
+#ifdef RC2DGI_DIAG_TIMING
+constexpr size_t kDiagWords = 256 * (1 + (size_t)kDiagSlots);
+#else
+constexpr size_t kDiagWords = 256;
+#endif
 unsigned long long *diag_stats_buffer() {
   static unsigned long long *d = nullptr;
-  if (!d && hipMalloc(&d, 16 * 3 * sizeof(unsigned long long)) == hipSuccess)
-    (void)hipMemset(d, 0, 16 * 3 * sizeof(unsigned long long));
+  if (!d && hipMalloc(&d, kDiagWords * sizeof(unsigned long long)) == hipSuccess)
+    (void)hipMemset(d, 0, kDiagWords * sizeof(unsigned long long));
   return d;
 }
 #endif
 
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
   RcParams P;
-#ifdef RC2DGI_DIAG_STATS
+#if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   P.stats = diag_stats_buffer();
 #endif
   P.s = s;
@@ -1241,8 +1288,8 @@ hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, 
   return hipGetLastError();
 }
 
-hipError_t launch_cell_dt(const unsigned char *hitc, unsigned char *cdt, hipStream_t st) {
-  hipLaunchKernelGGL(k_cell_dt, dim3(1), dim3(1024), 0, st, hitc, cdt);
+hipError_t launch_dir_clear(const unsigned char *hitc, unsigned char *dclr, int W, int H, hipStream_t st) {
+  hipLaunchKernelGGL(k_dir_clear, dim3(kDirBins * 16), dim3(256), 0, st, hitc, dclr, dist_cmin_shift(W, H));
   return hipGetLastError();
 }
 
@@ -1315,12 +1362,19 @@ hipError_t launch_quantize_u8(float4 *buf, int pitch, int W, int H, hipStream_t 
 
 }  // namespace rc2dgi
 
-#ifdef RC2DGI_DIAG_STATS
-extern "C" int rc2dgi_diag_stats(unsigned long long *out, int reset) {
+#if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
+extern "C" int rc2dgi_diag_stats(unsigned long long *out, int reset) {  // out: [16][16]
   hipDeviceSynchronize();
   unsigned long long *d = rc2dgi::diag_stats_buffer();
-  if (!d || hipMemcpy(out, d, 16 * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -3;
-  if (reset && hipMemset(d, 0, 16 * 3 * sizeof(unsigned long long)) != hipSuccess) return -3;
+  if (!d) return -3;
+  std::vector<unsigned long long> h(rc2dgi::kDiagWords);
+  if (hipMemcpy(h.data(), d, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -3;
+  for (int i = 0; i < 256; ++i) {
+    unsigned long long s = h[i];
+    for (size_t c = 256 + i; c < h.size(); c += 256) s += h[c];
+    out[i] = s;
+  }
+  if (reset && hipMemset(d, 0, h.size() * sizeof(unsigned long long)) != hipSuccess) return -3;
   return 0;
 }
 #endif

@@ -26,16 +26,27 @@ struct RcParams {
   const uint2 *wg_map;  // workgroup -> (tile x | y << 16, direction group), host-built (XCD remap + order)
   int tpr;              // 8x8 tiles per row of the tiled distance field (TILED)
   const float4 *cmin;   // coarse lower bound of the field (kCminDim^2 CminT entries as float4), nullptr: off
-  const float4 *cdt;    // cell distance table (k_cell_dt, kCminDim^2 bytes as float4): miss proofs, nullptr: off
+  const float4 *dclr;   // directional clear distances (k_dir_clear, kDirBins slices of kCminDim^2 bytes), nullptr: off
+  float kclr;           // interval length of one cell of clear distance: cell texels / texels per unit t
   const float4 *dexit;  // screen-exit terms per direction of the level (rc_exit_terms)
   int csh;              // its cells are 2^csh texels square
   int cscr;             // the exit proof tests the screen edge too
   int tailk;            // tail compaction after this many lockstep iterations (0: off)
   int wgp;              // workgroup-wide exit proof of the first samples
-#ifdef RC2DGI_DIAG_STATS
-  unsigned long long *stats;  // diagnostic builds: [16][3] counters (rc2dgi_diag_stats)
+#if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
+  unsigned long long *stats;  // diagnostic builds: [16 levels][16] counters (rc2dgi_diag_stats)
 #endif
 };
+
+// Diagnostic build (-DRC2DGI_DIAG_TIMING, python _build.py timing): wave-lifetime split of k_rc_level by
+// section, s_memtime stamps; lane 0 of every wave adds the cycles of section i to stats[level][i] and
+// counts the wave in stats[level][15] (scripts/rc_timing.py)
+#ifdef RC2DGI_DIAG_TIMING
+constexpr int kDiagSlots = 4096;  // copies of the [16][16] table the waves add into (summed on the host)
+#define RC_TSTAMP(i) rc_ts[i] = __builtin_amdgcn_s_memtime()
+#else
+#define RC_TSTAMP(i)
+#endif
 
 // q / 65535 exactly as the fp32 division of RadianceCascades.fs:32 gives it: one reciprocal
 // multiply and one fma residual correction reproduce the correctly rounded quotient for every
@@ -152,6 +163,23 @@ __device__ __forceinline__ float exit_bound(float t1n, bool scr, float4 e, float
   return scr ? fminf(t1n, fminf((e.z - ox) * e.x, (e.w - oy) * e.y)) : t1n;
 }
 
+// A wave-uniform read of a table the kernel never writes (workgroup map, directions, exit terms, sky),
+// through the constant address space: always a scalar load (lgkmcnt), never a vector load that would
+// have to wait behind the staging loads in flight (vmcnt retires in order) -- left to itself the
+// compiler picks the vector form as soon as some earlier instruction may clobber memory.
+template <class T>
+__device__ __forceinline__ T ld_uniform(const T *p) {
+  static_assert(sizeof(T) % 4 == 0, "whole dwords");
+  using W = const __attribute__((address_space(4))) unsigned;
+  W *q = (W *)(unsigned long long)p;
+  unsigned w[sizeof(T) / 4];
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) w[i] = q[i];
+  T v;
+  __builtin_memcpy(&v, w, sizeof(T));
+  return v;
+}
+
 // floor(x) as an int in one instruction (x finite, within int range)
 __device__ __forceinline__ int cvt_floor(float x) {
   int r;
@@ -173,34 +201,13 @@ __device__ __forceinline__ int cvt_floor(float x) {
 __device__ __forceinline__ unsigned ld_dist(const unsigned short *dist, unsigned off) {
   return *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + off);
 }
-// The 16-bit field read of an escaped packet sample, waited for right after it is issued.  A
-// wave's escape loads are issued under per-ray EXEC masks (the escape branch is divergent); left in
-// flight together and waited for at the branch join, as the compiler schedules them, some of them
-// return wrong data on gfx950 when other workgroups share the CU (reproduced on the
-// rolled and unrolled packed marches; the compiler's waitcnts are correct, a forced-zero waitcnt build
-// and L1-bypassing cache scopes still fail, one workgroup per CU or this immediate wait do not).
-// Escapes are rare at the sizes the packed marches are picked for, so the wait costs nothing there.
+// The 16-bit field read of an escaped packet sample, waited for right after it is issued (64-bit VGPR
+// address, one load in flight).  Round 1-2 builds that left a wave's escape loads in flight together
+// under their per-ray EXEC masks (scalar-base form, destination = address register for three of the
+// four) returned wrong texels on gfx950 with several workgroups per CU; the current code generation
+// no longer reproduces it in any form.  Escapes are rare at the sizes the packed
+// marches are picked for, so the wait costs nothing there.
 __device__ __forceinline__ unsigned ld_dist_esc(const unsigned short *dist, unsigned off) {
-#ifdef RC2DGI_DIAG_ESC_PLAIN  // diagnostic build reproducing the failure: a plain load, waited at the join
-  return ld_dist(dist, off);
-#endif
-#ifdef RC2DGI_DIAG_ESC_VADDR  // diagnostic: compiler-scheduled load (waited at the join), 64-bit VGPR address
-  {
-    const unsigned long long b = reinterpret_cast<unsigned long long>(dist);
-    unsigned lo, hi;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "s"((unsigned)b));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(hi) : "s"((unsigned)(b >> 32)));
-    const unsigned long long vb = ((unsigned long long)hi << 32 | lo) + off;
-    return *reinterpret_cast<const __attribute__((address_space(1))) unsigned short *>(vb);
-  }
-#endif
-#ifdef RC2DGI_DIAG_ESC_SADDR_WAIT  // diagnostic: scalar-base + 32-bit offset form, waited right after issue
-  {
-    unsigned v;
-    asm volatile("global_load_ushort %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(off), "s"(dist) : "memory");
-    return v;
-  }
-#endif
   unsigned v;
   const unsigned short *p = reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + off);
   asm volatile("global_load_ushort %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
@@ -214,7 +221,6 @@ __device__ __forceinline__ unsigned ld_dist_esc(const unsigned short *dist, unsi
 // 234 over the demo and random scenes).  The 1.14 B/texel layout puts 112 texels of a row in one
 // 128-byte line instead of 64, and the field (19 MB at 4096^2 instead of 32 MB) fits the L2s better.
 constexpr int kPackTexels = 14;
-constexpr int kMissSteps = 32;  // coarse steps of a ray's miss proof before it gives up (and marches)
 __host__ __device__ __forceinline__ int pack_per_row(int W) { return (W + kPackTexels - 1) / kPackTexels; }
 // ix / 14 for 0 <= ix < 16384 (37450 / 2^19 overestimates 1/14 by 2.3e-5: never crosses an integer)
 __device__ __forceinline__ unsigned pack_div14(unsigned ix) { return __umul24(ix, 37450u) >> 19; }
@@ -302,6 +308,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                      const float4 *__restrict__ sky,
                                                      const uint4 *__restrict__ dpk) {
   RC_SECTION("setup");
+#ifdef RC2DGI_DIAG_TIMING
+  unsigned long long rc_ts[8];
+#endif
+  RC_TSTAMP(0);
   constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
   constexpr bool TILED = DL == 1, PACKED = DL == 2 || DL == 3;
   // plain 16-bit field: the march carries byte offsets into it (twice the texel index; the
@@ -334,27 +344,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr int CMN = kCminDim * kCminDim;
   __shared__ __attribute__((aligned(16))) CminT s_cm[CMS ? CMN : 1];
   constexpr bool TLC = !Z0 && NR == 4;  // one probe and one direction block per lane (the high-level tiles)
-  // Miss proofs (one-probe tiles, P.cdt; they replace the exit proofs there, same LDS table slot).  A ray
-  // that hits nothing returns (0,0,0,1) however it ends (interval, screen edge or iteration cap), so
-  // a proof that no sample of the ray can pass the hit test replaces its whole march.  The table holds,
-  // per cell, the Chebyshev distance k (in cells) to the nearest cell holding a texel that passes the
-  // hit test (k_dist_cmin / k_cell_dt).  From a point of the ray in a cell with k >= 2, every point
-  // within max-norm distance (k - 1) * cell - 1 texels lies in a cell within k - 1 of it (the texel of
-  // slack covers the rounding of the positions), so the ray advances that far without a hit candidate;
-  // a ray that gets past t1 or off the screen this way (positions are monotone along it) never samples
-  // a hit.  At L4 on the demo scene 74 % of the rays are proved in 1.8 steps on average
-  // (scripts/missproof_model.py).
-  const bool mp = TLC && P.cdt != nullptr;
-  const bool cm = CMS && P.cmin != nullptr && !mp;
-  const float4 *ctab = mp ? P.cdt : P.cmin;
-  constexpr int CM4 = CMN * (int)sizeof(CminT) / 16;  // 16-byte pieces of the table
-  constexpr int CPT = CMS ? (CM4 + NT - 1) / NT : 1;  // per thread
-  float4 cmv[CPT];
-  if (cm || mp) {
-#pragma unroll
-    for (int j = 0; j < CPT; ++j)
-      if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4) cmv[j] = ctab[threadIdx.x + j * NT];
-  }
   // Tail compaction.  A lane marches its NR rays in lockstep and a wave runs until its longest ray
   // ends, so the few rays that pass close to a surface (steps shrink, then grow geometrically) set
   // the loop count of the whole wave: at L4 the waves run ~1.8x the iterations of their average
@@ -373,10 +362,34 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
   // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
-  const uint2 wgm = P.wg_map[blockIdx.x];
+  const uint2 wgm = ld_uniform(P.wg_map + blockIdx.x);
   const int tx = (int)(wgm.x & 0xFFFFu), ty = (int)(wgm.x >> 16), dgi = (int)wgm.y;
   (void)ngrp;
   const int bi0 = dgi * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
+  // Directional miss proofs (one-probe tiles at levels with 4^L >= kDirBins, P.dclr; they replace the
+  // exit proofs there, in the same LDS slot).  A ray that hits nothing returns (0,0,0,1) however its
+  // march ends (interval, screen edge, iteration cap), so a sample from which no later sample can pass
+  // the hit test ends the ray unread.  The workgroup's four directions lie in one angular bin of
+  // k_dir_clear's table (bins are unions of direction blocks at these levels); its 4 KB slice gives, per
+  // cell, a distance s such that from any point of the cell along any direction of the bin the ray meets
+  // no cell holding a hit-test texel within s cells.  So a sample at t with t + s * kclr >= te (te: the
+  // exit bound, successor of t1 or the screen edge) ends its ray: every later sample t' < te lies closer
+  // than s cells (kclr = cell texels / texels per unit t).  The test of a ray's first sample proves most
+  // misses before any gather (at L4 on the demo scene 72 % of the rays; samples per ray 2.10 -> 1.24 with
+  // the per-sample test, scripts/dirproof_model.py).
+  const bool dp = TLC && P.dclr != nullptr;
+  const bool cm = CMS && P.cmin != nullptr && !dp;
+  // (one bin per workgroup: bi0 * kDirBins / 4^L, exact for 4^L >= kDirBins)
+  const float4 *ctab = dp ? P.dclr + (size_t)((bi0 * kDirBins) >> (2 * P.level)) * (CMN / 16) : P.cmin;
+  constexpr int CM4 = CMN * (int)sizeof(CminT) / 16;  // 16-byte pieces of the table
+  constexpr int CPT = CMS ? (CM4 + NT - 1) / NT : 1;  // per thread
+  float4 cmv[CPT];
+  if (cm || dp) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+      if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4) cmv[j] = ctab[threadIdx.x + j * NT];
+  }
+
   const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
   const int cx = cx0 + (int)(threadIdx.x % TX);
   const int cyb = cy0 + (int)(threadIdx.x / TX);
@@ -442,19 +455,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
   };
   if constexpr (!Z0) stage_loads();
-  if (cm || mp || tl) {  // the bound table to LDS; its loads were issued first (vmcnt retires in order,
-                         // so this waits for them only, not for the staging loads in flight over the march)
-    if (cm || mp) {
-#pragma unroll
-      for (int j = 0; j < CPT; ++j)
-        if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4)
-          reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
-    }
-    if (tl && threadIdx.x == 0) s_qn = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-  }
 
   const float cxf = (float)cx;
   const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);  // rayOrigin / _CascadeResolution
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   float rdx[ND], rdy[ND];
 #pragma unroll
   for (int r = 0; r < ND; ++r) {
-    const float2 d = dirs[bi0 * 4 + r];
+    const float2 d = ld_uniform(dirs + bi0 * 4 + r);
     rdx[r] = d.x;
     rdy[r] = d.y;
     if constexpr (TLC) {  // VGPR copies: the wave-uniform directions otherwise pin 8 SGPRs over the march
@@ -506,39 +506,23 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (!on_screen<P2S>(pxy.x, pxy.y)) t[k] = kDone;
       }
     }
-    if (mp) {  // the miss proof (see mp above): a few coarse steps per ray, the rays in lockstep
-      float rate[ND];  // interval parameter per texel of max-norm advance, per direction
-#pragma unroll
-      for (int r = 0; r < ND; ++r) rate[r] = 1.0f / fmaxf(fabsf(rdx[r]) * P.aspy * P.sWf, fabsf(rdy[r]) * P.aspx * P.sHf);
-      float tc[NR];
-      unsigned pend = 0;  // bit k: ray k is still being traced
-#pragma unroll
-      for (int k = 0; k < NR; ++k) {
-        tc[k] = t[k];
-        pend |= t[k] < kDone ? 1u << k : 0u;
-      }
-      for (int s = 0; s < kMissSteps && pend; ++s) {
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-          if (!((pend >> k) & 1u)) continue;
-          const int r = k % ND;
-          const f2v_t pxy = f2v_t{ox, oy[k / ND]} + (f2v_t{tc[k], tc[k]} * f2v_t{rdx[r], rdy[r]}) * f2v_t{P.aspy, P.aspx};
-          if (tc[k] > P.t1 || !on_screen<P2S>(pxy.x, pxy.y)) {  // no sample from here on: proved
-            t[k] = kDone;
-            pend &= ~(1u << k);
-            continue;
-          }
-          const int ix = min(cvt_floor(pxy.x * P.sWf), P.s.W - 1), iy = min(cvt_floor(pxy.y * P.sHf), P.s.H - 1);
-          const int kc = s_cm[(iy >> P.csh) * kCminDim + (ix >> P.csh)];
-          if (kc <= 1) {  // a hit candidate within reach: the ray marches from t0
-            pend &= ~(1u << k);
-            continue;
-          }
-          tc[k] = tc[k] + (float)(((kc - 1) << P.csh) - 1) * rate[r];
-        }
-      }
-    }
   }
+  // The bound table to LDS and the workgroup barrier, as late as their first use: the table's load was
+  // issued first (vmcnt retires in order, so this waits for it only, not for the staging loads in
+  // flight over the march), and its latency overlaps the ray setup above.
+  if (cm || dp || tl) {
+    if (cm || dp) {
+#pragma unroll
+      for (int j = 0; j < CPT; ++j)
+        if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4)
+          reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
+    }
+    if (tl && threadIdx.x == 0) s_qn = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  }
+  RC_TSTAMP(1);
   // Workgroup-wide exit proof: a ray's first sample o + (t0 dir) asp lies within t0 (uv) of its
   // probe on each axis, so inside the tile's probe box grown by t0.  When every bound-table cell
   // under that box proves exit for a first sample (dl > 0 and t0 + dl > t1: every sample there
@@ -626,9 +610,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // them and test the screen at t + dl instead)
   float tend[TLC ? NR : 1];
   if constexpr (TLC) {
-    if (cm) {
+    if (cm || dp) {
+      struct E4 {
+        float4 e[4];
+      };
+      const E4 e4 = ld_uniform(reinterpret_cast<const E4 *>(P.dexit + bi0 * 4));  // one 64-byte scalar load
 #pragma unroll
-      for (int k = 0; k < NR; ++k) tend[k] = exit_bound(t1n, P.cscr, P.dexit[bi0 * 4 + k % ND], ox, oy[k / ND]);
+      for (int k = 0; k < NR; ++k) tend[k] = exit_bound(t1n, dp || P.cscr, e4.e[k % ND], ox, oy[k / ND]);
     }
   }
   bool more = false;  // a ray of this lane still marches
@@ -636,6 +624,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   for (int k = 0; k < NR; ++k) more |= t[k] < kDone;
   const int itend = tl ? max(0, min(P.tailk, RC2DGI_DIAG_MAX_ITERS)) : RC2DGI_DIAG_MAX_ITERS;
   RC_SECTION("march");
+  RC_TSTAMP(2);
   // BOFF with P2S: floor(p * 2W) & (2W - 2) = 2 (floor(p W) & (W - 1)) (p W and p 2W are exact)
   const float sWx = (BOFF && P2S) ? 2.0f * P.sWf : P.sWf;
   const int wmask = (BOFF && P2S) ? 2 * P.s.W - 2 : P.s.W - 1;
@@ -679,10 +668,14 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       ciy[k] = iy;
     }
     if constexpr (TLC) {
-      if (cm) {  // exit proof (see s_cm, exit_bound): the table reads together, one wait
+      if (cm || dp) {  // exit proof (see s_cm, exit_bound) or directional miss proof (see dp): the table
+                       // reads together, one wait
         float dl[NR];
 #pragma unroll
-        for (int k = 0; k < NR; ++k) dl[k] = cmin_value(s_cm[((ciy[k] >> P.csh) * kCminDim) + (cix[k] >> xsh)]);
+        for (int k = 0; k < NR; ++k) {
+          const CminT e = s_cm[((ciy[k] >> P.csh) * kCminDim) + (cix[k] >> xsh)];
+          dl[k] = dp ? (float)e * P.kclr : cmin_value(e);
+        }
 #pragma unroll
         for (int k = 0; k < NR; ++k) live[k] = live[k] && !(t[k] + dl[k] >= tend[k]);
       }
@@ -768,6 +761,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #endif
 
   RC_SECTION("tail");
+  RC_TSTAMP(3);
   int qpos[TLC ? NR : 1];  // queue entry of each pending ray of this lane
   if (tl) {
     // pending rays (still marching after itend iterations) -> LDS queue, wave-contiguous ranges
@@ -811,7 +805,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         qdy = r == q2 ? rdy[q2] : qdy;
       }
       float tt = __uint_as_float(e.x);
-      const float qte = cm ? exit_bound(t1n, P.cscr, P.dexit[bi0 * 4 + r], qox, qoy) : 0.0f;
+      const float qte = (cm || dp) ? exit_bound(t1n, dp || P.cscr, P.dexit[bi0 * 4 + r], qox, qoy) : 0.0f;
       int hit = -1;
       for (int it = itend; it < RC2DGI_DIAG_MAX_ITERS; ++it) {
         const float px = qox + (tt * qdx) * P.aspy;
@@ -827,7 +821,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
           ix = wrap_nearest(px, sax);
           iy = wrap_nearest(py, say);
         }
-        if (cm) live = live && !(tt + cmin_value(s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)]) >= qte);
+        if (cm || dp) {
+          const CminT e = s_cm[((iy >> P.csh) * kCminDim) + (ix >> P.csh)];
+          live = live && !(tt + (dp ? (float)e * P.kclr : cmin_value(e)) >= qte);
+        }
         if (!live) break;
         const int idx = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
         const float d = decode_dist(fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx));
@@ -842,6 +839,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
   }
 
+  RC_TSTAMP(4);
   RC_SECTION("stage_write");
   if (STG) {
 #pragma unroll
@@ -868,6 +866,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       if (t[k] < kDone) hit_idx[k] = (int)s_q[qpos[k]].x;
   }
 
+  RC_TSTAMP(5);
   RC_SECTION("merge");
   // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
   const bool pow2c = P2S || (P.c.powW && P.c.powH);  // P2S implies power-of-two cascades
@@ -961,7 +960,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
             rad.z = rad.z + up.z * rad.w;
             rad.w = rad.w * up.w;
           } else {
-            const float4 sk = sky[ai];  // top cascade: analytic sky, tabulated per angleIndex
+            const float4 sk = ld_uniform(sky + ai);  // top cascade: analytic sky, tabulated per angleIndex
             rad.x = rad.x + sk.x;
             rad.y = rad.y + sk.y;
             rad.z = rad.z + sk.z;
@@ -977,6 +976,14 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       GI::st(&out[(size_t)j * P.c.pitch + i], GI::blend_black(acc));
     }
   }
+#ifdef RC2DGI_DIAG_TIMING
+  RC_TSTAMP(6);
+  if ((threadIdx.x & 63) == 0) {  // spread over kDiagSlots copies (one hot address would serialize the atomics)
+    unsigned long long *st = P.stats + 256 + ((size_t)(blockIdx.x * (TX * TY / 64) + (threadIdx.x >> 6)) % kDiagSlots) * 256;
+    for (int i = 0; i < 6; ++i) atomicAdd(&st[P.level * 16 + i], rc_ts[i + 1] - rc_ts[i]);
+    atomicAdd(&st[P.level * 16 + 15], 1ull);
+  }
+#endif
 }
 
 template <int TX, int TY, int PY, int PD = 1, int UNR = 1, int DL = 0, class GI = GiF32>
@@ -1000,10 +1007,14 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
   P.cmin = reinterpret_cast<const float4 *>(a.cmin);
-  P.cdt = reinterpret_cast<const float4 *>(a.cdt);
   P.csh = dist_cmin_shift(P.s.W, P.s.H);
   P.cscr = a.cmin_screen;
   P.dexit = a.dexit;
+  // directional proofs only where a workgroup's direction block lies in one bin (4^L >= kDirBins)
+  P.dclr = (a.dclr && (1 << (2 * a.level)) >= kDirBins && P.dexit) ? reinterpret_cast<const float4 *>(a.dclr) : nullptr;
+  // texels per unit t: the position moves (dir * asp) per unit t, asp = (H, W) / max(W, H), i.e.
+  // W H / max(W, H) texels on either axis
+  P.kclr = (float)(1 << P.csh) * (float)std::max(P.s.W, P.s.H) / ((float)P.s.W * (float)P.s.H);
   if (P.cmin && P.cscr && !P.dexit) return hipErrorInvalidValue;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;

@@ -28,7 +28,7 @@ def main():
     c, e = scenes.demo(W, W)
     ctx.upload("color", c)
     ctx.upload("emissive", e)
-    buf = np.zeros((16, 3), np.uint64)
+    buf = np.zeros((16, 16), np.uint64)
     ctx.do_rc2dgi()
     ctx.sync()
     L.rc2dgi_diag_stats(buf.ctypes.data, 1)

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Wave-lifetime split of k_rc_level per level and section (diagnostic build librc2dgi_timing.so,
+python -m radiancecascade2dglobalillumination_amd._build timing): mean cycles per wave in
+setup (staging loads issued, bound table to LDS, barrier) / rays (origins, proofs) / march (lockstep)
+/ tail (queue, barrier) / stage_write (LDS, barrier) / merge (shading loads, bilinear, store).
+Run with the committed bench schedule; extra --tune KEY=VALUE knobs.  Prints one JSON line."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("RC2DGI_LIB", os.path.join(ROOT, "build", "diag", "librc2dgi_timing.so"))
+SECTIONS = ["setup", "rays", "march", "tail", "stage_write", "merge"]
+
+
+def main():
+    import numpy as np
+
+    from radiancecascade2dglobalillumination_amd import RC2DGI, scenes
+    from radiancecascade2dglobalillumination_amd.rc2dgi import load_library
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--cascades", type=int, default=6)
+    ap.add_argument("--ray-range", type=float, default=2.0)
+    ap.add_argument("--tune", action="append", default=[])
+    a = ap.parse_args()
+    W, N = a.size, a.cascades
+    L = load_library()
+    L.rc2dgi_diag_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ctx = RC2DGI(W, W, cascade_count=N, ray_range=a.ray_range)
+    sched = os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning", f"{W}x{W}_N{N}_rr{a.ray_range:g}_f32.json")
+    if os.path.exists(sched):
+        tun = json.load(open(sched))
+        for lv in range(N):
+            ctx.set_tuning(f"rc_order_L{lv}", tun["rc_order"][lv])
+            ctx.set_tuning(f"rc_variant_L{lv}", tun["rc_variant"][lv])
+    for kv in a.tune:
+        k, v = kv.split("=")
+        ctx.set_tuning(k, int(v))
+    c, e = scenes.demo(W, W)
+    ctx.upload("color", c)
+    ctx.upload("emissive", e)
+    buf = np.zeros((16, 16), np.uint64)
+    ctx.do_rc2dgi()
+    ctx.sync()
+    L.rc2dgi_diag_stats(buf.ctypes.data, 1)
+    ctx.set_timing(True)
+    ctx.do_rc2dgi()
+    ctx.sync()
+    L.rc2dgi_diag_stats(buf.ctypes.data, 1)
+    lv_ms = ctx.pass_times(levels=N)["levels"]
+    out = {"config": f"{W}x{W} N={N} rr={a.ray_range}", "tune": a.tune, "levels": {}}
+    for lv in range(N):
+        waves = int(buf[lv, 15])
+        cyc = {s: round(float(buf[lv, i]) / max(waves, 1), 1) for i, s in enumerate(SECTIONS)}
+        cyc["total"] = round(sum(cyc.values()), 1)
+        out["levels"][f"L{lv}"] = {"ms": round(lv_ms[lv], 4), "waves": waves, "cycles_per_wave": cyc}
+        print(f"L{lv} {lv_ms[lv]:.3f} ms waves {waves}: " + " ".join(f"{s} {cyc[s]:.0f}" for s in SECTIONS + ['total']),
+              file=sys.stderr)
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -54,12 +54,28 @@ def test_committed_pmc_record_has_the_gather_fields():
 
 
 def test_valu_roofline_is_issue_time_over_level_time(bench):
-    """valu_roofline: wave instructions per frame over the level times, against 256 CUs x 4 SIMDs at
-    one wave64 instruction per 4 cycles."""
-    rec = {"per_level": {f"k_rc_level L{L}": {"valu_insts": 614.4e6 / 4} for L in range(4)}}
-    v = bench.valu_roofline(rec, 4, [0.25] * 4)  # 614.4 M instructions in 1 ms
-    assert abs(v["achieved"] - 614.4) < 0.1 and abs(v["frac"] - 1.0) < 1e-3 and abs(v["floor_ms"] - 1.0) < 1e-3
+    """valu_roofline: wave instructions per frame, priced at each level's cycles per instruction
+    (plain wave64 VALU: 2 cycles on a SIMD-32, MI355X_MICROARCH.md), over the level times, against
+    256 CUs x 4 SIMDs at 2.4 GHz."""
+    rec = {"per_level": {f"k_rc_level L{L}": {"valu_insts": 1228.8e6 / 4} for L in range(4)}}
+    v = bench.valu_roofline(rec, 4, [0.25] * 4)  # 1228.8 M plain instructions in 1 ms: the peak
+    assert abs(v["achieved"] - 1228.8) < 0.1 and abs(v["frac"] - 1.0) < 1e-3 and abs(v["floor_ms"] - 1.0) < 1e-3
+    mix = {"levels": {f"L{L}": {"valu_cycles_per_inst": 4.0} for L in range(4)}}  # e.g. all v_pk_*_f32
+    v = bench.valu_roofline(rec, 4, [0.25] * 4, mix)
+    assert abs(v["frac"] - 2.0) < 1e-3 and abs(v["floor_ms"] - 2.0) < 1e-3
     assert bench.valu_roofline({"per_level": {}}, 4, [0.1] * 4) is None
+
+
+def test_isa_mix_classes():
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import isa_mix
+
+    assert isa_mix.classify("v_pk_fma_f32") == "valu_pk" and isa_mix.classify("v_fma_f32") == "valu"
+    assert isa_mix.classify("v_rcp_f32_e32") == "valu_tr" and isa_mix.classify("v_lshl_add_u64") == "valu_64"
+    assert isa_mix.classify("s_and_b64") == "salu" and isa_mix.classify("global_load_ushort") == "vmem"
+    assert isa_mix.classify("ds_read_u8") == "lds" and isa_mix.classify("s_waitcnt") == "wait"
 
 
 def _run_bench(args, env_extra=None, timeout=180):

@@ -580,13 +580,15 @@ def test_linux_merge_fallback_at_the_fused_blur_size(RC2DGI):
     (256, 128, 5, 64.0, 1.0, "rand:12", "f32"), (256, 256, 4, 2.0, 0.5, "rand:3", "f16"),
     (17, 5, 2, 8.0, 1.0, "rand:9", "f32"), (1024, 1024, 6, 2.0, 1.0, "rand:5", "f32"),
     (512, 512, 6, 2.0, 1.0, "rand:6", "rgba8"), (2048, 2048, 6, 2.0, 1.0, "demo", "f32"),
-    (64, 64, 3, 2.0, 1.0, "empty", "f32")])
+    (64, 64, 3, 2.0, 1.0, "empty", "f32"), (512, 512, 8, 64.0, 1.0, "rand:19", "f32"),
+    (640, 384, 5, 2.0, 1.0, "demo", "f32"), (512, 512, 5, 2.0, 1.0, "full", "f32")])
 def test_miss_proofs_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene, storage):
-    """Miss proofs (tuning rc_mp: a ray whose path provably holds no texel that passes the hit test is
-    not marched; k_dist_cmin's hit cells + k_cell_dt's Chebyshev cell distances) with every tail
-    setting (-1: every unproved ray queued at once, 0 off, 10 the default) in the one-probe tile
-    variants, and the variants without them (the flag must leave those alone): every level bit-exact
-    vs the oracle (RadianceCascades.fs:60-92: a miss returns (0,0,0,1) however it ends)."""
+    """Directional miss proofs (tuning rc_mp: a sample from which no later sample of the ray can pass the
+    hit test ends the ray unread -- k_dist_cmin's hit cells incl. the REPEAT wrap, k_dir_clear's clear
+    distances per angular bin) with every tail setting (-1: every unproved ray queued at once, 0 off, 10
+    the default) in the one-probe tile variants, and the variants without them (the flag must leave
+    those alone): every level bit-exact vs the oracle (RadianceCascades.fs:60-92: a miss returns
+    (0,0,0,1) however it ends)."""
     color, emis = make_scene(scene, W, H)
     if storage == "rgba8":
         color, emis = oracle.from_u8(np.rint(np.clip(color, 0, 1) * 255)), oracle.from_u8(np.rint(np.clip(emis, 0, 1) * 255))
