@@ -106,6 +106,7 @@ struct rc2dgi_ctx {
   CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
   unsigned char *hitc = nullptr;     // per bound-table cell: holds a texel that passes the hit test
   unsigned char *dclr = nullptr;     // directional clear distances of the miss proofs (k_dir_clear)
+  int4 *dboxes = nullptr;            // k_dir_clear's per-bin step boxes (dir_clear_boxes)
   float4 *gi1 = nullptr, *gi2 = nullptr, *blur = nullptr;
   float4 *gi_spare = nullptr;  // fused blur writes the copied-back final GI here, then swaps
   float2 *dirs = nullptr;  // concatenated per level
@@ -129,6 +130,7 @@ struct rc2dgi_ctx {
   std::vector<int> rc_tail;      // per level: tail compaction after this many lockstep iterations (tuning rc_tail_L<n>)
   int rc_wgproof = 1;            // tuning "rc_wgproof": workgroup-wide exit proof of the first samples
   std::vector<int> rc_mp;        // per level: directional miss proofs in the one-probe tiles (tuning rc_mp_L<n>)
+  std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
@@ -214,7 +216,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
-                  c->cmin,     c->dexit, c->hitc, c->dclr};
+                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -230,6 +232,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->shade = nullptr;
   c->cmin = nullptr;
   c->hitc = c->dclr = nullptr;
+  c->dboxes = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
   c->dexit = nullptr;
@@ -325,6 +328,12 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->cmin, (size_t)kCminDim * kCminDim * sizeof(CminT)));
   HIPCHK(c, alloc(&c->hitc, (size_t)kCminDim * kCminDim));
   HIPCHK(c, alloc(&c->dclr, (size_t)kDirBins * kCminDim * kCminDim));
+  {
+    std::vector<int4> boxes((size_t)kDirBins * kCminDim);
+    dir_clear_boxes(dist_cmin_shift(c->W, c->H), boxes.data());
+    HIPCHK(c, alloc(&c->dboxes, boxes.size() * sizeof(int4)));
+    HIPCHK(c, hipMemcpy(c->dboxes, boxes.data(), boxes.size() * sizeof(int4), hipMemcpyHostToDevice));
+  }
   const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
   HIPCHK(c, alloc(&c->gi1, nc * gsz));
   HIPCHK(c, alloc(&c->gi2, nc * gsz));
@@ -417,6 +426,25 @@ int upload_tables(rc2dgi_ctx *c) {
   std::vector<float2> dirs;
   std::vector<float4> dexit, sky;
   build_tables(c, dirs, dexit, sky);
+  // The directional miss proofs assume every direction of block bi lies in angular bin bi * kDirBins / 4^L
+  // and has unit length (the clear distances are texels along the ray, converted to t).  True of the
+  // library's own tables; a caller's table (rc2dgi_set_direction_table) is checked here, level by level,
+  // with 1e-5 of slack (k_dir_clear's boxes carry a texel of margin: 1e-5 rad is 0.08 texels at 8192).
+  c->dp_ok.assign(c->N, 0);
+  for (int L = 0; L < c->N; ++L) {
+    if ((1 << (2 * L)) < kDirBins) continue;
+    const double PI2 = 6.283185307179586, half = 0.5 * PI2 / kDirBins;
+    bool ok = true;
+    const size_t off = dir_table_offset(L), n = (size_t)4 << (2 * L);
+    for (size_t a = 0; a < n && ok; ++a) {
+      const double x = dirs[off + a].x, y = dirs[off + a].y;
+      const int j = (int)(((a / 4) * (size_t)kDirBins) >> (2 * L));
+      const double center = PI2 * (j + 0.5) / kDirBins;
+      const double d = std::remainder(std::atan2(y, x) - center, PI2);
+      ok = std::fabs(d) <= half + 1e-5 && std::fabs(std::hypot(x, y) - 1.0) <= 1e-5;
+    }
+    c->dp_ok[L] = ok;
+  }
   HIPCHK(c, hipMemcpyAsync(c->dirs, dirs.data(), dirs.size() * sizeof(float2), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->dexit, dexit.data(), dexit.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->sky, sky.data(), sky.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
@@ -855,7 +883,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   for (int v : c->rc_mp) mps |= v != 0;
   mps = mps && proofs;
   if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
-  if (mps) HIPCHK(c, launch_dir_clear(c->hitc, c->dclr, c->W, c->H, st));
+  if (mps) HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
@@ -880,7 +908,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.dist_packed = c->dist_p;
     a.dist_nib = c->dist_n;
     a.cmin = proofs ? c->cmin : nullptr;
-    a.dclr = (mps && c->rc_mp[L]) ? c->dclr : nullptr;
+    a.dclr = (mps && c->rc_mp[L] && L < (int)c->dp_ok.size() && c->dp_ok[L]) ? c->dclr : nullptr;
     // the screen-edge test pays where rays are long (t1 >= 1/8 of the screen: L4 / L5 at N = 6)
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];

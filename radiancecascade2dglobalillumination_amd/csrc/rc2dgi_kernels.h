@@ -140,7 +140,10 @@ hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, 
 // Directional clear distances of the march proofs (k_rc_level, one-probe tiles): kDirBins angular bins x
 // kCminDim^2 cells, bytes (k_dir_clear)
 constexpr int kDirBins = 64;
-hipError_t launch_dir_clear(const unsigned char *hitc, unsigned char *dclr, int W, int H, hipStream_t st);
+// per bin and step of k_dir_clear: the box of cells (x0, x1, y0, y1 relative to the start cell) the step's
+// points reach, for cells of 2^csh texels; kDirBins x kCminDim entries (host)
+void dir_clear_boxes(int csh, int4 *boxes);
+hipError_t launch_dir_clear(const unsigned char *hitc, const int4 *boxes, unsigned char *dclr, hipStream_t st);
 
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,

@@ -500,7 +500,8 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
 // One thread per (bin, cell): kDirBins x 16 workgroups of 256 cells (a quarter of the grid rows each); the
 // flag grid as one 64-bit word per row in LDS.
 __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restrict__ hitc,
-                                                   unsigned char *__restrict__ dclr, int csh) {
+                                                   const int4 *__restrict__ boxes,
+                                                   unsigned char *__restrict__ dclr) {
   constexpr int D = kCminDim, NS = kCminDim;
   static_assert(D == 64, "one 64-bit word per row");
   __shared__ unsigned short part[D * 4];      // 16-cell pieces of the rows
@@ -514,26 +515,12 @@ __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restri
     for (int q = 0; q < 16; ++q) m |= ((w[q >> 2] >> (8 * (q & 3))) & 0xFFu) ? 1u << q : 0u;
     part[threadIdx.x] = (unsigned short)m;
   }
-  if (threadIdx.x < NS) {
-    const double C = (double)(1 << csh), PI2 = 6.283185307179586;
-    const double ta = PI2 * j / kDirBins, tb = PI2 * (j + 1) / kDirBins;
-    const double sag = 1.0 - cos(0.5 * (tb - ta));
-    const double r0 = threadIdx.x * C, r1 = (threadIdx.x + 1) * C;
-    double lox = 1e30, hix = -1e30, loy = 1e30, hiy = -1e30;
-    const double ds[2][2] = {{cos(ta), sin(ta)}, {cos(tb), sin(tb)}};
-    for (int a = 0; a < 2; ++a)
-      for (int b = 0; b < 2; ++b) {
-        const double r = b ? r1 : r0;
-        lox = fmin(lox, ds[a][0] * r);
-        hix = fmax(hix, ds[a][0] * r);
-        loy = fmin(loy, ds[a][1] * r);
-        hiy = fmax(hiy, ds[a][1] * r);
-      }
-    const double m = r1 * sag + 1.0;
-    box[threadIdx.x][0] = (int)floor((lox - m) / C);
-    box[threadIdx.x][1] = (int)floor((hix + m + C - 1e-6) / C);
-    box[threadIdx.x][2] = (int)floor((loy - m) / C);
-    box[threadIdx.x][3] = (int)floor((hiy + m + C - 1e-6) / C);
+  if (threadIdx.x < NS) {  // the bin's per-step boxes (dir_clear_boxes, host-built once per context)
+    const int4 bx = boxes[j * NS + threadIdx.x];
+    box[threadIdx.x][0] = bx.x;
+    box[threadIdx.x][1] = bx.y;
+    box[threadIdx.x][2] = bx.z;
+    box[threadIdx.x][3] = bx.w;
   }
   __syncthreads();
   __shared__ unsigned long long rows[D];
@@ -1288,8 +1275,32 @@ hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, 
   return hipGetLastError();
 }
 
-hipError_t launch_dir_clear(const unsigned char *hitc, unsigned char *dclr, int W, int H, hipStream_t st) {
-  hipLaunchKernelGGL(k_dir_clear, dim3(kDirBins * 16), dim3(256), 0, st, hitc, dclr, dist_cmin_shift(W, H));
+void dir_clear_boxes(int csh, int4 *boxes) {
+  const double C = (double)(1 << csh), PI2 = 6.283185307179586;
+  for (int j = 0; j < kDirBins; ++j) {
+    const double ta = PI2 * j / kDirBins, tb = PI2 * (j + 1) / kDirBins;
+    const double sag = 1.0 - std::cos(0.5 * (tb - ta));
+    const double ds[2][2] = {{std::cos(ta), std::sin(ta)}, {std::cos(tb), std::sin(tb)}};
+    for (int s = 0; s < kCminDim; ++s) {
+      const double r0 = s * C, r1 = (s + 1) * C;
+      double lox = 1e30, hix = -1e30, loy = 1e30, hiy = -1e30;
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+          const double r = b ? r1 : r0;
+          lox = std::fmin(lox, ds[a][0] * r);
+          hix = std::fmax(hix, ds[a][0] * r);
+          loy = std::fmin(loy, ds[a][1] * r);
+          hiy = std::fmax(hiy, ds[a][1] * r);
+        }
+      const double m = r1 * sag + 1.0;
+      boxes[j * kCminDim + s] = make_int4((int)std::floor((lox - m) / C), (int)std::floor((hix + m + C - 1e-6) / C),
+                                          (int)std::floor((loy - m) / C), (int)std::floor((hiy + m + C - 1e-6) / C));
+    }
+  }
+}
+
+hipError_t launch_dir_clear(const unsigned char *hitc, const int4 *boxes, unsigned char *dclr, hipStream_t st) {
+  hipLaunchKernelGGL(k_dir_clear, dim3(kDirBins * 16), dim3(256), 0, st, hitc, boxes, dclr);
   return hipGetLastError();
 }
 
