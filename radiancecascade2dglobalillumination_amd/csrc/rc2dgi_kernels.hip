@@ -497,15 +497,16 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
 // u + d r (u in the cell, d in the bin, r in the step) lie in the box of the four chord corners grown by
 // the sagitta r (1 - cos(dtheta / 2)) and one texel (the fp32 rounding of positions and directions), and
 // the step's cells are the cells that box touches.  Cells off the grid are off screen: never sampled.
-// One thread per (bin, cell): kDirBins x 16 workgroups of 256 cells (a quarter of the grid rows each); the
-// flag grid as one 64-bit word per row in LDS.
+// One thread per (bin, cell), a wave per row of cells (the row's step rows are wave-uniform): kDirBins x 16
+// workgroups of 4 rows; the flag grid as one 64-bit word per row in LDS.
 __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restrict__ hitc,
                                                    const int4 *__restrict__ boxes,
                                                    unsigned char *__restrict__ dclr) {
   constexpr int D = kCminDim, NS = kCminDim;
-  static_assert(D == 64, "one 64-bit word per row");
-  __shared__ unsigned short part[D * 4];      // 16-cell pieces of the rows
-  __shared__ int box[NS][4];                   // per step: cell offsets x0, x1, y0, y1 relative to the start cell
+  static_assert(D == 64, "one 64-bit word per row, a wave per row");
+  __shared__ unsigned short part[D * 4];  // 16-cell pieces of the rows
+  __shared__ unsigned long long rows[D];
+  __shared__ int4 box[NS];                // per step: cell offsets x0, x1, y0, y1 relative to the start cell
   const int j = blockIdx.x >> 4, c = (int)((blockIdx.x & 15) * 256 + threadIdx.x);
   {  // thread t packs cells 16 t .. 16 t + 15 (row t / 4, piece t % 4)
     const uint4 v = reinterpret_cast<const uint4 *>(hitc)[threadIdx.x];
@@ -515,34 +516,45 @@ __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restri
     for (int q = 0; q < 16; ++q) m |= ((w[q >> 2] >> (8 * (q & 3))) & 0xFFu) ? 1u << q : 0u;
     part[threadIdx.x] = (unsigned short)m;
   }
-  if (threadIdx.x < NS) {  // the bin's per-step boxes (dir_clear_boxes, host-built once per context)
-    const int4 bx = boxes[j * NS + threadIdx.x];
-    box[threadIdx.x][0] = bx.x;
-    box[threadIdx.x][1] = bx.y;
-    box[threadIdx.x][2] = bx.z;
-    box[threadIdx.x][3] = bx.w;
-  }
+  if (threadIdx.x < NS) box[threadIdx.x] = boxes[j * NS + threadIdx.x];  // host-built (dir_clear_boxes)
   __syncthreads();
-  __shared__ unsigned long long rows[D];
   if (threadIdx.x < D)
     rows[threadIdx.x] = (unsigned long long)part[4 * threadIdx.x] | (unsigned long long)part[4 * threadIdx.x + 1] << 16 |
                         (unsigned long long)part[4 * threadIdx.x + 2] << 32 |
                         (unsigned long long)part[4 * threadIdx.x + 3] << 48;
   __syncthreads();
-  const int cx = c % D, cy = c / D;
+  const int cx = c % D, cy = __builtin_amdgcn_readfirstlane(c / D);
+  const int lane = (int)threadIdx.x & 63;
+  // lane s holds step s of this wave's row: the OR of the grid rows its box covers (the rows do not
+  // depend on the cell's column) and the box's column offsets; the steps are then read back with
+  // v_readlane (wave-uniform), so the per-cell loop below is plain VALU
+  const int4 bl = box[lane];
+  const int ly0 = max(0, cy + bl.z), ly1 = min(D - 1, cy + bl.w);
+  unsigned long long orow = 0;
+  for (int y = ly0; y <= ly1; ++y) orow |= rows[y];
+  // the boxes move outwards along the bin's directions: from the first step whose rows lie off the grid on
+  const unsigned long long off = __ballot(ly0 > ly1);
+  const int nsteps = off ? (int)__builtin_ctzll(off) : NS;
+  const unsigned olo = (unsigned)orow, ohi = (unsigned)(orow >> 32);
   int clear = 255;
-  for (int s = 0; s < NS; ++s) {
-    const int bx0 = cx + box[s][0], bx1 = cx + box[s][1], by0 = cy + box[s][2], by1 = cy + box[s][3];
-    // the boxes move outwards along the bin's directions: once one lies wholly off the grid, so do the next
-    if (bx1 < 0 || bx0 > D - 1 || by1 < 0 || by0 > D - 1) break;
-    const int x0 = max(0, bx0), x1 = min(D - 1, bx1), y0 = max(0, by0), y1 = min(D - 1, by1);
-    const unsigned long long mask = (x1 - x0 == 63 ? ~0ull : ((1ull << (x1 - x0 + 1)) - 1ull)) << x0;
-    bool hit = false;
-    for (int y = y0; y <= y1 && !hit; ++y) hit = (rows[y] & mask) != 0;
-    if (hit) {
-      clear = s;
-      break;
+  bool done = false;
+  for (int s = 0; s < nsteps; ++s) {
+    const unsigned long long o = (unsigned long long)__builtin_amdgcn_readlane(ohi, s) << 32 |
+                                 (unsigned)__builtin_amdgcn_readlane(olo, s);
+    const int bx0 = __builtin_amdgcn_readlane(bl.x, s), bx1 = __builtin_amdgcn_readlane(bl.y, s);
+    const int x0 = max(0, cx + bx0), x1 = min(D - 1, cx + bx1);
+    if (!done) {
+      if (x0 > x1) {
+        done = true;  // (off the grid sideways: so are the later steps)
+      } else {
+        const unsigned long long mask = (x1 - x0 == 63 ? ~0ull : ((1ull << (x1 - x0 + 1)) - 1ull)) << x0;
+        if (o & mask) {
+          clear = s;
+          done = true;
+        }
+      }
     }
+    if (__all(done)) break;
   }
   dclr[(size_t)j * D * D + c] = (unsigned char)clear;
 }
