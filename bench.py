@@ -271,6 +271,17 @@ def bench_batch(a, rank, local, world):
         g.close()
 
 
+def apply_schedule(g, tun, N, shards=1):
+    """Per-level rc_order / rc_variant of a committed schedule.  A schedule may carry a row-strip
+    entry ("strips": {"<shards>": {"rc_variant": [...], "rc_order": [...]}}) for the shard contexts
+    of that many strips: a shard computes a band of every block's rows, so the tile height that
+    wastes the fewest rows can differ from the whole frame's pick (results are identical either way)."""
+    sub = (tun.get("strips") or {}).get(str(shards), {}) if shards > 1 else {}
+    for L in range(N):
+        g.set_tuning(f"rc_order_L{L}", (sub.get("rc_order") or tun["rc_order"])[L])
+        g.set_tuning(f"rc_variant_L{L}", (sub.get("rc_variant") or tun["rc_variant"])[L])
+
+
 def bench_strips(a, rank, local, world):
     """SURVEY §8e / BASELINE configs[3]: ONE frame split into row strips, one shard per rank
     (strong scaling).  Ranks exchange their distRT strips over RCCL inside librc2dgi
@@ -300,11 +311,12 @@ def bench_strips(a, rank, local, world):
         g.upload("color", color)
         g.upload("emissive", emis)
         if tun:
-            for L in range(N):
-                g.set_tuning(f"rc_order_L{L}", tun["rc_order"][L])
-                g.set_tuning(f"rc_variant_L{L}", tun["rc_variant"][L])
+            apply_schedule(g, tun, N, nsh)
         elif not a.no_autotune:
             g.autotune(1)  # on the whole frame; the orders carry over to the shard
+        for kv in a.tune:
+            key, v = kv.split("=")
+            g.set_tuning(key, int(v))
         g.set_shard(k, nsh)
         return g
 
@@ -345,7 +357,8 @@ def bench_strips(a, rank, local, world):
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
             "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}, row strips",
-                       "shards": nsh, "parallelism": f"strips{nsh}" + ("-in-process" if virtual else "-rccl")},
+                       "shards": nsh, "parallelism": f"strips{nsh}" + ("-in-process" if virtual else "-rccl"),
+                       "rc_variant": [ctxs[0].get_tuning(f"rc_variant_L{L}") for L in range(N)]},
             "frames_per_s": round(a.steps / wall, 2)}), flush=True)
     for g in ctxs:
         g.close()

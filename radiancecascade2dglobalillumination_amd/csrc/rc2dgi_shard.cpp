@@ -136,16 +136,25 @@ FramePlan plan_frame(const PlanInputs &in) {
     for (auto &r : p.blur.iv) need0.add(r.first - h, r.second + h);
   }
   p.level[0] = need0;
-  // level L probe row c samples G_{L+1} inside its upper blocks at rows floor(c/2 - 0.25) and
-  // +1 (RadianceCascades.fs:131-139; clamp keeps it block-local), +-1 for rounding:
-  // [floor(c0/2) - 2, floor((c1-1)/2) + 3) in every upper block row, modulo the block height
+  // level L probe row c samples G_{L+1} inside its upper blocks at rows floor(py - 0.5) and +1,
+  // py = clamp(c/2 + 0.25, 0.5, nb - 0.5) (RadianceCascades.fs:131-139; the clamp keeps it
+  // block-local, its top row's second tap -- weight 0 -- is row 0 of the next block, i.e. row 0
+  // modulo the block height).  Power-of-two cascades: every term is exact (k_rc_level's pow2
+  // path), so the taps of [c0, c1) are [max(0, (c0-1) >> 1), max(0, (c1-2) >> 1) + 2).
+  // Otherwise +-1 row for rounding: [floor(c0/2) - 2, floor((c1-1)/2) + 3).
+  const bool exact = (in.CW & (in.CW - 1)) == 0 && (in.CH & (in.CH - 1)) == 0;
   for (int L = 0; L + 1 < in.N; ++L) {
     const int nb = in.CH >> (L + 1);
     RowSet up = RowSet::none(nb);
     if (p.level[L].is_full()) {
       up = RowSet::full(nb);
     } else {
-      for (auto &r : p.level[L].iv) up.add(r.first / 2 - 2, (r.second - 1) / 2 + 3);
+      for (auto &r : p.level[L].iv) {
+        if (exact)
+          up.add(std::max(0, (r.first - 1) >> 1), std::max(0, (r.second - 2) >> 1) + 2);
+        else
+          up.add(r.first / 2 - 2, (r.second - 1) / 2 + 3);
+      }
     }
     p.level[L + 1] = up;
   }

@@ -208,8 +208,8 @@ def test_c1_vs_llvmpipe_fixture(R):
 def test_c3_8192_eight_row_strips(R):
     """8192^2, N=8, rayRange 64 split into 8 row strips, run as 8 in-process shard
     contexts with the distRT exchange (rc2dgi_do_group), intermediates poisoned, all with the
-    committed schedule bench.py --mode strips times (tuning/8192x8192_N8_rr64_f32.json, the nibble
-    march at L4): every shard's colorRT / tempRT strip equals the unsharded frame bit for bit, and
+    committed schedule bench.py --mode strips times (tuning/8192x8192_N8_rr64_f32.json, the
+    packed-field march at L4): every shard's colorRT / tempRT strip equals the unsharded frame bit for bit, and
     the unsharded frame is checked against the oracle (JFA + DF whole frame, 1/4 of the rows of
     every level, blur / merge on every 8th row)."""
     from radiancecascade2dglobalillumination_amd import scenes

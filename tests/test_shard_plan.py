@@ -215,6 +215,7 @@ CASES = [
     (96, 64, 2, 2.0, 1.0, 0.0, 5, "rand:5"),      # blur off
     (256, 256, 5, 3.0, 1.0, 1.5, 8, "demo"),
     (333, 200, 4, 2.0, 1.7, 1.5, 3, "rand:6"),    # renderScale > 1
+    (512, 512, 5, 2.0, 1.0, 1.5, 8, "demo"),      # power of two: exact cascade rows, partial up to L4
 ]
 
 
