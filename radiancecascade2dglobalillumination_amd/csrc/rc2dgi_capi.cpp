@@ -132,6 +132,7 @@ struct rc2dgi_ctx {
   std::vector<int> rc_mp;        // per level: directional miss proofs in the one-probe tiles (tuning rc_mp_L<n>)
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
+  int jfa_coset = 1;             // tuning "jfa_coset": the first four steps in one kernel (k_jfa_coset) where they apply
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
@@ -753,9 +754,18 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
   unsigned short *dist = t == c->S - 1 ? c->dist : nullptr;  // 3. DistanceField fused into the last step
   hipStream_t st = c->stream;
   if (!c->strip) {
+    // the first four steps in one kernel (k_jfa_coset): the ScreenUV mask -> J_3
+    int cs = c->jfa_coset ? jfa_coset_steps(c->sd, c->S) : 0;
+    for (int q = 0; q < cs; ++q)
+      if (!plan.jfa[q].is_full()) cs = 0;
+    if (t < cs) {
+      if (t == 0) HIPCHK(c, launch_jfa_coset(c->occ, c->mpitch, jfa_out(c, cs - 1), c->sd, st));
+      return RC2DGI_OK;
+    }
+    unsigned *out = jfa_out(c, t);
     const unsigned *src = t == 0 ? c->occ : jfa_out(c, t - 1);
     for (auto &r : plan.jfa[t].iv)
-      HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, jfa_out(c, t), dist, c->sd, ox, oy, st,
+      HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, out, dist, c->sd, ox, oy, st,
                                 r.first, r.second, nullptr, 0, c->jfa_lds));
     return RC2DGI_OK;
   }
@@ -1397,6 +1407,10 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_wgproof = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "jfa_coset") {
+    c->jfa_coset = value != 0;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_lds") {
     c->jfa_lds = value != 0;
     return RC2DGI_OK;
@@ -1464,6 +1478,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "jfa_lds") {
     *value = c->jfa_lds;
+    return RC2DGI_OK;
+  }
+  if (k == "jfa_coset") {
+    *value = c->jfa_coset;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_tail_L", 0) == 0) {

@@ -22,7 +22,8 @@ struct BlurTaps {
 // power-of-two JFA: integer tap offsets and the distance-key scaling (see k_jfa_p2)
 struct JfaTaps {
   int dx[3], dy[3];
-  float scx, scy, dinit;
+  float scx, scy, dinit;  // key scale per axis (max(W,H) / W, / H) and the initial minimum max(W,H)^2
+  float inv_mx;           // 1 / max(W,H): distance = sqrt(key) / max(W,H)
 };
 
 struct CascadeDims {
@@ -62,6 +63,11 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
 // integer taps of the power-of-two JFA kernel (false: the float path runs); also used by the
 // row-strip planner
 bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp);
+
+// the first four steps in one kernel (k_jfa_coset): 4 where they apply (square power-of-two screens of
+// 512 texels or more), else 0.  launch_jfa_coset reads the ScreenUV mask and writes J_3.
+int jfa_coset_steps(ScreenDims s, int S);
+hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, ScreenDims s, hipStream_t st);
 
 // device copies of the host-built workgroup maps of k_rc_level, one per launch geometry
 struct RcMapCache {

@@ -25,6 +25,7 @@
 #include "rc2dgi_device.h"
 #include "rc2dgi_kernels.h"
 #include "rc2dgi_rc.h"
+#include "rc2dgi_shard.h"
 
 #include <algorithm>
 #include <cmath>
@@ -177,24 +178,67 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
   }
 }
 
-// JumpFlood.fs step for power-of-two W and H.  There every fragTexCoord + offset is exact, so a
-// tap's NEAREST texel is (i + dx, j + dy) & (size - 1) with integer dx, dy fixed per step (host:
-// floor(0.5 + offset * size)); tap rows are wave-uniform (scalar row addresses).
-// Seed distance: fragTexCoord differences are exact as well, dx = (si - i) / W, and a power-of-two
-// scaling commutes with rounding, so the shader's `dx*dx + dy*dy < minDist` is the same comparison
-// on ((si - i) * scx)^2 + ((sj - j) * scy)^2 < max(W,H)^2.
-//   IKEY (W == H <= 4096): (si - i)^2 and (sj - j)^2 are integers below 2^24 (exact in fp32), so
-//     the shader's rounded sum is the integer sum converted with round-to-nearest-even: one packed
-//     16-bit subtract and one clamped 16-bit dot product per tap, compared as integers (below).
-//   otherwise the fp32 form.
-// The no-seed value 0x80008000 is at least max(W,H) away from every texel (and below overflow),
-// so it never beats the initial minDist and needs no test of its own.
+// JumpFlood.fs's scan of a texel's 9 taps ("d < minDist" from minDist = 1, y outer, x inner: the first
+// of equal distances wins) as a min over per-tap keys and a select from the last tap to the first (no
+// compare-and-swap chain, whose VCC hand-offs serialise).  The keys are the shader's squared distance
+// scaled by the power of two mx^2 (mx = max(W, H); o.scx = mx / W, o.scy = mx / H): every fragTexCoord
+// difference is (si - i) / W exactly, and a power-of-two scale commutes with each rounding, so the keys
+// order as the shader's.  Non-negative finite floats order as their bit patterns.
+//   IKEY (W == H <= 4096): (si - i)^2 and (sj - j)^2 are integers below 2^24, exact in fp32, so the
+//     rounded float sum is the integer sum converted with round-to-nearest-even: one packed 16-bit
+//     subtract and one clamped 16-bit dot product per tap, compared as integers.
+//   otherwise: the packed 16-bit difference converted (exact: |si - i| < 2^15; the no-seed value
+//     0x8000 wraps to the same magnitude), scaled, squared and added in fp32 as the shader rounds.
+// A key >= dinit = mx^2 loses to the initial minDist (kNoSeed's is >= 2^28 >= dinit).  *key: the
+// winner's key as a float; sqrt(*key) / mx is its distance (DistanceField.fs) to the bit, the same
+// power-of-two argument.
+template <bool IKEY>
+__device__ __forceinline__ unsigned jfa_best9(const unsigned sd[9], unsigned here, const JfaTaps &o, float *key) {
+  typedef short v2s __attribute__((ext_vector_type(2)));
+  unsigned kb[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const v2s d = __builtin_bit_cast(v2s, sd[k]) - __builtin_bit_cast(v2s, here);
+    if constexpr (IKEY) {
+      kb[k] = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, true);  // clamped: >= 0
+    } else {
+      const float fx = (float)d.x * o.scx, fy = (float)d.y * o.scy;
+      kb[k] = __float_as_uint(fx * fx + fy * fy);
+    }
+  }
+  const unsigned m = min(min(min(kb[0], kb[1]), min(kb[2], kb[3])), min(min(kb[4], kb[5]), min(min(kb[6], kb[7]), kb[8])));
+  unsigned best = sd[8];
+#pragma unroll
+  for (int k = 7; k >= 0; --k) best = kb[k] == m ? sd[k] : best;
+  *key = IKEY ? (float)m : __uint_as_float(m);
+  return m >= (IKEY ? (unsigned)o.dinit : __float_as_uint(o.dinit)) ? kNoSeed : best;
+}
+
+// DistanceField.fs (distance(fragTexCoord, seed) -> packUNorm16) of texel (i, j) from its JumpFlood
+// result: sqrt(key) / mx when a seed was found (jfa_best9), else the distance to uv (0, 0).
+__device__ __forceinline__ unsigned short jfa_dist_q(unsigned best, float key, int i, int j, ScreenDims s, const JfaTaps &o) {
+  float d;
+  if (best != kNoSeed) {
+    d = sqrtf(key) * o.inv_mx;
+  } else {
+    const Axis ax{s.W, 1}, ay{s.H, 1};
+    const float dx = texcoord(i, ax), dy = texcoord(j, ay);
+    d = sqrtf(dx * dx + dy * dy);
+  }
+  const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
+  return (unsigned short)(unsigned)(cl * 65535.0f + 0.5f);
+}
+
 // physical workgroup id -> logical id: every XCD (own L2) a contiguous chunk of the logical order
 __host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
   const int q = n >> 3, r = n & 7, x = p & 7;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (p >> 3);
 }
 
+// JumpFlood.fs step for power-of-two W and H.  There every fragTexCoord + offset is exact, so a
+// tap's NEAREST texel is (i + dx, j + dy) & (size - 1) with integer dx, dy fixed per step (host:
+// floor(0.5 + offset * size)); tap rows are wave-uniform (scalar row addresses).  Keys and the
+// distance: jfa_best9 / jfa_dist_q.
 // U8: RGBA8 jumpRT (quantized seed uv, pack_seed_u8): the same integer taps, the float distance of
 // k_jfa_step's U8 path (the seed's uv is k * (1/255), not its texel centre).
 // LDS: a short step (offset s <= 8 texels on both axes): the workgroup stages its 64 x 16 tile and
@@ -290,7 +334,6 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
     }
   }
   }
-  typedef short v2s __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int t = 0; t < JT; ++t) {
     const int j = j0 + 4 * t;
@@ -327,53 +370,73 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
       }
       continue;
     }
-    unsigned best = kNoSeed;
-    const unsigned here = pack_seed(i, j);
-    if constexpr (IKEY) {
-      // The sequential "key < minKey" update keeps the first tap holding the minimum key, if that
-      // minimum is below dinit = max(W,H)^2 <= 2^24.  Integer keys below 2^24 convert exactly, and
-      // a key >= dinit loses both as an integer and as its rounded float, so the integer keys
-      // decide the same: one min3 tree over the 9 keys, then a select from the last tap to the
-      // first (no compare-and-swap chain, whose VCC hand-offs serialise; no conversions).
-      unsigned kb[9];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const v2s d = __builtin_bit_cast(v2s, seed[t][k]) - __builtin_bit_cast(v2s, here);
-        kb[k] = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, true);  // clamped: >= 0
-      }
-      const unsigned m = min(min(min(kb[0], kb[1]), min(kb[2], kb[3])),
-                             min(min(kb[4], kb[5]), min(min(kb[6], kb[7]), kb[8])));
-      best = seed[t][8];
-#pragma unroll
-      for (int k = 7; k >= 0; --k) best = kb[k] == m ? seed[t][k] : best;
-      if (m >= (unsigned)o.dinit) best = kNoSeed;
-    } else {
-      float minKey = o.dinit;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
-        const unsigned sd = seed[t][k];
-        const float dx = (float)((int)(sd & 0xFFFFu) - i) * o.scx, dy = (float)((int)(sd >> 16) - j) * o.scy;
-        const float key = dx * dx + dy * dy;
-        if (key < minKey) {
-          minKey = key;
-          best = sd;
-        }
-      }
-    }
+    float key;
+    const unsigned best = jfa_best9<IKEY>(seed[t], pack_seed(i, j), o, &key);
     dst[(size_t)(j - dst_row0) * s.pitch + i] = best;
-    if (dist) {  // DistanceField.fs, as in k_jfa_step
-      const Axis ax{s.W, 1}, ay{s.H, 1};
-      float bx = 0.0f, by = 0.0f;
-      if (best != kNoSeed) {
-        bx = texcoord((int)(best & 0xFFFFu), ax);
-        by = texcoord((int)(best >> 16), ay);
-      }
-      const float dx = texcoord(i, ax) - bx, dy = texcoord(j, ay) - by;
-      const float d = sqrtf(dx * dx + dy * dy);
-      const float cl = fminf(fmaxf(d, 0.0f), 1.0f);
-      dist[(size_t)j * s.pitch + i] = (unsigned short)(unsigned)(cl * 65535.0f + 0.5f);
+    if (dist) dist[(size_t)j * s.pitch + i] = jfa_dist_q(best, key, i, j, s, o);  // DistanceField.fs
+  }
+}
+
+// ---------------------------------------------------------------- JumpFlood: the long steps in one kernel
+// The long steps (JumpFlood.fs, RC2DGI.cs:296-326).  On a square power-of-two screen step t taps at
+// +-s_t = W / 2^(t+1) texels on both axes, so the texels (x0 + a g, y0 + b g) of one residue
+// (x0, y0) modulo g = W / 16 tap only one another in the steps with s_t >= g (t = 0..3): a 16 x 16
+// torus whose steps tap +-8, 4, 2, 1 lattice points.  A workgroup holds 32 adjacent residues (one
+// 128-byte segment at each of the 256 lattice points, 32 KB of LDS), seeds them from the ScreenUV
+// mask (step 0's input), runs the four steps in LDS and writes J_3 -- each texel read and written
+// once, no intermediate image in HBM.  A thread owns texel u of segment a at every lattice row b, so
+// every tap row is a compile-time LDS offset.  Same taps, order and keys as k_jfa_p2.
+constexpr int kCosetW = 32, kCosetL = 16, kCosetPlane = kCosetW * kCosetL;  // segment, lattice side, texels per lattice row
+// threads: one per (segment a, texel u), all 16 lattice rows each (the float keys spill a few row
+// coordinates at 128 VGPRs; splitting the rows over two threads to avoid it measured slower at 8192^2:
+// 0.72 vs 0.58 ms)
+template <bool IKEY> constexpr int coset_threads() { return kCosetPlane; }
+template <bool IKEY>
+__global__ __launch_bounds__(coset_threads<IKEY>()) __attribute__((amdgpu_waves_per_eu(4))) void k_jfa_coset(
+    const unsigned *__restrict__ mask, int mpitch, unsigned *__restrict__ dst, ScreenDims s, JfaTaps o) {
+  constexpr int RT = kCosetL * kCosetPlane / coset_threads<IKEY>();  // lattice rows per thread
+  __shared__ unsigned img[kCosetL * kCosetPlane];
+  const int g = s.W / kCosetL;  // lattice spacing (host: W == H, g a multiple of kCosetW)
+  const int nx = g / kCosetW;
+  const int x0 = (blockIdx.x % nx) * kCosetW, y0 = blockIdx.x / nx;
+  const int tid = (int)threadIdx.x, col0 = tid & (kCosetPlane - 1), u = tid & (kCosetW - 1), a = col0 >> 5;
+  const int b0 = (tid / kCosetPlane) * RT;  // the thread's first lattice row
+  const int x = x0 + a * g + u;
+  unsigned m[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) m[r] = mask[(size_t)(y0 + (b0 + r) * g) * mpitch + (x >> 5)];
+  unsigned v[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {  // ScreenUV seeds (k_jfa_p2<FIRST>)
+    const unsigned y = (unsigned)(y0 + (b0 + r) * g);
+    v[r] = ((m[r] >> u) & 1u) ? ((y << 16) | (unsigned)x) : kNoSeed;
+    img[(b0 + r) * kCosetPlane + col0] = v[r];
+  }
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int k = 8 >> st;  // tap offset in lattice points
+    __syncthreads();
+    int col[3];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) col[dx] = (((a + (dx - 1) * k) & (kCosetL - 1)) << 5) + u;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      unsigned sd[9];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) sd[dy * 3 + dx] = img[((b0 + r + (dy - 1) * k) & (kCosetL - 1)) * kCosetPlane + col[dx]];
+      float key;
+      v[r] = jfa_best9<IKEY>(sd, ((unsigned)(y0 + (b0 + r) * g) << 16) | (unsigned)x, o, &key);
+    }
+    if (st < 3) {
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < RT; ++r) img[(b0 + r) * kCosetPlane + col0] = v[r];
     }
   }
+#pragma unroll
+  for (int r = 0; r < RT; ++r) dst[(size_t)(y0 + (b0 + r) * g) * s.pitch + x] = v[r];
 }
 
 // ---------------------------------------------------------------- surface records
@@ -1001,6 +1064,39 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     hipLaunchKernelGGL((k_jfa_step<false, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
                        row1, win, dst_row0);
   }
+  return hipGetLastError();
+}
+
+int jfa_coset_steps(ScreenDims s, int S) {
+  // steps 0..3 tap +-W/2, W/4, W/8, W/16 on a square power-of-two screen whose lattice spacing W / 16
+  // holds whole 32-texel segments; the four steps must not be the last two (J_{S-2}, J_{S-1} are
+  // visible) nor overlap the fused short steps
+  if (!(s.powW && s.powH) || s.u8 || s.W != s.H || s.W < kCosetL * kCosetW || s.W > 16384 || S < 9) return 0;
+  for (int t = 0; t < 4; ++t) {
+    float ox[3], oy[3];
+    jfa_offsets(s.W, s.H, t, ox, oy);
+    JfaTaps tp;
+    if (!jfa_p2_taps(s, ox, oy, &tp)) return 0;
+    const int o = s.W >> (t + 1);
+    if (tp.dx[0] != -o || tp.dx[2] != o || tp.dy[0] != -o || tp.dy[2] != o) return 0;
+  }
+  return 4;
+}
+
+hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, ScreenDims s, hipStream_t st) {
+  float ox[3] = {-1.0f, 0.0f, 1.0f}, oy[3] = {-1.0f, 0.0f, 1.0f};
+  for (int k = 0; k < 3; ++k) {
+    ox[k] /= (float)s.W;
+    oy[k] /= (float)s.H;
+  }
+  JfaTaps tp;
+  if (!jfa_p2_taps(s, ox, oy, &tp)) return hipErrorInvalidValue;
+  const int g = s.W / kCosetL;
+  const dim3 grid((g / kCosetW) * g);
+  if (s.W <= 4096)
+    hipLaunchKernelGGL(k_jfa_coset<true>, grid, dim3(coset_threads<true>()), 0, st, mask, mpitch, dst, s, tp);
+  else
+    hipLaunchKernelGGL(k_jfa_coset<false>, grid, dim3(coset_threads<false>()), 0, st, mask, mpitch, dst, s, tp);
   return hipGetLastError();
 }
 

@@ -91,6 +91,7 @@ bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTa
   tp->scx = (float)(mx / s.W);
   tp->scy = (float)(mx / s.H);
   tp->dinit = (float)mx * (float)mx;
+  tp->inv_mx = 1.0f / (float)mx;  // exact: a power of two
   return true;
 }
 

@@ -503,6 +503,7 @@ def test_jfa_lds_staging_is_bit_identical(RC2DGI, W, H, N, storage):
     ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
+    ctx.set_tuning("jfa_coset", 0)  # the per-step kernels (the fused long steps are tested below)
     out = {}
     for lds in (0, 1):
         ctx.set_tuning("jfa_lds", lds)
@@ -510,6 +511,31 @@ def test_jfa_lds_staging_is_bit_identical(RC2DGI, W, H, N, storage):
         ctx.do_rc2dgi()
         ctx.sync()
         out[lds] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
+    for k in out[0]:
+        assert np.array_equal(out[0][k], out[1][k]), f"{k}: {np.count_nonzero(out[0][k] != out[1][k])}"
+    ctx.close()
+
+
+@pytest.mark.parametrize("W,H,N,storage", [(256, 256, 4, "f32"), (512, 512, 4, "f32"), (1024, 1024, 5, "f32"),
+                                           (512, 256, 4, "f32"), (512, 512, 4, "rgba8"), (4096, 4096, 6, "f32"),
+                                           (8192, 8192, 8, "f32")])
+def test_jfa_coset_long_steps_are_bit_identical(RC2DGI, W, H, N, storage):
+    """The first four JumpFlood steps in one kernel (k_jfa_coset, tuning jfa_coset: square power-of-two
+    screens >= 512, the residues modulo W/16 as 16 x 16 tori in LDS) leave the same jumpRT1 / jumpRT2,
+    distance field and frame as the per-step kernels: integer keys (<= 4096), float keys (8192^2);
+    screens it does not take (256^2, non-square, RGBA8) are unchanged."""
+    color, emis = make_scene("demo", W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for on in (0, 1):
+        ctx.set_tuning("jfa_coset", on)
+        assert ctx.get_tuning("jfa_coset") == on
+        ctx.set_tuning("poison", 1)
+        ctx.do_rc2dgi()
+        ctx.sync()
+        out[on] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
     for k in out[0]:
         assert np.array_equal(out[0][k], out[1][k]), f"{k}: {np.count_nonzero(out[0][k] != out[1][k])}"
     ctx.close()
