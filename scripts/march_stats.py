@@ -37,7 +37,7 @@ def main():
     L.rc2dgi_diag_stats(buf.ctypes.data, 1)
     out = {}
     for lv in range(N):
-        slots, samples, waves = (int(x) for x in buf[lv])
+        slots, samples, waves = (int(x) for x in buf.reshape(-1)[3 * lv:3 * lv + 3])  # P.stats[level * 3 + i]
         rays = 4 * W * W
         out[f"L{lv}"] = {"samples_per_ray": round(samples / rays, 3), "slot_iters_per_ray": round(slots / rays, 3),
                          "lockstep_efficiency": round(samples / max(slots, 1), 3),
