@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Wave-lifetime split of k_rc_level per level and section (diagnostic build librc2dgi_timing.so,
 python -m radiancecascade2dglobalillumination_amd._build timing): mean cycles per wave in
-setup (staging loads issued, bound table to LDS, barrier) / rays (origins, proofs) / march (lockstep)
+map (workgroup-map scalar load) / table (staging loads issued, proof table loaded and written to LDS) /
+barrier / rays (origins, proofs) / march (lockstep)
 / tail (queue, barrier) / stage_write (LDS, barrier) / merge (shading loads, bilinear, store).
 Run with the committed bench schedule; extra --tune KEY=VALUE knobs.  Prints one JSON line."""
 import argparse
@@ -13,7 +14,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("RC2DGI_LIB", os.path.join(ROOT, "build", "diag", "librc2dgi_timing.so"))
-SECTIONS = ["setup", "rays", "march", "tail", "stage_write", "merge"]
+SECTIONS = ["map", "table", "barrier", "rays", "march", "tail", "stage_write", "merge"]
 
 
 def main():
