@@ -309,7 +309,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                      const uint4 *__restrict__ dpk) {
   RC_SECTION("setup");
 #ifdef RC2DGI_DIAG_TIMING
-  unsigned long long rc_ts[8];
+  unsigned long long rc_ts[9];
 #endif
   RC_TSTAMP(0);
   constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
@@ -364,6 +364,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
   const uint2 wgm = ld_uniform(P.wg_map + blockIdx.x);
   const int tx = (int)(wgm.x & 0xFFFFu), ty = (int)(wgm.x >> 16), dgi = (int)wgm.y;
+#ifdef RC2DGI_DIAG_TIMING
+  asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(wgm.x), "s"(wgm.y));  // the map has arrived
+#endif
+  RC_TSTAMP(1);
   (void)ngrp;
   const int bi0 = dgi * PD;  // first blockIndex = blk.x + blk.y * blockSqrtCount
   // Directional miss proofs (one-probe tiles at levels with 4^L >= kDirBins, P.dclr; they replace the
@@ -517,12 +521,17 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4)
           reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
     }
+#ifdef RC2DGI_DIAG_TIMING
+    if (cm || dp)  // (diagnostic: the table's words have arrived -- not the staging loads behind them)
+      for (int j = 0; j < CPT; ++j) asm volatile("" ::"v"(cmv[j].x), "v"(cmv[j].w));
+#endif
+    RC_TSTAMP(2);
     if (tl && threadIdx.x == 0) s_qn = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   }
-  RC_TSTAMP(1);
+  RC_TSTAMP(3);
   // Workgroup-wide exit proof: a ray's first sample o + (t0 dir) asp lies within t0 (uv) of its
   // probe on each axis, so inside the tile's probe box grown by t0.  When every bound-table cell
   // under that box proves exit for a first sample (dl > 0 and t0 + dl > t1: every sample there
@@ -624,7 +633,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   for (int k = 0; k < NR; ++k) more |= t[k] < kDone;
   const int itend = tl ? max(0, min(P.tailk, RC2DGI_DIAG_MAX_ITERS)) : RC2DGI_DIAG_MAX_ITERS;
   RC_SECTION("march");
-  RC_TSTAMP(2);
+  RC_TSTAMP(4);
   // BOFF with P2S: floor(p * 2W) & (2W - 2) = 2 (floor(p W) & (W - 1)) (p W and p 2W are exact)
   const float sWx = (BOFF && P2S) ? 2.0f * P.sWf : P.sWf;
   const int wmask = (BOFF && P2S) ? 2 * P.s.W - 2 : P.s.W - 1;
@@ -761,7 +770,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #endif
 
   RC_SECTION("tail");
-  RC_TSTAMP(3);
+  RC_TSTAMP(5);
   int qpos[TLC ? NR : 1];  // queue entry of each pending ray of this lane
   if (tl) {
     // pending rays (still marching after itend iterations) -> LDS queue, wave-contiguous ranges
@@ -839,7 +848,19 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
   }
 
-  RC_TSTAMP(4);
+  // Hit shading records (k_shade; RadianceCascades.fs:79-86), one load of the texel's record per hit ray,
+  // under the hit mask: a wave whose rays all miss skips the load -- an unconditional load of a "miss" record
+  // was measured 5 % slower at L0-L2.  The several-rays-per-lane tiles (no tail queue) load them here, so
+  // that the round trip overlaps the staging's LDS writes and the barrier (L0 0.126 -> 0.123 ms); in the
+  // one-probe tiles the same placement cost L4 / L5 3-6 us (the loads join the queue behind the march's
+  // gathers), so they load at the merge (profiles/r03/ab/late_loads.txt).
+  float4 hr[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    hr[k] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+    if (!TLC && hit_idx[k] >= 0) hr[k] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
+  }
+  RC_TSTAMP(6);
   RC_SECTION("stage_write");
   if (STG) {
 #pragma unroll
@@ -865,8 +886,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     for (int k = 0; k < NR; ++k)
       if (t[k] < kDone) hit_idx[k] = (int)s_q[qpos[k]].x;
   }
+  if constexpr (TLC) {  // (see hr above)
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      if (hit_idx[k] >= 0) hr[k] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
+  }
 
-  RC_TSTAMP(5);
+  RC_TSTAMP(7);
   RC_SECTION("merge");
   // ---- hit shading, merge with the upper cascade or the sky, average (RadianceCascades.fs:79-88, 115-158)
   const bool pow2c = P2S || (P.c.powW && P.c.powH);  // P2S implies power-of-two cascades
@@ -891,18 +917,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       lx0 = (int)fx - ((cx0 >> 1) - 1);
       ly0 = (int)fy - ((cy0 >> 1) - 1);
     }
-    // hit shading of the probe's rays (RadianceCascades.fs:79-86): one load of the texel's
-    // surface record (k_shade: the emissive or the albedo + reflectivity branch, resolved once
-    // per frame for every hittable texel).  Loaded under the hit mask: a wave whose rays all miss
-    // skips the load (and its round trip) entirely; an unconditional load of a "miss" record was
-    // measured 5 % slower at L0-L2.
-    float4 hr[ND];
-#pragma unroll
-    for (int r = 0; r < ND; ++r) {
-      const int k = p * ND + r;
-      hr[r] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-      if (hit_idx[k] >= 0) hr[r] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
-    }
+    // (hit shading of the probe's rays: the records hr, loaded above)
 #pragma unroll
     for (int dblk = 0; dblk < PD; ++dblk) {
       const int bi = bi0 + dblk;
@@ -910,7 +925,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
         const int r = dblk * 4 + r4;  // index into the 4*PD directions
-        float4 rad = hr[r];
+        float4 rad = hr[p * ND + r];
         const int ai = bi * 4 + r4;  // angleIndex
         if (rad.w != 0.0f && (STG || TOP)) {
           if (!TOP) {
@@ -977,10 +992,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
   }
 #ifdef RC2DGI_DIAG_TIMING
-  RC_TSTAMP(6);
+  RC_TSTAMP(8);
   if ((threadIdx.x & 63) == 0) {  // spread over kDiagSlots copies (one hot address would serialize the atomics)
     unsigned long long *st = P.stats + 256 + ((size_t)(blockIdx.x * (TX * TY / 64) + (threadIdx.x >> 6)) % kDiagSlots) * 256;
-    for (int i = 0; i < 6; ++i) atomicAdd(&st[P.level * 16 + i], rc_ts[i + 1] - rc_ts[i]);
+    for (int i = 0; i < 8; ++i) atomicAdd(&st[P.level * 16 + i], rc_ts[i + 1] - rc_ts[i]);
     atomicAdd(&st[P.level * 16 + 15], 1ull);
   }
 #endif
