@@ -47,10 +47,12 @@ def committed_schedule(W, H, N, rr, storage="f32"):
         return json.load(f)
 
 
-def apply_schedule(ctx, sched, N):
+def apply_schedule(ctx, sched, N, shards=1):
+    """the committed schedule, or its row-strip entry for `shards` strips (as bench.py applies it)"""
+    sub = (sched.get("strips") or {}).get(str(shards), {}) if shards > 1 else {}
     for L in range(N):
-        ctx.set_tuning(f"rc_order_L{L}", sched["rc_order"][L])
-        ctx.set_tuning(f"rc_variant_L{L}", sched["rc_variant"][L])
+        ctx.set_tuning(f"rc_order_L{L}", (sub.get("rc_order") or sched["rc_order"])[L])
+        ctx.set_tuning(f"rc_variant_L{L}", (sub.get("rc_variant") or sched["rc_variant"])[L])
 
 
 def level_offsets(N):
@@ -208,8 +210,9 @@ def test_c1_vs_llvmpipe_fixture(R):
 def test_c3_8192_eight_row_strips(R):
     """8192^2, N=8, rayRange 64 split into 8 row strips, run as 8 in-process shard
     contexts with the distRT exchange (rc2dgi_do_group), intermediates poisoned, all with the
-    committed schedule bench.py --mode strips times (tuning/8192x8192_N8_rr64_f32.json, the
-    packed-field march at L4): every shard's colorRT / tempRT strip equals the unsharded frame bit for bit, and
+    committed schedules bench.py times (tuning/8192x8192_N8_rr64_f32.json: the packed-field march at L4 for
+    the whole frame, its "strips" entry for the shards; the shards make their surface records at the hit):
+    every shard's colorRT / tempRT strip equals the unsharded frame bit for bit, and
     the unsharded frame is checked against the oracle (JFA + DF whole frame, 1/4 of the rows of
     every level, blur / merge on every 8th row)."""
     from radiancecascade2dglobalillumination_amd import scenes
@@ -249,7 +252,7 @@ def test_c3_8192_eight_row_strips(R):
         g = R.RC2DGI(W, H, cascade_count=N, ray_range=rr)
         g.upload("color", color)
         g.upload("emissive", emis)
-        apply_schedule(g, sched, N)
+        apply_schedule(g, sched, N, P)  # the strips' own entry (bench.py --mode strips --shards 8 times it)
         g.set_tuning("poison", 1)
         g.set_shard(k, P)
         shards.append(g)
