@@ -507,20 +507,30 @@ def main():
         ctx.do_rc2dgi()
     ctx.sync()
 
+    # The timed steps carry events around the passes only (timing mode 2): an event between two
+    # levels idles the GPU ~5 us (rocprofv3 trace), which a frame without timing does not.
+    ctx.set_timing(2)
     rc_ms, tot_ms, lvl_ms = [], [], np.zeros(N)
     rdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         ctx.do_rc2dgi()
-        t = ctx.pass_times(levels=N)  # waits for this frame's last event
+        t = ctx.pass_times()  # waits for this frame's last event
         rc_ms.append(t["rc"])
         tot_ms.append(t["total"])
-        lvl_ms += np.array(t["levels"])
     ctx.sync()
     torch.cuda.synchronize()
     rdist.barrier()
     wall = time.perf_counter() - t0
+    # per-level breakdown (and the gather / VALU rooflines priced on it): further frames with an
+    # event around every level, after the timed region
+    ctx.set_timing(True)
+    lvl_steps = max(1, min(a.steps, 20))
+    for _ in range(lvl_steps):
+        ctx.do_rc2dgi()
+        lvl_ms += np.array(ctx.pass_times(levels=N)["levels"])
+    lvl_ms *= a.steps / lvl_steps  # (as a sum over a.steps frames, like rc_ms)
     t_rc, t_tot, wall = rdist.max_over_ranks([sum(rc_ms), sum(tot_ms), wall], device="cuda")
     units = CW * CH * N * a.steps * world
     value = units / (t_rc / 1e3) / 1e6
@@ -562,6 +572,7 @@ def main():
                                    ("default" if a.no_autotune else "autotune in setup"))},
         "rc_ms_per_frame": round(t_rc / a.steps, 4),
         "rc_level_ms": [round(x / a.steps, 4) for x in lvl_ms.tolist()],
+        "rc_level_timing": f"{lvl_steps} further frames with an event around every level (timing mode 1)",
         "full_pipeline_ms": round(t_tot / a.steps, 4),
         "full_pipeline_fps": round(1e3 * a.steps / t_tot, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

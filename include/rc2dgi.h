@@ -139,11 +139,13 @@ const char *rc2dgi_last_error(rc2dgi_ctx *ctx);
 int rc2dgi_abi_version(void);
 
 /* ---- stream / timing.  rc2dgi_set_stream: run on a caller-owned hipStream_t on the
- * context's device (NULL = back to the context's own stream).  With timing enabled,
- * rc2dgi_do() records HIP events around each pass; rc2dgi_pass_times() returns the last
- * frame's milliseconds in the order {screenuv, jfa (all steps, DF fused into the last),
- * rc (all N levels), blur (+copy-back), merge (+copy-back), total} and, when
- * level_ms != NULL, the N per-level RC times indexed by level. */
+ * context's device (NULL = back to the context's own stream).  rc2dgi_set_timing(ctx, mode):
+ * 0 off; 1 rc2dgi_do() records HIP events around each pass and each RC level; 2 around each
+ * pass only (every event idles the GPU a few microseconds before the next kernel, so mode 2
+ * times the RC pass as it runs untimed).  rc2dgi_pass_times() returns the last frame's
+ * milliseconds in the order {screenuv, jfa (all steps, DF fused into the last), rc (all N
+ * levels), blur (+copy-back), merge (+copy-back), total} and, when level_ms != NULL (the
+ * last frame ran in mode 1, else RC2DGI_E_STATE), the N per-level RC times indexed by level. */
 int rc2dgi_set_stream(rc2dgi_ctx *ctx, void *hip_stream);
 int rc2dgi_set_timing(rc2dgi_ctx *ctx, int enable);
 int rc2dgi_pass_times(rc2dgi_ctx *ctx, float *pass_ms, int n_pass, float *level_ms, int n_level);

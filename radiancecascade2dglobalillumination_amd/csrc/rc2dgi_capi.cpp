@@ -119,7 +119,8 @@ struct rc2dgi_ctx {
   bool frame_done = false;   // colorRT holds the merged result
   bool have_frame = false;
   int final_gi = 1;
-  bool timing = false;
+  bool level_times = false;  // the last frame recorded ev_level
+  int timing = 0;  // rc2dgi_set_timing: 0 off, 1 pass and per-level events, 2 pass events only
   hipEvent_t ev[P_COUNT + 1] = {};
   std::vector<hipEvent_t> ev_level;  // N + 1
   std::vector<int> rc_variant;  // per level tile shape (tuning)
@@ -189,6 +190,19 @@ void derive_sizes(int W, int H, int N, float rs, int &CW, int &CH, int &S) {
   const int mx = W > H ? W : H;
   S = (int)std::ceil(std::log((double)mx) / std::log(2.0));
   if (S < 1) S = 1;
+}
+
+// Flags of the timing events (per pass, per cascade level).  They only timestamp the stream, so they skip
+// the system-scope fence (L2 writeback / invalidate) a default event performs: with it every event left
+// the next kernel a colder cache (RC pass 1.473 -> 1.461 ms, profiles/r03/ab/events.txt).  Every event
+// still leaves a ~5 us idle gap before the next kernel (rocprofv3 trace), hence timing mode 2 (passes
+// only, rc2dgi_set_timing).  RC2DGI_TIMING_EVENT_FLAGS (an int) overrides the flags for experiments.
+unsigned timing_event_flags() {
+  static const unsigned f = [] {
+    const char *v = getenv("RC2DGI_TIMING_EVENT_FLAGS");
+    return v ? (unsigned)strtoul(v, nullptr, 0) : (unsigned)hipEventDisableSystemFence;
+  }();
+  return f;
 }
 
 // tail compaction default: rays still marching after kDefaultTail lockstep iterations finish one per lane
@@ -542,7 +556,7 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
     return e == hipErrorOutOfMemory ? RC2DGI_E_OOM : RC2DGI_E_HIP;
   }
   c->stream = c->own_stream;
-  for (auto &ev : c->ev) (void)hipEventCreate(&ev);
+  for (auto &ev : c->ev) (void)hipEventCreateWithFlags(&ev, timing_event_flags());
   (void)hipEventCreateWithFlags(&c->ev_phase1, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&c->ev_frame, hipEventDisableTiming);
   for (auto &ev : c->ev_jfa) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
@@ -552,7 +566,7 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
     rc2dgi_destroy(c);
     return rc;
   }
-  for (auto &ev : c->ev_level) (void)hipEventCreate(&ev);
+  for (auto &ev : c->ev_level) (void)hipEventCreateWithFlags(&ev, timing_event_flags());
   *out = c;
   return RC2DGI_OK;
 }
@@ -646,7 +660,7 @@ int rc2dgi_set_uniform_i(rc2dgi_ctx *c, const char *name, int v) {
     c->broken = true;  // no half-allocated context runs a frame: every later call reports it
     return rc;
   }
-  for (auto &ev : c->ev_level) (void)hipEventCreate(&ev);
+  for (auto &ev : c->ev_level) (void)hipEventCreateWithFlags(&ev, timing_event_flags());
   HIPCHK(c, hipMemcpy(c->color_in, col.data(), col.size() * sizeof(float4), hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->emissive, em.data(), em.size() * sizeof(float4), hipMemcpyHostToDevice));
   return RC2DGI_OK;
@@ -875,7 +889,9 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   const bool T = c->timing;
   // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362).  The "t" / "p" / "o" variants read re-laid-out
   // copies of distRT; building them is timed with the top level (it is RC work, not DistanceField's)
-  if (T) HIPCHK(c, hipEventRecord(c->ev_level[c->N], st));
+  // per-level events only in timing mode 1: each one idles the GPU ~5 us before the next level
+  const bool LT = c->timing == 1;
+  if (LT) HIPCHK(c, hipEventRecord(c->ev_level[c->N], st));
   bool tiled = false, packed = false, nib = false;
   for (int v : c->rc_variant) {
     tiled |= rc_variant_tiled(v);
@@ -898,7 +914,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   for (int L = c->N - 1; L >= 0; --L) {
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
     float4 *dstGI = gi1final ? c->gi2 : c->gi1;
-    if (T && L + 1 < c->N) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
+    if (LT && L + 1 < c->N) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
     RcLevelArgs a;
     a.upper = (L == c->N - 1) ? nullptr : srcGI;
     a.out = dstGI;
@@ -934,7 +950,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
                                hipMemcpyDeviceToDevice, st));
     gi1final = !gi1final;
   }
-  if (T) HIPCHK(c, hipEventRecord(c->ev_level[0], st));
+  if (LT) HIPCHK(c, hipEventRecord(c->ev_level[0], st));
   if (T) HIPCHK(c, hipEventRecord(c->ev[3], st));
   float4 *&finalGI = gi1final ? c->gi1 : c->gi2;  // RC2DGI.cs:365
   c->final_gi = gi1final ? 1 : 2;
@@ -983,6 +999,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   if (T) HIPCHK(c, hipEventRecord(c->ev[5], st));
   c->frame_done = true;
   c->have_frame = true;
+  c->level_times = LT;
   return RC2DGI_OK;
 }
 
@@ -1037,8 +1054,8 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   RC2DGI_USABLE(c);
   if (c->world > 1) return fail(c, RC2DGI_E_STATE, "autotune an unsharded context (the orders carry over)");
   if (frames < 1) frames = 1;
-  const bool timing = c->timing;
-  c->timing = true;
+  const int timing = c->timing;
+  c->timing = 1;
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
   // march rolled / unrolled x linear / 8x8-tiled / packed / nibble-predicted distance field; 32x8 tiles
   // (x2 probes per lane)
@@ -1320,7 +1337,9 @@ int rc2dgi_set_stream(rc2dgi_ctx *c, void *s) {
 
 int rc2dgi_set_timing(rc2dgi_ctx *c, int enable) {
   if (!c) return RC2DGI_E_ARG;
-  c->timing = enable != 0;
+  if (enable < 0 || enable > 2) return fail(c, RC2DGI_E_ARG, "timing mode is 0 (off), 1 (passes + levels) or 2 (passes)");
+  c->timing = enable;
+  c->level_times = false;
   return RC2DGI_OK;
 }
 
@@ -1335,6 +1354,8 @@ int rc2dgi_pass_times(rc2dgi_ctx *c, float *pass_ms, int n_pass, float *level_ms
   HIPCHK(c, hipEventElapsedTime(&t[P_TOTAL], c->ev[0], c->ev[5]));
   if (pass_ms)
     for (int p = 0; p < n_pass && p < P_COUNT; ++p) pass_ms[p] = t[p];
+  if (level_ms && !c->level_times)
+    return fail(c, RC2DGI_E_STATE, "per-level times need timing mode 1 for the last frame");
   if (level_ms)
     for (int L = 0; L < n_level && L < c->N; ++L)
       HIPCHK(c, hipEventElapsedTime(&level_ms[L], c->ev_level[L + 1], c->ev_level[L]));

@@ -337,8 +337,11 @@ class RC2DGI:
     def set_stream(self, hip_stream: Optional[int]) -> None:
         self._check(self._L.rc2dgi_set_stream(self._h, ctypes.c_void_p(hip_stream or 0)), "set_stream")
 
-    def set_timing(self, enable: bool = True) -> None:
-        self._check(self._L.rc2dgi_set_timing(self._h, int(bool(enable))), "set_timing")
+    def set_timing(self, enable=True) -> None:
+        """True / 1: events around every pass and RC level; 2: around every pass only (no idle gaps
+        between the levels); False / 0: off."""
+        mode = 2 if enable == 2 and not isinstance(enable, bool) else int(bool(enable))
+        self._check(self._L.rc2dgi_set_timing(self._h, mode), "set_timing")
 
     def pass_times(self, levels: int = 0):
         """HIP-event milliseconds of the last frame: dict(screenuv, jfa, rc, blur, merge, total[, levels])."""

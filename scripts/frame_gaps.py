@@ -1,0 +1,15 @@
+#!/usr/bin/env python3
+"""Kernels of the last whole frame of a rocprofv3 kernel trace with the idle gap before each one
+(usage: frame_gaps.py run_kernel_trace.csv).  A frame starts at k_occupancy."""
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+starts = [i for i, r in enumerate(rows) if "k_occupancy" in r["Kernel_Name"]]
+lo, hi = (starts[-2], starts[-1]) if len(starts) > 1 else (starts[-1], len(rows))
+prev_end = None
+for r in rows[lo:hi]:
+    st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    gap = (st - prev_end) / 1e3 if prev_end is not None else 0.0
+    print(f"{r['Kernel_Name'][:72]:72s} gap {gap:7.2f} us  dur {(en - st) / 1e3:8.2f} us")
+    prev_end = en if prev_end is None else max(prev_end, en)

@@ -353,6 +353,16 @@ def test_timing_reports_passes(RC2DGI):
     t = ctx.pass_times(levels=4)
     assert t["total"] > 0 and all(v >= 0 for k, v in t.items() if k != "levels")
     assert len(t["levels"]) == 4 and sum(t["levels"]) <= t["rc"] * 1.01 + 0.05
+    # mode 2: pass events only (no per-level events, which idle the GPU between levels)
+    ctx.set_timing(2)
+    ctx.frame(color, emis)
+    t2 = ctx.pass_times()
+    assert t2["rc"] > 0 and t2["total"] >= t2["rc"]
+    with pytest.raises(RuntimeError):
+        ctx.pass_times(levels=4)
+    ctx.set_timing(True)
+    ctx.frame(color, emis)
+    assert len(ctx.pass_times(levels=4)["levels"]) == 4
     ctx.close()
 
 
