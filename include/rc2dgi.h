@@ -173,6 +173,8 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *   "rc_wgproof"      1 (default): a workgroup whose first samples all provably miss skips the march
  *   "rc_tail" / "rc_tail_L<n>"  rays still marching after this many lockstep iterations finish one
  *                     per lane in a compacted queue (0 off; default 10)
+ *   "shade_fused"     1 (default): surface records and the proofs' bound table in one pass over
+ *                     distRT where its cells are >= 64 texels (square power-of-two screens >= 4096)
  * rc2dgi_get_tuning also answers "rc_variant_count". */
 int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
 /* time `frames` frames per candidate workgroup order x march variant ("rc_variant" 0 / 13 / 14 / 15) on

@@ -134,6 +134,7 @@ struct rc2dgi_ctx {
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   int jfa_coset = 1;             // tuning "jfa_coset": the first four steps in one kernel (k_jfa_coset) where they apply
+  int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
@@ -901,14 +902,20 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
   if (packed) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
   if (nib) HIPCHK(c, launch_dist_nib(c->dist, c->sd.pitch, c->dist_n, c->W, c->H, st));
-  HIPCHK(c, launch_shade(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, st));
   // exit proofs: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
   // staging and barrier cost more than the skipped samples save (RC 0.338 vs 0.376 ms, measured)
   const bool proofs = c->rc_skip > 1 || (c->rc_skip == 1 && std::max(c->W, c->H) >= 2048);
   bool mps = false;
   for (int v : c->rc_mp) mps |= v != 0;
   mps = mps && proofs;
-  if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
+  // surface records and the bound table in one pass over distRT where its cells are >= 64 texels
+  if (proofs && c->shade_fused && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch)) {
+    HIPCHK(c, launch_shade_cmin(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, c->cmin,
+                                mps ? c->hitc : nullptr, st));
+  } else {
+    HIPCHK(c, launch_shade(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, st));
+    if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
+  }
   if (mps) HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
   bool gi1final = false;
   for (int L = c->N - 1; L >= 0; --L) {
@@ -1432,6 +1439,10 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->jfa_coset = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "shade_fused") {
+    c->shade_fused = value != 0;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_lds") {
     c->jfa_lds = value != 0;
     return RC2DGI_OK;
@@ -1503,6 +1514,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "jfa_coset") {
     *value = c->jfa_coset;
+    return RC2DGI_OK;
+  }
+  if (k == "shade_fused") {
+    *value = c->shade_fused;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_tail_L", 0) == 0) {

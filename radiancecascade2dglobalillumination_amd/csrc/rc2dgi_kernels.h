@@ -141,6 +141,11 @@ struct RcLevelArgs {
 int dist_cmin_shift(int W, int H);
 // hitc (optional): per cell 1 when a texel the march may sample there passes the hit test (the REPEAT wrap of
 // u = 1 / v = 1 onto column / row 0 included in the last cell column / row), else 0
+// launch_shade and launch_dist_cmin (with hitc) as one pass over distRT: square power-of-two screens with
+// cells of >= 64 texels only (shade_cmin_fused_ok; 4096^2 and up)
+bool shade_cmin_fused_ok(int W, int H, int pitch);
+hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
+                             ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st);
 hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st,
                             unsigned char *hitc = nullptr);
 // Directional clear distances of the march proofs (k_rc_level, one-probe tiles): kDirBins angular bins x

@@ -552,6 +552,74 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
   }
 }
 
+// k_shade and k_dist_cmin in one pass over distRT, for square power-of-two screens with cells of >= 64
+// texels (W = H = kCminDim << csh, csh >= 6: 4096^2 and up).  One workgroup per cell; wave w takes rows
+// w, w + 4, ... of it, a lane one column of each 64-column run, four rows at a time (each load instruction
+// one contiguous run: 128 B of distance, 1 KB of emission or albedo).  Same records, same bound table and
+// flags as the two kernels (the cell minimum includes the REPEAT-wrap texels of the last row / column).
+__global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__restrict__ dist,
+                                                    const float4 *__restrict__ color, const float4 *__restrict__ emis,
+                                                    float4 *__restrict__ shade, ScreenDims s, float reflectivity,
+                                                    int csh, CminT *__restrict__ cmin, unsigned char *__restrict__ hitc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cw = 1 << csh;
+  const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
+  unsigned m = 0xFFFFu;
+  for (int c = lane; c < cw; c += 64) {
+    for (int r0 = w; r0 < cw; r0 += 16) {
+      size_t at[4];
+      unsigned q[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        at[t] = (size_t)(y0 + r0 + 4 * t) * s.pitch + x0 + c;
+        q[t] = dist[at[t]];
+      }
+      bool h[4];
+      float4 e[4], cl[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        m = min(m, q[t]);
+        h[t] = decode_dist(q[t]) < 0.001f;
+        e[t] = cl[t] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (h[t]) {
+          e[t] = emis[at[t]];
+          cl[t] = color[at[t]];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (h[t]) {
+          float4 rec = make_float4(e[t].x, e[t].y, e[t].z, 1.0f);
+          if (!(sqrtf(e[t].x * e[t].x + e[t].y * e[t].y + e[t].z * e[t].z) > 0.0f))
+            rec = make_float4(cl[t].x, cl[t].y, cl[t].z, reflectivity);
+          shade[at[t]] = rec;
+        }
+      }
+    }
+  }
+  // REPEAT wrap (k_dist_cmin): samples at u = 1 / v = 1 read column 0 / row 0
+  if (x0 + cw == s.W)
+    for (int e = (int)threadIdx.x; e < cw; e += 256) m = min(m, (unsigned)dist[(size_t)(y0 + e) * s.pitch]);
+  if (y0 + cw == s.H)
+    for (int e = (int)threadIdx.x; e < cw; e += 256) m = min(m, (unsigned)dist[x0 + e]);
+  if (x0 + cw == s.W && y0 + cw == s.H && threadIdx.x == 0) m = min(m, (unsigned)dist[0]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, o, 64));
+  __shared__ unsigned s_m[4];
+  if (lane == 0) s_m[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
+    const float d = decode_dist(m);
+    if (hitc) hitc[blockIdx.y * kCminDim + blockIdx.x] = d < 0.001f ? 1 : 0;
+#ifdef RC2DGI_CMIN_U8
+    cmin[blockIdx.y * kCminDim + blockIdx.x] = d >= 0.001f ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
+#else
+    cmin[blockIdx.y * kCminDim + blockIdx.x] = d >= 0.001f ? d : 0.0f;
+#endif
+  }
+}
+
 // ---------------------------------------------------------------- directional clear distances (march proofs)
 // dclr[j][c] = s: from any point of cell c (kCminDim x kCminDim cells of 2^csh texels, k_dist_cmin's grid) and
 // for every direction of angular bin j (angles [2 pi j / kDirBins, 2 pi (j + 1) / kDirBins)), the ray stays
@@ -1457,6 +1525,19 @@ hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, 
                             unsigned char *hitc) {
   hipLaunchKernelGGL(k_dist_cmin, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, pitch, cmin, W, H,
                      dist_cmin_shift(W, H), hitc);
+  return hipGetLastError();
+}
+
+bool shade_cmin_fused_ok(int W, int H, int pitch) {
+  const int csh = dist_cmin_shift(W, H);
+  return csh >= 6 && W == H && W == (kCminDim << csh) && pitch % 64 == 0;
+}
+
+hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
+                             ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st) {
+  if (!shade_cmin_fused_ok(s.W, s.H, s.pitch)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_shade_cmin, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, color, emis, shade, s, reflectivity,
+                     dist_cmin_shift(s.W, s.H), cmin, hitc);
   return hipGetLastError();
 }
 

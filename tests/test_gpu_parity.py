@@ -551,6 +551,30 @@ def test_jfa_coset_long_steps_are_bit_identical(RC2DGI, W, H, N, storage):
     ctx.close()
 
 
+@pytest.mark.parametrize("W,H,N", [(4096, 4096, 6), (8192, 8192, 8)])
+def test_shade_cmin_fused_is_bit_identical(RC2DGI, W, H, N):
+    """k_shade_cmin (surface records + the proofs' bound table and hit flags in one pass over distRT,
+    tuning shade_fused) gives the same frame as k_shade + k_dist_cmin: every level at 4096^2, the merged
+    colorRT at 8192^2."""
+    color, emis = make_scene("demo", W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0)
+    ctx.set_keep_levels(W <= 4096)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for on in (0, 1):
+        ctx.set_tuning("shade_fused", on)
+        assert ctx.get_tuning("shade_fused") == on
+        ctx.do_rc2dgi()
+        ctx.sync()
+        out[on] = {"color": ctx.download("color")}
+        if W <= 4096:
+            out[on].update({f"G{L}": ctx.download_level(L) for L in range(N)})
+    for k in out[0]:
+        assert np.array_equal(out[0][k], out[1][k]), f"{k}: {np.count_nonzero(out[0][k] != out[1][k])}"
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,N", [(256, 256, 4), (512, 256, 4), (240, 180, 3)])
 def test_degenerate_direction_tables(RC2DGI, W, H, N):
     """Direction tables with exact zero components, unit axes, components below the exit table's
