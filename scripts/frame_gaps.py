@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
-"""Kernels of the last whole frame of a rocprofv3 kernel trace with the idle gap before each one
-(usage: frame_gaps.py run_kernel_trace.csv).  A frame starts at k_occupancy."""
+"""Kernels of one whole frame of a rocprofv3 kernel trace with the idle gap before each one
+(usage: frame_gaps.py run_kernel_trace.csv [k]: the k-th frame from the end, default 1 = the last;
+bench.py's timed frames (timing mode 2) come before its per-level frames).  A frame starts at k_occupancy."""
 import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if "k_occupancy" in r["Kernel_Name"]]
-lo, hi = (starts[-2], starts[-1]) if len(starts) > 1 else (starts[-1], len(rows))
+k = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+lo, hi = (starts[-k - 1], starts[-k]) if len(starts) > k else (starts[-1], len(rows))
 prev_end = None
 for r in rows[lo:hi]:
     st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
