@@ -554,7 +554,7 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
 
 // k_shade and k_dist_cmin in one pass over distRT, for square power-of-two screens with cells of >= 64
 // texels (W = H = kCminDim << csh, csh >= 6: 4096^2 and up).  One workgroup per cell; wave w takes rows
-// w, w + 4, ... of it, a lane one column of each 64-column run, four rows at a time (each load instruction
+// w, w + 4, ... of it, a lane one column of each 64-column run, 16 rows at a time (each load instruction
 // one contiguous run: 128 B of distance, 1 KB of emission or albedo).  Same records, same bound table and
 // flags as the two kernels (the cell minimum includes the REPEAT-wrap texels of the last row / column).
 __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__restrict__ dist,
@@ -565,34 +565,41 @@ __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__rest
   const int cw = 1 << csh;
   const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
   unsigned m = 0xFFFFu;
+  const size_t rstep = (size_t)4 * s.pitch;  // a wave's consecutive rows are 4 apart
   for (int c = lane; c < cw; c += 64) {
-    for (int r0 = w; r0 < cw; r0 += 16) {
-      size_t at[4];
-      unsigned q[4];
+    for (int rb = 0; rb < cw; rb += 64) {
+      // the wave's 16 rows of this 64-row block: every distance load in flight at once, then the records
+      // of the hittable texels 8 rows at a time (two round trips, not one per 4 rows)
+      const size_t base = (size_t)(y0 + rb + w) * s.pitch + x0 + c;
+      unsigned q[16];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        at[t] = (size_t)(y0 + r0 + 4 * t) * s.pitch + x0 + c;
-        q[t] = dist[at[t]];
-      }
-      bool h[4];
-      float4 e[4], cl[4];
+      for (int t = 0; t < 16; ++t) q[t] = dist[base + t * rstep];
+      unsigned hm = 0;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+      for (int t = 0; t < 16; ++t) {
         m = min(m, q[t]);
-        h[t] = decode_dist(q[t]) < 0.001f;
-        e[t] = cl[t] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (h[t]) {
-          e[t] = emis[at[t]];
-          cl[t] = color[at[t]];
-        }
+        hm |= decode_dist(q[t]) < 0.001f ? 1u << t : 0u;
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (h[t]) {
-          float4 rec = make_float4(e[t].x, e[t].y, e[t].z, 1.0f);
-          if (!(sqrtf(e[t].x * e[t].x + e[t].y * e[t].y + e[t].z * e[t].z) > 0.0f))
-            rec = make_float4(cl[t].x, cl[t].y, cl[t].z, reflectivity);
-          shade[at[t]] = rec;
+      for (int h = 0; h < 2; ++h) {
+        if (!(hm >> (8 * h) & 0xFFu)) continue;
+        float4 e[8], cl[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          e[k] = cl[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          if (hm >> (8 * h + k) & 1u) {
+            e[k] = emis[base + (8 * h + k) * rstep];
+            cl[k] = color[base + (8 * h + k) * rstep];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (hm >> (8 * h + k) & 1u) {
+            float4 rec = make_float4(e[k].x, e[k].y, e[k].z, 1.0f);
+            if (!(sqrtf(e[k].x * e[k].x + e[k].y * e[k].y + e[k].z * e[k].z) > 0.0f))
+              rec = make_float4(cl[k].x, cl[k].y, cl[k].z, reflectivity);
+            shade[base + (8 * h + k) * rstep] = rec;
+          }
         }
       }
     }
