@@ -635,8 +635,9 @@ __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__rest
 // u + d r (u in the cell, d in the bin, r in the step) lie in the box of the four chord corners grown by
 // the sagitta r (1 - cos(dtheta / 2)) and one texel (the fp32 rounding of positions and directions), and
 // the step's cells are the cells that box touches.  Cells off the grid are off screen: never sampled.
-// One thread per (bin, cell), a wave per row of cells (the row's step rows are wave-uniform): kDirBins x 16
-// workgroups of 4 rows; the flag grid as one 64-bit word per row in LDS.
+// A wave per (bin, row of cells), one lane per step: the step's row OR and box, then per cell of the row one
+// ballot of the steps that meet a hit cell: kDirBins x 16 workgroups of 4 rows; the flag grid as one 64-bit
+// word per row in LDS.
 __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restrict__ hitc,
                                                    const int4 *__restrict__ boxes,
                                                    unsigned char *__restrict__ dclr) {
@@ -661,38 +662,33 @@ __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restri
                         (unsigned long long)part[4 * threadIdx.x + 2] << 32 |
                         (unsigned long long)part[4 * threadIdx.x + 3] << 48;
   __syncthreads();
-  const int cx = c % D, cy = __builtin_amdgcn_readfirstlane(c / D);
+  const int cy = __builtin_amdgcn_readfirstlane(c / D);
   const int lane = (int)threadIdx.x & 63;
   // lane s holds step s of this wave's row: the OR of the grid rows its box covers (the rows do not
-  // depend on the cell's column) and the box's column offsets; the steps are then read back with
-  // v_readlane (wave-uniform), so the per-cell loop below is plain VALU
+  // depend on the cell's column) and the box's column offsets
   const int4 bl = box[lane];
   const int ly0 = max(0, cy + bl.z), ly1 = min(D - 1, cy + bl.w);
   unsigned long long orow = 0;
   for (int y = ly0; y <= ly1; ++y) orow |= rows[y];
-  // the boxes move outwards along the bin's directions: from the first step whose rows lie off the grid on
-  const unsigned long long off = __ballot(ly0 > ly1);
-  const int nsteps = off ? (int)__builtin_ctzll(off) : NS;
-  const unsigned olo = (unsigned)orow, ohi = (unsigned)(orow >> 32);
+  // the boxes move outwards along the bin's directions: from the first step whose rows lie off the grid on,
+  // nothing is reached
+  const unsigned long long voff = __ballot(ly0 > ly1);
+  const int nsteps = voff ? (int)__builtin_ctzll(voff) : NS;
+  // per cell of the row (wave-uniform loop), every step at once, one lane each: the first step whose box
+  // meets a hit cell, unless the box has left the grid sideways (so have the later steps) or vertically first
   int clear = 255;
-  bool done = false;
-  for (int s = 0; s < nsteps; ++s) {
-    const unsigned long long o = (unsigned long long)__builtin_amdgcn_readlane(ohi, s) << 32 |
-                                 (unsigned)__builtin_amdgcn_readlane(olo, s);
-    const int bx0 = __builtin_amdgcn_readlane(bl.x, s), bx1 = __builtin_amdgcn_readlane(bl.y, s);
-    const int x0 = max(0, cx + bx0), x1 = min(D - 1, cx + bx1);
-    if (!done) {
-      if (x0 > x1) {
-        done = true;  // (off the grid sideways: so are the later steps)
-      } else {
-        const unsigned long long mask = (x1 - x0 == 63 ? ~0ull : ((1ull << (x1 - x0 + 1)) - 1ull)) << x0;
-        if (o & mask) {
-          clear = s;
-          done = true;
-        }
-      }
+  for (int cx = 0; cx < D; ++cx) {
+    const int x0 = max(0, cx + bl.x), x1 = min(D - 1, cx + bl.y);
+    const bool off = x0 > x1;
+    bool hit = false;
+    if (!off) {
+      const unsigned long long mask = (x1 - x0 == 63 ? ~0ull : ((1ull << (x1 - x0 + 1)) - 1ull)) << x0;
+      hit = (orow & mask) != 0;
     }
-    if (__all(done)) break;
+    const unsigned long long hb = __ballot(hit), ob = __ballot(off);
+    const int first_hit = hb ? (int)__builtin_ctzll(hb) : NS;
+    const int first_off = min(nsteps, ob ? (int)__builtin_ctzll(ob) : NS);
+    if (lane == cx) clear = first_hit < first_off ? first_hit : 255;
   }
   dclr[(size_t)j * D * D + c] = (unsigned char)clear;
 }
