@@ -199,7 +199,8 @@ def schedule_path(W, H, N, ray_range=2.0, storage="f32"):
 def lib_variant_name(v):
     names = ["16x16x1", "16x8x2", "16x16x2", "32x8x1", "64x4x1", "8x8x1", "32x8x2", "16x16x1d2", "16x16x1d4",
              "16x8x1d2", "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t",
-             "16x16x1up", "16x16x1un", "16x16x1p", "16x16x1n"]
+             "16x16x1up", "16x16x1un", "16x16x1p", "16x16x1n", "32x16x1", "16x32x1", "32x32x1", "32x16x1u",
+             "32x32x1u"]
     return names[v] if v < len(names) else str(v)
 
 
@@ -230,9 +231,7 @@ def bench_batch(a, rank, local, world):
         with open(committed) as f:  # the committed schedule of this size (tested by the parity suite)
             tun = json.load(f)
         for g in ctxs:
-            for L in range(N):
-                g.set_tuning(f"rc_order_L{L}", tun["rc_order"][L])
-                g.set_tuning(f"rc_variant_L{L}", tun["rc_variant"][L])
+            apply_schedule(g, tun, N)
     elif ctxs and not a.no_autotune:  # setup: one context picks the schedule, the others reuse it
         ctxs[0].autotune(3)
         for g in ctxs[1:]:
@@ -280,6 +279,9 @@ def apply_schedule(g, tun, N, shards=1):
     for L in range(N):
         g.set_tuning(f"rc_order_L{L}", (sub.get("rc_order") or tun["rc_order"])[L])
         g.set_tuning(f"rc_variant_L{L}", (sub.get("rc_variant") or tun["rc_variant"])[L])
+        ph = sub.get("rc_phase") or tun.get("rc_phase")
+        if ph:  # optional: phase-plane march samples per level (rc_phase_L<n>)
+            g.set_tuning(f"rc_phase_L{L}", ph[L])
 
 
 def bench_strips(a, rank, local, world):
@@ -484,9 +486,7 @@ def main():
     if a.load_tuning:
         with open(a.load_tuning) as f:
             tun = json.load(f)
-        for L in range(N):
-            ctx.set_tuning(f"rc_order_L{L}", tun["rc_order"][L])
-            ctx.set_tuning(f"rc_variant_L{L}", tun["rc_variant"][L])
+        apply_schedule(ctx, tun, N)
         orders = tun["rc_order"]
     else:
         orders = None if a.no_autotune else ctx.autotune(3)  # setup: schedule choice, results identical
@@ -498,7 +498,8 @@ def main():
     if a.save_tuning and rank == 0:
         with open(a.save_tuning, "w") as f:
             json.dump({"config": f"{W}x{H} N={N} rayRange={a.ray_range} {a.storage}",
-                       "rc_order": [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)], "rc_variant": variants}, f)
+                       "rc_order": [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)], "rc_variant": variants,
+                       "rc_phase": [ctx.get_tuning(f"rc_phase_L{L}") for L in range(N)]}, f)
     ctx.set_timing(True)
     if a.sweep_rc:
         sweep_rc(ctx, N, a.steps, rounds=3)
@@ -567,6 +568,7 @@ def main():
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
                    "parallelism": f"replicas{world}",
                    "rc_order": orders or "default", "rc_variant": variants,
+                   "rc_phase": [ctx.get_tuning(f"rc_phase_L{L}") for L in range(N)],
                    "rc_skip": ctx.get_tuning("rc_skip"),
                    "rc_schedule": (os.path.relpath(a.load_tuning, ROOT) if a.load_tuning else
                                    ("default" if a.no_autotune else "autotune in setup"))},

@@ -102,6 +102,7 @@ struct rc2dgi_ctx {
   unsigned short *dist_t = nullptr;  // 8x8-tiled copy for the "t" RC variants
   uint4 *dist_p = nullptr;           // packed copy for the "p" RC variants (k_dist_pack)
   uint4 *dist_n = nullptr;           // nibble-predicted copy for the "n" RC variants (k_dist_nib)
+  std::vector<unsigned short *> dist_ph;  // per level: phase-plane copy of distRT (tuning rc_phase_L<n>, k_dist_phase)
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
   unsigned char *hitc = nullptr;     // per bound-table cell: holds a texel that passes the hit test
@@ -131,6 +132,7 @@ struct rc2dgi_ctx {
   std::vector<int> rc_tail;      // per level: tail compaction after this many lockstep iterations (tuning rc_tail_L<n>)
   int rc_wgproof = 1;            // tuning "rc_wgproof": workgroup-wide exit proof of the first samples
   std::vector<int> rc_mp;        // per level: directional miss proofs in the one-probe tiles (tuning rc_mp_L<n>)
+  std::vector<int> rc_phase;     // per level: march samples from the phase-plane copy (tuning rc_phase_L<n>: 0, 1, 2)
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   int jfa_coset = 1;             // tuning "jfa_coset": the first four steps in one kernel (k_jfa_coset) where they apply
@@ -226,8 +228,16 @@ void free_level_bufs(rc2dgi_ctx *c) {
   c->level_bufs.clear();
 }
 
+void free_phase_bufs(rc2dgi_ctx *c) {
+  for (unsigned short *&p : c->dist_ph) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+  }
+}
+
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
+  free_phase_bufs(c);
   c->rc_maps.clear();
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
@@ -375,6 +385,8 @@ int allocate(rc2dgi_ctx *c) {
   for (int L = 0; L < c->N; ++L) c->rc_order[L] = default_rc_order(L);
   c->rc_tail.assign(c->N, kDefaultTail);
   c->rc_mp.assign(c->N, 1);  // directional miss proofs wherever they apply (one-probe tiles, 4^L >= kDirBins)
+  c->rc_phase.assign(c->N, 0);
+  c->dist_ph.assign(c->N, nullptr);
   if (int rc = jfa_buffers(c)) return rc;
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
@@ -905,8 +917,12 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   // exit proofs: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
   // staging and barrier cost more than the skipped samples save (RC 0.338 vs 0.376 ms, measured)
   const bool proofs = c->rc_skip > 1 || (c->rc_skip == 1 && std::max(c->W, c->H) >= 2048);
+  // the directional table only where some level reads it: a one-probe tile at a level with 4^L >= kDirBins,
+  // directional proofs on there and the level's direction table binnable (dp_ok)
   bool mps = false;
-  for (int v : c->rc_mp) mps |= v != 0;
+  for (int L = 0; L < c->N; ++L)
+    mps |= c->rc_mp[L] != 0 && (1 << (2 * L)) >= kDirBins && rc_variant_one_probe(c->rc_variant[L]) &&
+           L < (int)c->dp_ok.size() && c->dp_ok[L];
   mps = mps && proofs;
   // surface records and the bound table in one pass over distRT where its cells are >= 64 texels
   if (proofs && c->shade_fused && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch)) {
@@ -946,6 +962,13 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
+    if (c->rc_phase[L] > 0 && dist_phase_ok(c->W, c->H, L) && rc_variant_one_probe(c->rc_variant[L])) {
+      // the level's phase-plane copy, made right before it (timed with the level)
+      if (!c->dist_ph[L]) HIPCHK(c, alloc(&c->dist_ph[L], (size_t)c->sd.pitch * c->H * sizeof(unsigned short)));
+      HIPCHK(c, launch_dist_phase(c->dist, c->sd.pitch, c->dist_ph[L], c->W, c->H, L, st));
+      a.dist_phase = c->dist_ph[L];
+      a.phase_mode = c->rc_phase[L];
+    }
 
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
@@ -1065,8 +1088,8 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   c->timing = 1;
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
   // march rolled / unrolled x linear / 8x8-tiled / packed / nibble-predicted distance field; 32x8 tiles
-  // (x2 probes per lane)
-  const int kVariants[] = {0, 3, 6, 13, 14, 15, 16, 17, 18, 19};
+  // (x2 probes per lane); one probe per lane in 512- and 1024-lane workgroups
+  const int kVariants[] = {0, 3, 6, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
   const int nv = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
   std::vector<float> best(c->N, 1e30f);
   std::vector<int> pick(c->rc_order), pickv(c->rc_variant);
@@ -1469,6 +1492,17 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_tail[L] = value;
     return RC2DGI_OK;
   }
+  if (k == "rc_phase" || k.rfind("rc_phase_L", 0) == 0) {
+    if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "rc_phase is 0 (off), 1 (first sample), 2 (lockstep)");
+    if (k == "rc_phase") {
+      for (int &v : c->rc_phase) v = value;
+      return RC2DGI_OK;
+    }
+    const int L = std::atoi(k.c_str() + 10);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    c->rc_phase[L] = value;
+    return RC2DGI_OK;
+  }
   if (k.rfind("rc_order_L", 0) == 0) {
     const int L = std::atoi(k.c_str() + 10);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
@@ -1530,6 +1564,12 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
     const int L = std::atoi(k.c_str() + 7);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
     *value = c->rc_mp[L];
+    return RC2DGI_OK;
+  }
+  if (k.rfind("rc_phase_L", 0) == 0) {
+    const int L = std::atoi(k.c_str() + 10);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    *value = c->rc_phase[L];
     return RC2DGI_OK;
   }
   if (k.rfind("rc_order_L", 0) == 0) {

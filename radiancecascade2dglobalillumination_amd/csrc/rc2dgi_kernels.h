@@ -82,35 +82,18 @@ struct RcMapCache {
 };
 
 // coarse lower bound of the distance field: kCminDim x kCminDim cells of 2^dist_cmin_shift texels
-// (row-major, kCminDim per row).  Default: 64 x 64 byte entries (4 KB of LDS per workgroup, as the
-// round-2 32 x 32 float table): entry k stands for the lower bound k / 512 = floor(512 d) / 512 <= d
-// of the cell's smallest decode_dist(q), 0 where a texel is a hit.  -DRC2DGI_CMIN_F32 builds the
-// older 32 x 32 float table (A/B: the finer cells cut RC 1.717 -> 1.707 ms on one box).
-#ifndef RC2DGI_CMIN_F32
-#define RC2DGI_CMIN_U8 1
-#endif
-#ifdef RC2DGI_CMIN_U8
+// (row-major, kCminDim per row): 64 x 64 byte entries (4 KB of LDS per workgroup, as the round-2
+// 32 x 32 float table, which the finer cells beat: RC 1.717 -> 1.707 ms on one box, and which the
+// directional proofs' byte tables do not support): entry k stands for the lower bound
+// k / 512 = floor(512 d) / 512 <= d of the cell's smallest decode_dist(q), 0 where a texel is a hit.
 using CminT = unsigned char;
-#ifndef RC2DGI_CMIN_DIM
-#define RC2DGI_CMIN_DIM 64
-#endif
-#else
-using CminT = float;
-#ifndef RC2DGI_CMIN_DIM
-#define RC2DGI_CMIN_DIM 32
-#endif
-#endif
-constexpr int kCminDim = RC2DGI_CMIN_DIM;
+constexpr int kCminDim = 64;
 #ifndef RC2DGI_CMIN_SCALE
 #define RC2DGI_CMIN_SCALE 512.0f  // a power of two (experiment builds may override it)
 #endif
 constexpr float kCminScale = RC2DGI_CMIN_SCALE, kCminStep = 1.0f / RC2DGI_CMIN_SCALE;
 __host__ __device__ __forceinline__ float cmin_value(CminT v) {
-#ifdef RC2DGI_CMIN_U8
   return (float)v * kCminStep;  // exact: k < 2^8, power-of-two step
-#else
-  return v;
-#endif
 }
 
 struct RcLevelArgs {
@@ -130,6 +113,8 @@ struct RcLevelArgs {
   const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
   const uint4 *dist_nib = nullptr;             // nibble-predicted distance field (variants "n", k_dist_nib)
+  const unsigned short *dist_phase = nullptr;  // phase-plane copy of distRT for this level (k_dist_phase), or nullptr
+  int phase_mode = 0;  // 1: the first lockstep sample of every ray reads dist_phase, 2: every lockstep sample
   const CminT *cmin = nullptr;  // coarse lower bound of the field (launch_dist_cmin); nullptr: no exit proofs
   const unsigned char *dclr = nullptr;  // directional clear distances (launch_dir_clear): the one-probe tiles prove
                                        // misses with them instead of cmin (levels with 4^L >= kDirBins)
@@ -156,6 +141,14 @@ constexpr int kDirBins = 64;
 void dir_clear_boxes(int csh, int4 *boxes);
 hipError_t launch_dir_clear(const unsigned char *hitc, const int4 *boxes, unsigned char *dclr, hipStream_t st);
 
+// distRT -> its phase-plane copy for level `lg` (probe spacing s = 2^lg texels, power-of-two screens of up to
+// 16384 columns): texel (x, y) moves to column (x mod s) W/s + x div s of row (y mod s) H/s + y div s, so the
+// probes of a level, s texels apart, sample consecutive texels of one row whenever their rays sit at one t
+// (k_rc_level's first lockstep sample).  Same pitch as distRT.
+bool dist_phase_ok(int W, int H, int lg);
+hipError_t launch_dist_phase(const unsigned short *dist, int pitch, unsigned short *phase, int W, int H, int lg,
+                             hipStream_t st);
+
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,
                             hipStream_t st);
@@ -170,6 +163,7 @@ const char *rc_variant_name(int v);
 bool rc_variant_tiled(int v);  // reads the 8x8-tiled distance field
 bool rc_variant_packed(int v);  // reads the packed distance field
 bool rc_variant_nib(int v);     // reads the nibble-predicted distance field
+bool rc_variant_one_probe(int v);  // one probe and one direction block per lane (directional proofs apply)
 
 // distRT -> packed 14-texel packets (16 B each: the minimum q + one excess byte per texel)
 size_t dist_packed_bytes(int W, int H);

@@ -543,12 +543,8 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
     m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
     const float d = decode_dist(m);
     if (hitc) hitc[blockIdx.y * kCminDim + blockIdx.x] = (in && d < 0.001f) ? 1 : 0;
-#ifdef RC2DGI_CMIN_U8
     // floor(d * scale) / scale <= d (power-of-two scaling and floor are exact); 0 where a texel hits
     cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
-#else
-    cmin[blockIdx.y * kCminDim + blockIdx.x] = (in && d >= 0.001f) ? d : 0.0f;
-#endif
   }
 }
 
@@ -619,11 +615,7 @@ __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__rest
     m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
     const float d = decode_dist(m);
     if (hitc) hitc[blockIdx.y * kCminDim + blockIdx.x] = d < 0.001f ? 1 : 0;
-#ifdef RC2DGI_CMIN_U8
     cmin[blockIdx.y * kCminDim + blockIdx.x] = d >= 0.001f ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
-#else
-    cmin[blockIdx.y * kCminDim + blockIdx.x] = d >= 0.001f ? d : 0.0f;
-#endif
   }
 }
 
@@ -1268,11 +1260,13 @@ const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int
 static const char *kRcVariantNames[] = {"16x16x1", "16x8x2",   "16x16x2",  "32x8x1",   "64x4x1",
                                         "8x8x1",   "32x8x2",   "16x16x1d2", "16x16x1d4", "16x8x1d2",
                                         "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t",
-                                        "16x16x1up", "16x16x1un", "16x16x1p", "16x16x1n"};
+                                        "16x16x1up", "16x16x1un", "16x16x1p", "16x16x1n",
+                                        "32x16x1", "16x32x1", "32x32x1", "32x16x1u", "32x32x1u"};
 int rc_variant_count() { return (int)(sizeof(kRcVariantNames) / sizeof(kRcVariantNames[0])); }
 bool rc_variant_tiled(int v) { return v == 14 || v == 15; }
 bool rc_variant_packed(int v) { return v == 16 || v == 18; }
 bool rc_variant_nib(int v) { return v == 17 || v == 19; }
+bool rc_variant_one_probe(int v) { return v == 0 || (v >= 3 && v <= 5) || (v >= 13 && v < rc_variant_count()); }
 const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ? kRcVariantNames[v] : "?"; }
 
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
@@ -1324,6 +1318,8 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
     e = launch_rc_u8(a, P, st);  // RGBA8 cascades: the 16x16x1 family only
   else if (c.gi_f16)
     e = launch_rc_f16(a, P, st);  // RGBA16F cascades: the 16x16x1 family only
+  else if (a.variant >= 20 && a.variant < rc_variant_count())
+    e = launch_rc_f32_wide(a, P, st);
   else if (a.variant >= 13 && a.variant < rc_variant_count())
     e = launch_rc_f32_unrolled(a, P, st);
   else
@@ -1503,6 +1499,45 @@ int rc_order_plan(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, in
 
 size_t dist_packed_bytes(int W, int H) { return (size_t)pack_per_row(W) * H * sizeof(uint4); }
 
+
+// Phase-plane copy (launch_dist_phase): one workgroup per input row, read whole into LDS, written permuted as
+// output row (y mod s) H/s + y div s, column X' <- input column (X' mod W/s) s + X' div (W/s).  Both passes
+// are whole coalesced rows; the LDS reads stride by s texels.
+__global__ __launch_bounds__(256) void k_dist_phase(const unsigned short *__restrict__ dist, int pitch,
+                                                    unsigned short *__restrict__ out, int W, int H, int lg, int lgw,
+                                                    int lgh) {
+  __shared__ unsigned short row[16384];
+  const int y = blockIdx.x;
+  const unsigned short *src = dist + (size_t)y * pitch;
+  for (int x = (int)threadIdx.x * 8; x < W; x += 256 * 8)  // 16-byte pieces (W is a multiple of 8 here)
+    *reinterpret_cast<uint4 *>(row + x) = *reinterpret_cast<const uint4 *>(src + x);
+  __syncthreads();
+  const int s = 1 << lg, yo = ((y & (s - 1)) << (lgh - lg)) | (y >> lg);
+  unsigned short *dst = out + (size_t)yo * pitch;
+  const int cw = lgw - lg;  // log2 of the columns per plane
+  for (int xo = (int)threadIdx.x * 2; xo < W; xo += 256 * 2) {
+    const int x0 = ((xo & ((1 << cw) - 1)) << lg) | (xo >> cw), x1 = (((xo + 1) & ((1 << cw) - 1)) << lg) | ((xo + 1) >> cw);
+    *reinterpret_cast<unsigned *>(dst + xo) = (unsigned)row[x0] | ((unsigned)row[x1] << 16);
+  }
+}
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+bool dist_phase_ok(int W, int H, int lg) {
+  return W >= 16 && W <= 16384 && H >= 1 && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && lg >= 1 && (1 << lg) <= W &&
+         (1 << lg) <= H;
+}
+
+hipError_t launch_dist_phase(const unsigned short *dist, int pitch, unsigned short *phase, int W, int H, int lg,
+                             hipStream_t st) {
+  if (!dist_phase_ok(W, H, lg) || pitch % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dist_phase, dim3(H), dim3(256), 0, st, dist, pitch, phase, W, H, lg, ilog2(W), ilog2(H));
+  return hipGetLastError();
+}
 
 hipError_t launch_dist_pack(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st) {
   const int ppr = pack_per_row(W);

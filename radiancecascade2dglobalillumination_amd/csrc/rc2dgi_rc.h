@@ -33,6 +33,9 @@ struct RcParams {
   int cscr;             // the exit proof tests the screen edge too
   int tailk;            // tail compaction after this many lockstep iterations (0: off)
   int wgp;              // workgroup-wide exit proof of the first samples
+  const unsigned short *dph;  // phase-plane copy of distRT for this level (k_dist_phase), nullptr: off
+  int phm;                    // 1: the first lockstep sample reads dph, 2: every lockstep sample
+  int phcw, phch;             // log2 of the columns / rows per phase plane (log2(W) - level, log2(H) - level)
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   unsigned long long *stats;  // diagnostic builds: [16 levels][16] counters (rc2dgi_diag_stats)
 #endif
@@ -322,9 +325,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr int RW = TX / 2 + 2, RH = THY / 2 + 2;
   constexpr int NSTAGE = ND * RH * RW;
   // staging assignment: wave w stages directions w, w + NW, ...; a lane the texels lane + 64 q of
-  // each, so the direction (and its footprint origin) is wave-uniform scalar arithmetic
-  constexpr int NW = NT / 64, DPW = ND / NW, FP = RH * RW, QPD = (FP + 63) / 64;
-  static_assert(NT % 64 == 0 && ND % NW == 0, "whole waves, whole directions per wave");
+  // each, so the direction (and its footprint origin) is wave-uniform scalar arithmetic.  Workgroups
+  // of more waves than directions (the 512- and 1024-lane one-probe tiles) give each direction WPD
+  // waves: wave w stages direction w % ND, the 64-texel chunks w / ND, w / ND + WPD, ... of it.
+  constexpr int NW = NT / 64, FP = RH * RW;
+  static_assert(NT % 64 == 0 && (ND % NW == 0 || NW % ND == 0), "whole waves, whole directions per wave");
+  constexpr int DPW = NW <= ND ? ND / NW : 1, WPD = NW <= ND ? 1 : NW / ND;
+  constexpr int QPD = (FP + 64 * WPD - 1) / (64 * WPD);  // chunks per wave and direction
   constexpr int PT = DPW * QPD;
 #ifdef RC2DGI_DIAG_NOMERGE
   constexpr bool STG = false;  // timing-only ablation build: no upper staging, no merge (WRONG results)
@@ -383,8 +390,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // the per-sample test, scripts/dirproof_model.py).
   const bool dp = TLC && P.dclr != nullptr;
   const bool cm = CMS && P.cmin != nullptr && !dp;
-  // (one bin per workgroup: bi0 * kDirBins / 4^L, exact for 4^L >= kDirBins)
-  const float4 *ctab = dp ? P.dclr + (size_t)((bi0 * kDirBins) >> (2 * P.level)) * (CMN / 16) : P.cmin;
+  // (one bin per workgroup: bi0 * kDirBins / 4^L, exact for 4^L >= kDirBins; as a shift, since the product
+  // overflows 32 bits from level 13 on)
+  static_assert(kDirBins == 64, "the bin shift below assumes 64 = 4^3 bins");
+  const float4 *ctab = dp ? P.dclr + (size_t)(bi0 >> max(0, 2 * P.level - 6)) * (CMN / 16) : P.cmin;
   constexpr int CM4 = CMN * (int)sizeof(CminT) / 16;  // 16-byte pieces of the table
   constexpr int CPT = CMS ? (CM4 + NT - 1) / NT : 1;  // per thread
   float4 cmv[CPT];
@@ -410,6 +419,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   const int lane = (int)threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int yy0 = lane / RW, xx0 = lane - (lane / RW) * RW;
+  // (WPD > 1) the direction and first chunk this wave stages
+  const int wdir = WPD > 1 ? wv % ND : wv, wch = WPD > 1 ? wv / ND : 0;
   // staging loads of the level-(L+1) footprint, issued now and written to LDS after the march.
   // Level 0 issues its shared first distance sample before them (vmcnt retires in order, so
   // the march then waits for that sample only).
@@ -417,16 +428,18 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     if (STG) {
   #pragma unroll
       for (int j = 0; j < DPW; ++j) {
-        const int r = wv + j * NW;  // direction (of the 4*PD) this wave stages
+        const int r = wdir + j * NW;  // direction (of the 4*PD) this wave stages
         const int a = bi0 * 4 + r;
         const int bx = (a & umask) * ubx + (cx0 >> 1) - 1, by = (a >> ushift) * uby + (cy0 >> 1) - 1;
         // REPEAT wrap only where the footprint crosses a texture edge (a wave-uniform branch)
         const bool wrap = bx < 0 || bx + RW > P.c.CW || by < 0 || by + RH > P.c.CH;
   #pragma unroll
         for (int q = 0; q < QPD; ++q) {
-          // texel e = lane + 64 q of the footprint: (yy, xx) from the lane's (yy0, xx0), clamped to
-          // the footprint (unconditional loads keep the staging arrays in registers)
-          int xx = xx0 + (64 * q) % RW, yy = yy0 + (64 * q) / RW;
+          // texel e = lane + 64 ch of the footprint (chunk ch = wch + WPD q): (yy, xx) from the lane's
+          // (yy0, xx0) and the chunk's wave-uniform offset, clamped to the footprint (unconditional loads
+          // keep the staging arrays in registers)
+          const int ce = 64 * (wch + WPD * q);
+          int xx = xx0 + ce % RW, yy = yy0 + ce / RW;
           if (xx >= RW) {
             xx -= RW;
             ++yy;
@@ -634,6 +647,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   const int itend = tl ? max(0, min(P.tailk, RC2DGI_DIAG_MAX_ITERS)) : RC2DGI_DIAG_MAX_ITERS;
   RC_SECTION("march");
   RC_TSTAMP(4);
+  // Phase-plane samples (P.dph, k_dist_phase): the probes of a level are 2^L texels apart, so at one t the
+  // lanes of a wave sample texels 2^L apart -- each its own 128-byte line in distRT, consecutive texels of one
+  // row of the copy, where texel (x, y) sits at column (x mod 2^L) W/2^L + x div 2^L of row
+  // (y mod 2^L) H/2^L + y div 2^L.  The lockstep march's first sample (every ray at its t0) reads the copy
+  // (phm 1), or every lockstep sample does (phm 2); the same q either way.
+  constexpr bool PHC = BOFF && P2S && TLC;
+  const bool phon = PHC && P.dph != nullptr;
   // BOFF with P2S: floor(p * 2W) & (2W - 2) = 2 (floor(p W) & (W - 1)) (p W and p 2W are exact)
   const float sWx = (BOFF && P2S) ? 2.0f * P.sWf : P.sWf;
   const int wmask = (BOFF && P2S) ? 2 * P.s.W - 2 : P.s.W - 1;
@@ -738,6 +758,16 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         for (int k = 0; k < NR; ++k)
           if (ek[k]) q[k] = ld_dist_esc(dist, (unsigned)idx[k] << 1);
       }
+    } else if (PHC && phon && (P.phm == 2 || it == it0)) {
+      const unsigned pm = (1u << P.level) - 1u;
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {  // the same texels in the phase-plane copy (dead rays: texel 0)
+        const unsigned col = (unsigned)cix[k] >> 1, row = (unsigned)ciy[k];
+        const unsigned xo = ((col & pm) << P.phcw) | (col >> P.level), yo = ((row & pm) << P.phch) | (row >> P.level);
+        const unsigned off = __umul24(yo, (unsigned)(2 * P.s.pitch)) + 2u * xo;
+        q[k] = ld_dist(P.dph, live[k] ? off : 0u);
+      }
+      if constexpr (NR == 4) asm volatile("" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]));
     } else {
 #pragma unroll
       for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
@@ -867,9 +897,9 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     for (int j = 0; j < DPW; ++j) {
 #pragma unroll
       for (int q = 0; q < QPD; ++q) {
-        const int e = lane + 64 * q, t = j * QPD + q;
-        const int k = (wv + j * NW) * FP + e;
-        if (64 * (q + 1) <= FP || e < FP) {
+        const int e = lane + 64 * (wch + WPD * q), t = j * QPD + q;
+        const int k = (wdir + j * NW) * FP + e;
+        if ((WPD == 1 && 64 * (q + 1) <= FP) || e < FP) {
           if constexpr (NWD == 1)
             s_up[k] = GI::stage(stx[t], 0u, 0u, 0u);
           else if constexpr (NWD == 2)
@@ -889,7 +919,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   if constexpr (TLC) {  // (see hr above)
 #pragma unroll
     for (int k = 0; k < NR; ++k)
+#ifdef RC2DGI_DIAG_NOHIT  // timing-only ablation build: no hit-record loads (WRONG results)
+      if (hit_idx[k] >= 0) hr[k] = make_float4(0.5f, 0.5f, 0.5f, 1.0f);
+#else
       if (hit_idx[k] >= 0) hr[k] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
+#endif
   }
 
   RC_TSTAMP(7);
@@ -1033,6 +1067,11 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   if (P.cmin && P.cscr && !P.dexit) return hipErrorInvalidValue;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
+  P.dph = (a.dist_phase && a.phase_mode > 0 && p2s && dist_phase_ok(P.s.W, P.s.H, a.level)) ? a.dist_phase : nullptr;
+  P.phm = a.phase_mode;
+  P.phcw = P.phch = 0;
+  while ((1 << (P.phcw + a.level)) < P.s.W) ++P.phcw;
+  while ((1 << (P.phch + a.level)) < P.s.H) ++P.phch;
 #define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \
   hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL >= 2 ? 0 : DL)), GI, Z0V>), \
                      dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),   \
@@ -1054,6 +1093,7 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
 // per translation unit dispatchers of the tile variants (rc2dgi_rc_*.hip)
 hipError_t launch_rc_f32_rolled(const RcLevelArgs &a, RcParams P, hipStream_t st);
 hipError_t launch_rc_f32_unrolled(const RcLevelArgs &a, RcParams P, hipStream_t st);
+hipError_t launch_rc_f32_wide(const RcLevelArgs &a, RcParams P, hipStream_t st);
 hipError_t launch_rc_f16(const RcLevelArgs &a, RcParams P, hipStream_t st);
 hipError_t launch_rc_u8(const RcLevelArgs &a, RcParams P, hipStream_t st);
 

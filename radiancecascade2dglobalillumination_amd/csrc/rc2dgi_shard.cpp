@@ -151,7 +151,8 @@ FramePlan plan_frame(const PlanInputs &in) {
       up = RowSet::full(nb);
     } else {
       for (auto &r : p.level[L].iv) {
-        if (exact)
+        if (exact)  // (r.second = 2 nb, the block's top row: the end nb + 1 wraps to include row 0, whose
+                    // weight-0 tap GL's lerp fma(w, b - a, a) still reads -- a NaN there is a NaN result)
           up.add(std::max(0, (r.first - 1) >> 1), std::max(0, (r.second - 2) >> 1) + 2);
         else
           up.add(r.first / 2 - 2, (r.second - 1) / 2 + 3);

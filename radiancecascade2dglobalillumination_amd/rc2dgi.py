@@ -62,7 +62,7 @@ def load_library(path: Optional[str] = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or os.environ.get("RC2DGI_LIB", LIB_PATH)
+    path = path or os.environ.get("RC2DGI_LIB") or LIB_PATH  # (an empty RC2DGI_LIB: the in-tree build)
     if not os.path.exists(path):
         raise RuntimeError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                            "(there is no CPU fallback)")
@@ -340,7 +340,12 @@ class RC2DGI:
     def set_timing(self, enable=True) -> None:
         """True / 1: events around every pass and RC level; 2: around every pass only (no idle gaps
         between the levels); False / 0: off."""
-        mode = 2 if enable == 2 and not isinstance(enable, bool) else int(bool(enable))
+        if isinstance(enable, bool):
+            mode = int(enable)
+        elif isinstance(enable, (int, np.integer)) and int(enable) in (0, 1, 2):
+            mode = int(enable)
+        else:
+            raise ValueError(f"set_timing: expected a bool or 0, 1, 2, got {enable!r}")
         self._check(self._L.rc2dgi_set_timing(self._h, mode), "set_timing")
 
     def pass_times(self, levels: int = 0):

@@ -6,13 +6,15 @@ the CPU oracle (oracle/, pinned to the reference shaders by tests/test_oracle_go
 * H   4096^2, N=6, rayRange 2   -- the metric's configuration, committed bench schedule
 * C1  1200x900, N=6             -- the reference app's own size, f32, every texel of every texture
 * C2  4096^2, N=8, rayRange 64  -- committed bench schedule
-* C3  8192^2, N=8, rayRange 64  -- 8 row-strip shards (rc2dgi_do_group) vs the unsharded frame
-* C4  batch of 4096^2 N=8 scenes on one shared stream (the bench's batch mode)
+* C3  8192^2, N=8, rayRange 64  -- unsharded frame vs the oracle, then 8 row-strip shards
+                                  (rc2dgi_do_group) vs the unsharded frame
+* C4  batch of 4096^2 N=8 scenes, on one shared stream and on one stream per scene
+* f16 / rgba8 storage at 4096^2 N=6 on the schedules bench.py --storage times
 
 At the 4096^2 / 8192^2 sizes the oracle checks the JFA state and distRT over the whole frame,
 every cascade level (the oracle level pass fed the HIP pipeline's own G_{L+1} and distRT) on
-every row at H and C2 and on 1/4 of the rows at C3, and blur / copy-back / merge over the whole
-frame (every 8th row at 8192^2).  The
+every row at H, C2 and C3 (half of the rows per C4 scene), and blur / copy-back / merge over the
+whole frame.  The
 bar is bit-exact equality (the written tolerance, max rel err <= 1e-4, is implied).
 Reference: RC2DGI.cs:66-77 (knobs), RC2DGI.cs:267-406 (the pass chain).
 """
@@ -53,6 +55,9 @@ def apply_schedule(ctx, sched, N, shards=1):
     for L in range(N):
         ctx.set_tuning(f"rc_order_L{L}", (sub.get("rc_order") or sched["rc_order"])[L])
         ctx.set_tuning(f"rc_variant_L{L}", (sub.get("rc_variant") or sched["rc_variant"])[L])
+        ph = sub.get("rc_phase") or sched.get("rc_phase")
+        if ph:
+            ctx.set_tuning(f"rc_phase_L{L}", ph[L])
 
 
 def level_offsets(N):
@@ -207,18 +212,16 @@ def test_c1_vs_llvmpipe_fixture(R):
 
 
 # ---------------------------------------------------------------- C3: 8192^2 row strips
-def test_c3_8192_eight_row_strips(R):
-    """8192^2, N=8, rayRange 64 split into 8 row strips (SURVEY §8e), run as 8 in-process shard
-    contexts with the distRT exchange (rc2dgi_do_group), intermediates poisoned, all with the
-    committed schedules bench.py times (tuning/8192x8192_N8_rr64_f32.json: the packed-field march at L4 for
-    the whole frame, its "strips" entry for the shards; the shards make their surface records at the hit):
-    every shard's colorRT / tempRT strip equals the unsharded frame bit for bit, and
-    the unsharded frame is checked against the oracle (JFA + DF whole frame, 1/4 of the rows of
-    every level, blur / merge on every 8th row)."""
+C3 = dict(W=8192, H=8192, N=8, rr=64.0, P=8)
+
+
+@pytest.fixture(scope="module")
+def c3_whole(R):
+    """The unsharded C3 frame on the committed schedule, every level kept (8 x 1 GB on the device),
+    and its distRT / colorRT / tempRT downloaded once for the tests below."""
     from radiancecascade2dglobalillumination_amd import scenes
 
-    W = H = 8192
-    N, rr, P = 8, 64.0, 8
+    W, H, N, rr = C3["W"], C3["H"], C3["N"], C3["rr"]
     sched = committed_schedule(W, H, N, rr)
     color, emis = scenes.demo(W, H)
     p = oracle.Params(W=W, H=H, N=N, ray_range=rr)
@@ -229,30 +232,68 @@ def test_c3_8192_eight_row_strips(R):
     whole.sync()
     for L in range(N):
         assert whole.get_tuning(f"rc_variant_L{L}") == sched["rc_variant"][L]
-    # the unsharded frame vs the oracle
-    jfin, dist = oracle_jfa(color, W, H)
-    final_rt = "jump1" if (whole.jfa_steps % 2 == 0) else "jump2"
-    assert np.array_equal(whole.download(final_rt), jfin), "C3 final JFA state"
-    del jfin
-    got_dist = whole.download("dist")
-    assert np.array_equal(got_dist, dist), "C3 distRT"
-    del dist
-    check_levels(p, whole.download_level, color, emis, got_dist, 4, "C3")
-    want_color, want_temp = whole.download("color"), whole.download("temp")
-    g0 = whole.download_level(0)
-    bl = oracle.blur(g0, p.blur_radius)
-    fin = oracle.blur_copyback(bl, g0)
-    temp, col = oracle.merge(color, fin)
-    assert np.array_equal(want_color[::8], col[::8]) and np.array_equal(want_temp[::8], temp[::8]), "C3 merge"
-    del bl, fin, temp, col, g0, got_dist
+    d = dict(ctx=whole, p=p, color=color, emis=emis, sched=sched, dist=whole.download("dist"),
+             color_out=whole.download("color"), temp=whole.download("temp"))
+    yield d
     whole.close()
-    # 8 shards on the same schedule, two frames (the second reuses the exchange buffers)
+
+
+def test_c3_8192_jfa_and_distance_field(c3_whole):
+    """8192^2 N=8 rayRange 64 (BASELINE configs[3]), unsharded: the final JumpFlood state and distRT over
+    the whole frame vs the oracle's ScreenUV + 13 steps + DistanceField."""
+    w = c3_whole
+    jfin, dist = oracle_jfa(w["color"], w["p"].W, w["p"].H)
+    final_rt = "jump1" if (w["ctx"].jfa_steps % 2 == 0) else "jump2"
+    assert np.array_equal(w["ctx"].download(final_rt), jfin), "C3 final JFA state"
+    assert np.array_equal(w["dist"], dist), "C3 distRT"
+
+
+@pytest.mark.parametrize("L", range(C3["N"]))
+def test_c3_8192_level_every_row(c3_whole, L):
+    """C3, unsharded, committed schedule: cascade level L on EVERY probe row of every direction block vs
+    the oracle level pass (RadianceCascades.fs) fed the HIP frame's own G_{L+1} and distRT."""
+    w = c3_whole
+    p, N = w["p"], w["p"].N
+    got = w["ctx"].download_level(L)
+    upper = w["ctx"].download_level(L + 1) if L + 1 < N else None
+    out = np.zeros_like(got)
+    oracle.rc_level_rows(p, L, upper, w["color"], w["emis"], w["dist"], out,
+                         np.ascontiguousarray(oracle.dir_tables(p)[level_offsets(N)[L]:]), oracle.sky_table(p), 0,
+                         None, 1)
+    assert rel_err(got, out).max() <= TOL, f"C3 level {L}: max rel err {rel_err(got, out).max():.3e}"
+    assert np.array_equal(got, out), f"C3 level {L}: {np.count_nonzero(np.any(got != out, -1))} texels"
+
+
+def test_c3_8192_blur_and_merge_every_row(c3_whole):
+    """C3, unsharded: cascadeBlurRT + blended copy-back + merge + copy-back on every row vs the oracle,
+    fed the HIP frame's own level 0."""
+    w = c3_whole
+    p = w["p"]
+    g0 = w["ctx"].download_level(0)
+    bl = oracle.blur(g0, p.blur_radius)
+    assert np.array_equal(w["ctx"].download("blur"), bl), "C3 cascadeBlurRT"
+    fin = oracle.blur_copyback(bl, g0)
+    del bl, g0
+    assert np.array_equal(w["ctx"].download("final_gi"), fin), "C3 final GI"
+    temp, col = oracle.merge(w["color"], fin)
+    assert np.array_equal(w["temp"], temp), "C3 tempRT"
+    assert np.array_equal(w["color_out"], col), "C3 colorRT"
+
+
+def test_c3_8192_eight_row_strips(R, c3_whole):
+    """8192^2, N=8, rayRange 64 split into 8 row strips (SURVEY §8e), run as 8 in-process shard
+    contexts with the JumpFlood row exchange and the distRT exchange (rc2dgi_do_group), intermediates
+    poisoned, on the committed schedule's strips entry (bench.py --mode strips --shards 8 times it):
+    every shard's colorRT / tempRT strip equals the unsharded frame bit for bit (which the tests above
+    check against the oracle on every row), over two frames (the second reuses the exchange buffers)."""
+    w = c3_whole
+    W, H, N, rr, P = C3["W"], C3["H"], C3["N"], C3["rr"], C3["P"]
     shards = []
     for k in range(P):
         g = R.RC2DGI(W, H, cascade_count=N, ray_range=rr)
-        g.upload("color", color)
-        g.upload("emissive", emis)
-        apply_schedule(g, sched, N, P)  # the strips' own entry (bench.py --mode strips --shards 8 times it)
+        g.upload("color", w["color"])
+        g.upload("emissive", w["emis"])
+        apply_schedule(g, w["sched"], N, P)
         g.set_tuning("poison", 1)
         g.set_shard(k, P)
         shards.append(g)
@@ -262,17 +303,19 @@ def test_c3_8192_eight_row_strips(R):
         g.sync()
         y0, y1 = g.shard_rows()
         c, t = g.download("color"), g.download("temp")
-        assert np.array_equal(c[y0:y1], want_color[y0:y1]), f"C3 shard rows {y0}:{y1} colorRT"
-        assert np.array_equal(t[y0:y1], want_temp[y0:y1]), f"C3 shard rows {y0}:{y1} tempRT"
+        assert np.array_equal(c[y0:y1], w["color_out"][y0:y1]), f"C3 shard rows {y0}:{y1} colorRT"
+        assert np.array_equal(t[y0:y1], w["temp"][y0:y1]), f"C3 shard rows {y0}:{y1} tempRT"
         g.close()
 
 
 # ---------------------------------------------------------------- C4: batch of independent scenes
-def test_c4_batch_of_4096_scenes_one_stream(R):
-    """BASELINE configs[4] on one GPU: 8 independent 4096^2 N=8 scenes, one context each, all on
-    one shared stream with the frames back to back (bench.py --batch), two frames in flight per
-    context; each context's frame vs the oracle (JFA + DF whole frame, levels on sampled rows,
-    merge whole frame)."""
+@pytest.mark.parametrize("streams", ["shared", "own"])
+def test_c4_batch_of_4096_scenes(R, streams):
+    """BASELINE configs[4] on one GPU: 8 independent 4096^2 N=8 scenes, one context each, two frames in
+    flight per context; "shared": all on one stream, frames back to back (bench.py --batch 8);
+    "own": one stream per scene (the contexts' own streams, bench.py --batch 8 --batch-streams 0), all
+    frames in flight together.  Each context's frame vs the oracle: JFA + DF whole frame, every level on
+    half of its rows (a different half per level), blur / merge whole frame."""
     import torch
 
     from radiancecascade2dglobalillumination_amd import dist as rdist
@@ -280,12 +323,13 @@ def test_c4_batch_of_4096_scenes_one_stream(R):
 
     W = H = 4096
     N, rr, B = 8, 2.0, 8
-    stream = torch.cuda.Stream(device=0)
+    stream = torch.cuda.Stream(device=0) if streams == "shared" else None
     ctxs, inputs = [], []
     for i in range(B):
         color, emis = scenes.random_scene(W, H, seed=rdist.scene_seed(i))
         g = R.RC2DGI(W, H, cascade_count=N, ray_range=rr)
-        g.set_stream(stream.cuda_stream)
+        if stream is not None:
+            g.set_stream(stream.cuda_stream)
         g.set_keep_levels(True)
         g.upload("color", color)
         g.upload("emissive", emis)
@@ -298,5 +342,36 @@ def test_c4_batch_of_4096_scenes_one_stream(R):
         g.sync()
     p = oracle.Params(W=W, H=H, N=N, ray_range=rr)
     for i, (g, (color, emis)) in enumerate(zip(ctxs, inputs)):
-        check_frame(g, p, color, emis, stride=64, what=f"C4 scene {i}")
+        check_frame(g, p, color, emis, stride=2, what=f"C4 {streams} scene {i}")
         g.close()
+
+
+# ---------------------------------------------------------------- f16 / rgba8 storage at the timed size
+@pytest.mark.parametrize("storage", ["f16", "rgba8"])
+def test_storage_schedule_full_size(R, storage):
+    """The RGBA16F and RGBA8 storage modes at 4096^2 N=6 on the schedule bench.py
+    --storage times (tuning/4096x4096_N6_rr2_<storage>.json), every texel of every render texture and
+    of every level vs the oracle frame in the same storage mode."""
+    from radiancecascade2dglobalillumination_amd import scenes
+
+    W = H = 4096
+    N, rr = 6, 2.0
+    sched = committed_schedule(W, H, N, rr, storage)
+    color, emis = scenes.demo(W, H)
+    p = oracle.Params(W=W, H=H, N=N, ray_range=rr, gi_f16=storage == "f16", rgba8=storage == "rgba8")
+    ctx = R.RC2DGI(W, H, cascade_count=N, ray_range=rr, storage=storage)
+    apply_schedule(ctx, sched, N)
+    for L in range(N):
+        assert ctx.get_tuning(f"rc_variant_L{L}") == sched["rc_variant"][L]
+    ctx.set_keep_levels(True)
+    ctx.frame(color, emis)
+    ctx.sync()
+    fr = oracle.frame(p, color, emis, keep_levels=True)
+    want = dict(color=fr.color_out, jump1=fr.jump1, jump2=fr.jump2, dist=fr.dist, temp=fr.temp, gi1=fr.gi1,
+                gi2=fr.gi2, blur=fr.blur, final_gi=fr.gi_final)
+    for k, w in want.items():
+        g = ctx.download(k)
+        assert np.array_equal(g, w), f"{storage} 4096^2 {k}: {np.count_nonzero(g != w)}"
+    for L in range(N):
+        assert np.array_equal(ctx.download_level(L), fr.gi_levels[L]), f"{storage} 4096^2 level {L}"
+    ctx.close()
