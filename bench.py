@@ -282,6 +282,8 @@ def apply_schedule(g, tun, N, shards=1):
         ph = sub.get("rc_phase") or tun.get("rc_phase")
         if ph:  # optional: phase-plane march samples per level (rc_phase_L<n>)
             g.set_tuning(f"rc_phase_L{L}", ph[L])
+    for k, v in {**tun.get("knobs", {}), **sub.get("knobs", {})}.items():  # optional tuning knobs (rc_skip, ...)
+        g.set_tuning(k, int(v))
 
 
 def bench_strips(a, rank, local, world):

@@ -251,6 +251,11 @@ int rc2dgi_plan_rows(const rc2dgi_config *cfg, float blur_radius, int rank, int 
  * row, rows, dst shard, dst buffer (0 window, 1 block A, 2 block B), dst row}; returns the
  * number of transfers.  A shard's window holds global rows [y0 - m, y1 + m) modulo H. */
 int rc2dgi_plan_jfa_exchange(const rc2dgi_config *cfg, int world, int step, int *info, int *xfers, int max_xfers);
+/* host-only: the peers shard `rank` awaits (their step step-1 done) before JFA step `step` of a group frame
+ * (rc2dgi_do_group): the readers of its J_{step-2} (the ping-pong buffer step `step` overwrites) as their
+ * shard index, then the senders of the rows of J_{step-1} it copies as -1 - shard; up to max_peers written,
+ * returns the count. */
+int rc2dgi_plan_group_waits(const rc2dgi_config *cfg, int world, int rank, int step, int *peers, int max_peers);
 /* where shard `rank` reads tap y (dy = -1, 0, +1) of step `step`: buffer buf[y] (0 window, 1 A,
  * 2 B) whose local row 0 is global row row0[y] (modulo H) */
 int rc2dgi_plan_jfa_window(const rc2dgi_config *cfg, int rank, int world, int step, int *buf, int *row0);

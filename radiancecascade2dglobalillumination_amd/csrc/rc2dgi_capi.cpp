@@ -103,6 +103,9 @@ struct rc2dgi_ctx {
   uint4 *dist_p = nullptr;           // packed copy for the "p" RC variants (k_dist_pack)
   uint4 *dist_n = nullptr;           // nibble-predicted copy for the "n" RC variants (k_dist_nib)
   std::vector<unsigned short *> dist_ph;  // per level: phase-plane copy of distRT (tuning rc_phase_L<n>, k_dist_phase)
+  unsigned short *mfield = nullptr;  // march field of the surface palettes (tuning rc_pal, launch_shade_cmin)
+  float4 *cell_pal = nullptr;        // kCminDim^2 cells x kCellPalStride palette entries
+  int rc_pal = 1;                    // surface palettes on (where they apply: 4096^2 .. 8192^2 square screens)
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
   unsigned char *hitc = nullptr;     // per bound-table cell: holds a texel that passes the hit test
@@ -242,7 +245,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
-                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes};
+                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes, c->mfield, c->cell_pal};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -258,6 +261,8 @@ void free_buffers(rc2dgi_ctx *c) {
   c->shade = nullptr;
   c->cmin = nullptr;
   c->hitc = c->dclr = nullptr;
+  c->mfield = nullptr;
+  c->cell_pal = nullptr;
   c->dboxes = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
@@ -924,10 +929,17 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     mps |= c->rc_mp[L] != 0 && (1 << (2 * L)) >= kDirBins && rc_variant_one_probe(c->rc_variant[L]) &&
            L < (int)c->dp_ok.size() && c->dp_ok[L];
   mps = mps && proofs;
-  // surface records and the bound table in one pass over distRT where its cells are >= 64 texels
-  if (proofs && c->shade_fused && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch)) {
+  // surface records and the bound table in one pass over distRT where its cells are >= 64 texels; with the
+  // surface palettes also the march field the plain-field levels read (launch_shade_cmin)
+  const bool fused = proofs && c->shade_fused && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch);
+  const bool pal = fused && c->rc_pal && (size_t)c->sd.pitch * c->H <= ((size_t)1 << 26);
+  if (pal && !c->mfield) {
+    HIPCHK(c, alloc(&c->mfield, (size_t)c->sd.pitch * c->H * sizeof(unsigned short)));
+    HIPCHK(c, alloc(&c->cell_pal, (size_t)kCminDim * kCminDim * kCellPalStride * sizeof(float4)));
+  }
+  if (fused) {
     HIPCHK(c, launch_shade_cmin(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, c->cmin,
-                                mps ? c->hitc : nullptr, st));
+                                mps ? c->hitc : nullptr, st, pal ? c->mfield : nullptr, pal ? c->cell_pal : nullptr));
   } else {
     HIPCHK(c, launch_shade(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, st));
     if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
@@ -941,7 +953,11 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     RcLevelArgs a;
     a.upper = (L == c->N - 1) ? nullptr : srcGI;
     a.out = dstGI;
-    a.dist = c->dist;
+    // (palettes: the one-probe tiles of the plain field, rc2dgi_rc.h PALC; level 0 shares its first sample)
+    const bool plain = !rc_variant_tiled(c->rc_variant[L]) && !rc_variant_packed(c->rc_variant[L]) &&
+                       !rc_variant_nib(c->rc_variant[L]) && rc_variant_one_probe(c->rc_variant[L]) && L > 0;
+    a.dist = (pal && plain) ? c->mfield : c->dist;  // the march field: same samples, hits carry a palette entry
+    a.cell_pal = (pal && plain) ? c->cell_pal : nullptr;
     a.shade = c->shade;
     a.dirs = c->dirs + dir_table_offset(L);
     a.dexit = c->dexit + dir_table_offset(L);
@@ -965,7 +981,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     if (c->rc_phase[L] > 0 && dist_phase_ok(c->W, c->H, L) && rc_variant_one_probe(c->rc_variant[L])) {
       // the level's phase-plane copy, made right before it (timed with the level)
       if (!c->dist_ph[L]) HIPCHK(c, alloc(&c->dist_ph[L], (size_t)c->sd.pitch * c->H * sizeof(unsigned short)));
-      HIPCHK(c, launch_dist_phase(c->dist, c->sd.pitch, c->dist_ph[L], c->W, c->H, L, st));
+      HIPCHK(c, launch_dist_phase(a.dist, c->sd.pitch, c->dist_ph[L], c->W, c->H, L, st));
       a.dist_phase = c->dist_ph[L];
       a.phase_mode = c->rc_phase[L];
     }
@@ -1089,8 +1105,12 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
   // march rolled / unrolled x linear / 8x8-tiled / packed / nibble-predicted distance field; 32x8 tiles
   // (x2 probes per lane); one probe per lane in 512- and 1024-lane workgroups
-  const int kVariants[] = {0, 3, 6, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
-  const int nv = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+  // (RGBA16F / RGBA8 cascades build the 16x16x1 family only: the other ids would time that kernel again)
+  const int kVariantsF32[] = {0, 3, 6, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
+  const int kVariantsOther[] = {0, 13, 14, 15, 16, 17, 18, 19};
+  const bool f32 = c->storage == RC2DGI_STORAGE_F32;
+  const int *kVariants = f32 ? kVariantsF32 : kVariantsOther;
+  const int nv = f32 ? (int)(sizeof(kVariantsF32) / sizeof(int)) : (int)(sizeof(kVariantsOther) / sizeof(int));
   std::vector<float> best(c->N, 1e30f);
   std::vector<int> pick(c->rc_order), pickv(c->rc_variant);
   std::vector<float> lv(c->N);
@@ -1157,24 +1177,18 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
       HIPCHK(c, hipSetDevice(c->device));
       if (c->strip) {
         const size_t rowb = (size_t)c->sd.pitch * sizeof(unsigned);
-        std::vector<int> waited(n, 0);
-        // step t overwrites J_{t-2} (ping-pong); the peers that copied rows of J_{t-2} from us
-        // before their step t-1 did so on their own streams, so wait for those steps (the block
-        // partners change from step to step, so they need not be the peers we receive from now)
-        if (t >= 2) {
-          std::vector<int> rd(n, 0);
-          for (const JfaXfer &x : c->jx.steps[t - 1].xfers)
-            if (x.src == k && x.dst != k && !rd[x.dst]) {
-              HIPCHK(c, hipStreamWaitEvent(c->stream, cs[x.dst]->ev_jfa[(t - 1) & 1], 0));
-              rd[x.dst] = 1;
-            }
-        }
+        // step t overwrites J_{t-2} (ping-pong); the peers that copied rows of J_{t-2} from us before their
+        // step t-1 did so on their own streams, so wait for those steps (the block partners change from step
+        // to step, so they need not be the peers we receive from now); and the owners of the rows of J_{t-1}
+        // we copy now must have finished their step t-1 (group_step_waits; tests/test_shard_plan.py)
+        std::vector<int> readers, senders;
+        group_step_waits(c->jx, k, t, readers, senders);
+        for (int q : readers) HIPCHK(c, hipStreamWaitEvent(c->stream, cs[q]->ev_jfa[(t - 1) & 1], 0));
+        for (int q : senders)
+          if (std::find(readers.begin(), readers.end(), q) == readers.end())
+            HIPCHK(c, hipStreamWaitEvent(c->stream, cs[q]->ev_jfa[(t - 1) & 1], 0));
         for (const JfaXfer &x : c->jx.steps[t].xfers) {
           if (x.dst != k) continue;
-          if (x.src != k && !waited[x.src]) {
-            HIPCHK(c, hipStreamWaitEvent(c->stream, cs[x.src]->ev_jfa[(t - 1) & 1], 0));
-            waited[x.src] = 1;
-          }
           HIPCHK(c, hipMemcpyAsync(jfa_xbuf(c, t, x.dst_buf, x.dst_row), jfa_xbuf(cs[x.src], t, 0, x.src_row),
                                    x.rows * rowb, hipMemcpyDeviceToDevice, c->stream));
         }
@@ -1311,6 +1325,28 @@ int rc2dgi_plan_jfa_exchange(const rc2dgi_config *cfg, int world, int step, int 
       const int r[6] = {t.src, t.src_row, t.rows, t.dst, t.dst_buf, t.dst_row};
       for (int k = 0; k < 6; ++k) xfers[6 * n + k] = r[k];
     }
+    ++n;
+  }
+  return n;
+}
+
+int rc2dgi_plan_group_waits(const rc2dgi_config *cfg, int world, int rank, int step, int *peers, int max_peers) {
+  if (!cfg || cfg->screen_width < 1 || cfg->screen_height < 1 || world < 2 || rank < 0 || rank >= world ||
+      world > cfg->screen_height || cfg->cascade_count < 1 || cfg->cascade_count > 15 || !(cfg->render_scale > 0.0f) ||
+      max_peers < 0 || (max_peers > 0 && !peers))
+    return RC2DGI_E_ARG;
+  int CW, CH, S;
+  derive_sizes(cfg->screen_width, cfg->screen_height, cfg->cascade_count, cfg->render_scale, CW, CH, S);
+  if (S < 2 || step < 1 || step >= S) return RC2DGI_E_ARG;
+  std::vector<int> readers, senders;
+  group_step_waits(plan_jfa_exchange(cfg->screen_width, cfg->screen_height, S, world), rank, step, readers, senders);
+  int n = 0;
+  for (int q : readers) {
+    if (n < max_peers) peers[n] = q;
+    ++n;
+  }
+  for (int q : senders) {
+    if (n < max_peers) peers[n] = -1 - q;  // senders as -1 - shard
     ++n;
   }
   return n;
@@ -1492,6 +1528,10 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_tail[L] = value;
     return RC2DGI_OK;
   }
+  if (k == "rc_pal") {
+    c->rc_pal = value != 0;
+    return RC2DGI_OK;
+  }
   if (k == "rc_phase" || k.rfind("rc_phase_L", 0) == 0) {
     if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "rc_phase is 0 (off), 1 (first sample), 2 (lockstep)");
     if (k == "rc_phase") {
@@ -1564,6 +1604,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
     const int L = std::atoi(k.c_str() + 7);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
     *value = c->rc_mp[L];
+    return RC2DGI_OK;
+  }
+  if (k == "rc_pal") {
+    *value = c->rc_pal;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_phase_L", 0) == 0) {

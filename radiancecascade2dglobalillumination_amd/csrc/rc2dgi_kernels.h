@@ -113,6 +113,7 @@ struct RcLevelArgs {
   const unsigned short *dist_tiled = nullptr;  // 8x8-tiled distance field (variants "t")
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
   const uint4 *dist_nib = nullptr;             // nibble-predicted distance field (variants "n", k_dist_nib)
+  const float4 *cell_pal = nullptr;  // surface palettes: `dist` is then the march field (launch_shade_cmin), or nullptr
   const unsigned short *dist_phase = nullptr;  // phase-plane copy of distRT for this level (k_dist_phase), or nullptr
   int phase_mode = 0;  // 1: the first lockstep sample of every ray reads dist_phase, 2: every lockstep sample
   const CminT *cmin = nullptr;  // coarse lower bound of the field (launch_dist_cmin); nullptr: no exit proofs
@@ -129,8 +130,15 @@ int dist_cmin_shift(int W, int H);
 // launch_shade and launch_dist_cmin (with hitc) as one pass over distRT: square power-of-two screens with
 // cells of >= 64 texels only (shade_cmin_fused_ok; 4096^2 and up)
 bool shade_cmin_fused_ok(int W, int H, int pitch);
+// Surface palettes (launch_shade_cmin with mf / cpal): kCellPal distinct hit records per bound-table cell, and
+// the march field mf = distRT with each hittable texel's q (<= 65: decode_dist < 0.001) replaced by the index of
+// its record in its cell's palette, kCellPal when the palette is full (the record is then read from shade).
+// A march reading mf takes the same samples (a hit is still a value <= 65, other texels keep q) and finds a
+// hit's record in a 1 MB table shared by all the rays that end on one surface of the cell.
+constexpr int kCellPal = 15, kCellPalStride = 16;  // entries per cell (index 15 marks "no entry"), slots per cell
 hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
-                             ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st);
+                             ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st,
+                             unsigned short *mf = nullptr, float4 *cpal = nullptr);
 hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st,
                             unsigned char *hitc = nullptr);
 // Directional clear distances of the march proofs (k_rc_level, one-probe tiles): kDirBins angular bins x

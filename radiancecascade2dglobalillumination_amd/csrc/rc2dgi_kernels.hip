@@ -553,13 +553,28 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
 // w, w + 4, ... of it, a lane one column of each 64-column run, 16 rows at a time (each load instruction
 // one contiguous run: 128 B of distance, 1 KB of emission or albedo).  Same records, same bound table and
 // flags as the two kernels (the cell minimum includes the REPEAT-wrap texels of the last row / column).
+// PAL: also the cell's surface palette and the march field (see kCellPal): the distinct records of the
+// cell's hittable texels in cpal[cell * kCellPal + i] (deduplicated in LDS; two waves inserting one record
+// at once may both add it -- a wasted entry, never a wrong one), and mf = distRT with every hittable texel's
+// q replaced by its palette entry i (kCellPal: no entry left, the march reads its record from shade).
+template <bool PAL>
 __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__restrict__ dist,
                                                     const float4 *__restrict__ color, const float4 *__restrict__ emis,
                                                     float4 *__restrict__ shade, ScreenDims s, float reflectivity,
-                                                    int csh, CminT *__restrict__ cmin, unsigned char *__restrict__ hitc) {
+                                                    int csh, CminT *__restrict__ cmin, unsigned char *__restrict__ hitc,
+                                                    unsigned short *__restrict__ mf, float4 *__restrict__ cpal) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cw = 1 << csh;
   const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
+  __shared__ float4 s_pal[PAL ? kCellPal : 1];
+  __shared__ unsigned s_rdy[PAL ? kCellPal : 1];  // entry i holds its record (set after the record is written)
+  __shared__ unsigned s_npal;
+  if (PAL) {
+    if (threadIdx.x == 0) s_npal = 0u;
+    if (threadIdx.x < kCellPal) s_rdy[threadIdx.x] = 0u;
+    __syncthreads();
+  }
+  float4 *const gpal = PAL ? cpal + (size_t)(blockIdx.y * kCminDim + blockIdx.x) * kCellPalStride : nullptr;
   unsigned m = 0xFFFFu;
   const size_t rstep = (size_t)4 * s.pitch;  // a wave's consecutive rows are 4 apart
   for (int c = lane; c < cw; c += 64) {
@@ -578,7 +593,14 @@ __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__rest
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        if (!(hm >> (8 * h) & 0xFFu)) continue;
+        // (with palettes the skip is wave-uniform: the palette code below needs every lane of the wave)
+        if (PAL ? __ballot((hm >> (8 * h) & 0xFFu) != 0u) == 0ull : !(hm >> (8 * h) & 0xFFu)) {
+          if (PAL) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) mf[base + (8 * h + k) * rstep] = (unsigned short)q[8 * h + k];
+          }
+          continue;
+        }
         float4 e[8], cl[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -590,11 +612,57 @@ __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__rest
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          if (hm >> (8 * h + k) & 1u) {
-            float4 rec = make_float4(e[k].x, e[k].y, e[k].z, 1.0f);
-            if (!(sqrtf(e[k].x * e[k].x + e[k].y * e[k].y + e[k].z * e[k].z) > 0.0f))
-              rec = make_float4(cl[k].x, cl[k].y, cl[k].z, reflectivity);
-            shade[base + (8 * h + k) * rstep] = rec;
+          const bool hit = hm >> (8 * h + k) & 1u;
+          float4 rec = make_float4(e[k].x, e[k].y, e[k].z, 1.0f);
+          if (!(sqrtf(e[k].x * e[k].x + e[k].y * e[k].y + e[k].z * e[k].z) > 0.0f))
+            rec = make_float4(cl[k].x, cl[k].y, cl[k].z, reflectivity);
+          if (hit) shade[base + (8 * h + k) * rstep] = rec;
+          if (PAL) {
+            // the wave's distinct records of this row, one at a time (usually one: a surface's texels of a
+            // 64-texel run share it): the first remaining lane's record, the lanes holding the same bits,
+            // the entry found or added by lane 0 of the wave
+            unsigned idx = kCellPal;
+            unsigned long long rem = __ballot(hit);
+            while (rem) {
+              const int ld = __ffsll((long long)rem) - 1;
+              const float rx = __shfl(rec.x, ld, 64), ry = __shfl(rec.y, ld, 64), rz = __shfl(rec.z, ld, 64),
+                          rw = __shfl(rec.w, ld, 64);
+              const auto same = [&](float4 v) {
+                return __float_as_uint(v.x) == __float_as_uint(rx) && __float_as_uint(v.y) == __float_as_uint(ry) &&
+                       __float_as_uint(v.z) == __float_as_uint(rz) && __float_as_uint(v.w) == __float_as_uint(rw);
+              };
+              const unsigned long long mine = __ballot(hit && same(rec)) & rem;
+              // the lanes below the palette's fill compare one entry each; lane 0 adds the record if none holds it
+              const unsigned n = min(__builtin_amdgcn_readfirstlane(*(volatile unsigned *)&s_npal), (unsigned)kCellPal);
+              // (an entry counted but not yet written is skipped: at worst the record is added twice)
+              bool hold = false;
+              if ((unsigned)lane < n) {
+                const bool rdy = *(volatile unsigned *)&s_rdy[lane] != 0u;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                const volatile float *pe = reinterpret_cast<const volatile float *>(&s_pal[lane]);
+                hold = rdy && same(make_float4(pe[0], pe[1], pe[2], pe[3]));
+              }
+              const unsigned long long found = __ballot(hold);
+              unsigned e_idx;
+              if (found) {
+                e_idx = (unsigned)(__ffsll((long long)found) - 1);
+              } else {
+                unsigned slot = 0;
+                if (lane == 0) {
+                  slot = atomicAdd(&s_npal, 1u);
+                  if (slot < (unsigned)kCellPal) {
+                    s_pal[slot] = make_float4(rx, ry, rz, rw);
+                    gpal[slot] = make_float4(rx, ry, rz, rw);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                    *(volatile unsigned *)&s_rdy[slot] = 1u;
+                  }
+                }
+                e_idx = min((unsigned)__builtin_amdgcn_readfirstlane((int)slot), (unsigned)kCellPal);
+              }
+              if ((mine >> lane) & 1ull) idx = e_idx;
+              rem &= ~mine;
+            }
+            mf[base + (8 * h + k) * rstep] = (unsigned short)(hit ? idx : q[8 * h + k]);
           }
         }
       }
@@ -1572,10 +1640,15 @@ bool shade_cmin_fused_ok(int W, int H, int pitch) {
 }
 
 hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
-                             ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st) {
+                             ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st,
+                             unsigned short *mf, float4 *cpal) {
   if (!shade_cmin_fused_ok(s.W, s.H, s.pitch)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_shade_cmin, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, color, emis, shade, s, reflectivity,
-                     dist_cmin_shift(s.W, s.H), cmin, hitc);
+  if (mf && cpal)
+    hipLaunchKernelGGL(k_shade_cmin<true>, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, color, emis, shade, s,
+                       reflectivity, dist_cmin_shift(s.W, s.H), cmin, hitc, mf, cpal);
+  else
+    hipLaunchKernelGGL(k_shade_cmin<false>, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, color, emis, shade, s,
+                       reflectivity, dist_cmin_shift(s.W, s.H), cmin, hitc, mf, cpal);
   return hipGetLastError();
 }
 

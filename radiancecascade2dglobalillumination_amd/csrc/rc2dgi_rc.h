@@ -36,6 +36,9 @@ struct RcParams {
   const unsigned short *dph;  // phase-plane copy of distRT for this level (k_dist_phase), nullptr: off
   int phm;                    // 1: the first lockstep sample reads dph, 2: every lockstep sample
   int phcw, phch;             // log2 of the columns / rows per phase plane (log2(W) - level, log2(H) - level)
+  const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
+                              // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
+  int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   unsigned long long *stats;  // diagnostic builds: [16 levels][16] counters (rc2dgi_diag_stats)
 #endif
@@ -217,6 +220,20 @@ __device__ __forceinline__ unsigned ld_dist_esc(const unsigned short *dist, unsi
   return v;
 }
 
+// Surface palettes (P.cpal, launch_shade_cmin): the march reads the march field, where a hittable texel holds
+// the index of its record in its cell's palette instead of its q (both <= 65: the march's hit test is
+// unchanged).  A hit is kept as its byte offset with that index in bits 27-30 (screens of up to 2^26 texels),
+// kCellPal when the cell's palette had no room (the record is then read from shade).
+__device__ __forceinline__ int pal_mark(unsigned boff, unsigned q) { return (int)(boff | (min(q, (unsigned)kCellPal) << 27)); }
+// the record of hit h (byte-offset convention, pal_mark when palettes are on)
+__device__ __forceinline__ float4 hit_record(const float4 *shade, const float4 *cpal, int h, int lgw, int csh) {
+  const unsigned t = cpal ? ((unsigned)h & 0x07FFFFFFu) >> 1 : (unsigned)h >> 1, e = (unsigned)h >> 27;
+  const unsigned cell = ((t >> (lgw + csh)) * (unsigned)kCminDim) + ((t & ((1u << lgw) - 1u)) >> csh);
+  // one load either way: the palette entry, or the texel's record (palettes off, or no entry)
+  const float4 *p = (cpal && e < (unsigned)kCellPal) ? cpal + (cell * kCellPalStride + e) : shade + t;
+  return *p;
+}
+
 // Packed distance field (DL = 2, k_dist_pack): one 16-byte packet per 14 texels of a row.  Bytes
 // 0-1 hold the packet's minimum q, byte 2 + t the excess q - min of texel t, or 255 (escape: read
 // the 16-bit field).  A distance field changes by at most 65535 / max(W, H) per texel plus the
@@ -291,6 +308,10 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
   }
 }
 
+#ifndef RC2DGI_EARLY_UPPER
+#define RC2DGI_EARLY_UPPER 1  // k_rc_level: upper-cascade samples before the hit records arrive (A/B: -D...=0)
+#endif
+
 // ISA section markers (scripts/isa_mix.py builds with -DRC2DGI_ISA_SECTIONS to split the kernel's
 // instruction mix into staging / march / tail / merge; the product build has none)
 #ifdef RC2DGI_ISA_SECTIONS
@@ -351,6 +372,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr int CMN = kCminDim * kCminDim;
   __shared__ __attribute__((aligned(16))) CminT s_cm[CMS ? CMN : 1];
   constexpr bool TLC = !Z0 && NR == 4;  // one probe and one direction block per lane (the high-level tiles)
+  constexpr bool PALC = TLC && !TILED && !PACKED;  // surface palettes (P.cpal): the one-probe tiles of the plain field
   // Tail compaction.  A lane marches its NR rays in lockstep and a wave runs until its longest ray
   // ends, so the few rays that pass close to a surface (steps shrink, then grow geometrically) set
   // the loop count of the whole wave: at L4 the waves run ~1.8x the iterations of their average
@@ -783,7 +805,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     for (int k = 0; k < NR; ++k) {  // branch-free: selects, no exec-mask juggling
       const float d = decode_dist(q[k]);
       const bool hit = live[k] && d < 0.001f;
-      hit_idx[k] = hit ? idx[k] : hit_idx[k];
+      if (PALC && P.cpal)
+        hit_idx[k] = hit ? pal_mark((unsigned)idx[k], q[k]) : hit_idx[k];
+      else
+        hit_idx[k] = hit ? idx[k] : hit_idx[k];
       const float tn = t[k] + d;
       const bool go = live[k] && !hit && !(tn > P.t1);  // the next iteration's interval test, done now
       t[k] = go ? tn : kDone;
@@ -866,9 +891,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         }
         if (!live) break;
         const int idx = (int)__umul24((unsigned)iy, (unsigned)P.s.pitch) + ix;
-        const float d = decode_dist(fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx));
+        const unsigned qq = fetch_q<DL>(dist, dpk, P.tpr, ix, iy, idx);
+        const float d = decode_dist(qq);
         if (d < 0.001f) {
-          hit = BOFF ? 2 * idx : idx;  // the owner's convention
+          hit = BOFF ? ((PALC && P.cpal) ? pal_mark(2u * (unsigned)idx, qq) : 2 * idx) : idx;  // the owner's convention
           break;
         }
         tt = tt + d;
@@ -922,7 +948,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #ifdef RC2DGI_DIAG_NOHIT  // timing-only ablation build: no hit-record loads (WRONG results)
       if (hit_idx[k] >= 0) hr[k] = make_float4(0.5f, 0.5f, 0.5f, 1.0f);
 #else
-      if (hit_idx[k] >= 0) hr[k] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
+      if (hit_idx[k] >= 0) hr[k] = PALC ? hit_record(shade, P.cpal, hit_idx[k], P.lgw, P.csh) : shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
 #endif
   }
 
@@ -956,12 +982,36 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     for (int dblk = 0; dblk < PD; ++dblk) {
       const int bi = bi0 + dblk;
       float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      // Early upper samples (power-of-two cascades): the four bilinear taps of every ray from the staged
+      // footprint before the hit records are looked at, so the LDS reads and the lerps run while the record
+      // loads are in flight (the shader samples only when radiance.a != 0; a sample computed and not applied
+      // changes nothing -- the apply below is a select on the same test).
+      constexpr bool EUP = RC2DGI_EARLY_UPPER && STG && !TOP && NR == 4;  // (one probe per lane: the registers allow it)
+      float4 upe[EUP ? 4 : 1];
+      if constexpr (EUP) {
+        if (pow2c) {
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const typename GI::S *sr = s_up + (dblk * 4 + r4) * RH * RW;
+            upe[r4] = GI::bilerp(sr[ly0 * RW + lx0], sr[ly0 * RW + lx0 + 1], sr[(ly0 + 1) * RW + lx0],
+                                 sr[(ly0 + 1) * RW + lx0 + 1], wx, wy);
+          }
+        }
+      }
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
         const int r = dblk * 4 + r4;  // index into the 4*PD directions
         float4 rad = hr[p * ND + r];
         const int ai = bi * 4 + r4;  // angleIndex
-        if (rad.w != 0.0f && (STG || TOP)) {
+        if (EUP && pow2c) {
+          const bool m = rad.w != 0.0f;
+          const float4 up = upe[EUP ? r4 : 0];
+          const f2v_t rxy = f2v_t{rad.x, rad.y} + f2v_t{up.x, up.y} * f2v_t{rad.w, rad.w};  // packed pair
+          rad.x = m ? rxy.x : rad.x;
+          rad.y = m ? rxy.y : rad.y;
+          rad.z = m ? rad.z + up.z * rad.w : rad.z;
+          rad.w = m ? rad.w * up.w : rad.w;
+        } else if (rad.w != 0.0f && (STG || TOP)) {
           if (!TOP) {
             typename GI::S t00, t10, t01, t11;
             float ux = wx, uy = wy;
@@ -1069,6 +1119,11 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   P.wgp = a.wg_proof;
   P.dph = (a.dist_phase && a.phase_mode > 0 && p2s && dist_phase_ok(P.s.W, P.s.H, a.level)) ? a.dist_phase : nullptr;
   P.phm = a.phase_mode;
+  // palettes: the plain field's march (DL 0) on power-of-two screens whose byte offsets fit 27 bits
+  P.cpal = (a.cell_pal && DL == 0 && p2s && (size_t)P.s.pitch * P.s.H <= ((size_t)1 << 26)) ? a.cell_pal : nullptr;
+  P.lgw = 0;
+  while ((1 << P.lgw) < P.s.pitch) ++P.lgw;
+  if (P.cpal && (1 << P.lgw) != P.s.pitch) P.cpal = nullptr;
   P.phcw = P.phch = 0;
   while ((1 << (P.phcw + a.level)) < P.s.W) ++P.phcw;
   while ((1 << (P.phch + a.level)) < P.s.H) ++P.phch;

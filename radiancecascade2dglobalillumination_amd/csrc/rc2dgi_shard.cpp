@@ -321,4 +321,18 @@ RowSet jfa_mask_rows(int W, int H, int rank, int world) {
   return r;
 }
 
+void group_step_waits(const JfaExchange &x, int k, int t, std::vector<int> &readers, std::vector<int> &senders) {
+  readers.clear();
+  senders.clear();
+  const auto add = [](std::vector<int> &v, int q) {
+    if (std::find(v.begin(), v.end(), q) == v.end()) v.push_back(q);
+  };
+  if (t >= 2 && t - 1 < (int)x.steps.size())
+    for (const JfaXfer &e : x.steps[t - 1].xfers)
+      if (e.src == k && e.dst != k) add(readers, e.dst);
+  if (t >= 1 && t < (int)x.steps.size())
+    for (const JfaXfer &e : x.steps[t].xfers)
+      if (e.dst == k && e.src != k) add(senders, e.src);
+}
+
 }  // namespace rc2dgi

@@ -88,6 +88,10 @@ JfaExchange plan_jfa_exchange(int W, int H, int S, int world);
 // where shard `rank` finds the rows tap y of step t reads: buffer (0 window, 1 A, 2 B) and the
 // global row (mod H) of the buffer's local row 0
 void jfa_window(const JfaExchange &x, int t, int rank, int buf[3], int row0[3]);
+// The peers whose step t-1 shard k awaits before its step t of a group frame (rc2dgi_do_group, one stream per
+// shard; peers = every shard but k): readers[] -- those that copied rows of k's J_{t-2} before their step t-1
+// (step t overwrites that ping-pong buffer), senders[] -- those whose rows of J_{t-1} k copies before step t.
+void group_step_waits(const JfaExchange &x, int k, int t, std::vector<int> &readers, std::vector<int> &senders);
 // screen rows of the ScreenUV mask step 0 of shard `rank` reads
 RowSet jfa_mask_rows(int W, int H, int rank, int world);
 

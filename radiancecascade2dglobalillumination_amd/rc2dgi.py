@@ -112,6 +112,8 @@ def load_library(path: Optional[str] = None):
                                      ctypes.c_int),
         "rc2dgi_plan_jfa_window": ([ctypes.POINTER(_Config), ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ip],
                                    ctypes.c_int),
+        "rc2dgi_plan_group_waits": ([ctypes.POINTER(_Config), ctypes.c_int, ctypes.c_int, ctypes.c_int, ip,
+                                     ctypes.c_int], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -455,6 +457,19 @@ def plan_jfa_exchange(W: int, H: int, N: int, world: int, step: int, render_scal
     buf = (ctypes.c_int * max(6 * n, 1))()
     L.rc2dgi_plan_jfa_exchange(ctypes.byref(cfg), world, step, info, buf, n)
     return dict(zip(JFA_INFO, list(info))), [tuple(buf[6 * k:6 * k + 6]) for k in range(n)]
+
+
+def plan_group_waits(W: int, H: int, N: int, world: int, rank: int, step: int, render_scale: float = 1.0):
+    """Host-only: the peers shard `rank` of a group frame awaits (their step step-1 done) before JFA step
+    `step` (rc2dgi_plan_group_waits): (readers of its J_{step-2}, senders of the J_{step-1} rows it copies)."""
+    L = load_library()
+    cfg = _Config(W, H, N, render_scale, 2.0, 0, 0, 0, (ctypes.c_int * 4)())
+    buf = (ctypes.c_int * max(2 * world, 1))()
+    n = L.rc2dgi_plan_group_waits(ctypes.byref(cfg), world, rank, step, buf, 2 * world)
+    if n < 0:
+        raise RC2DGIError(n, "rc2dgi_plan_group_waits")
+    got = list(buf[:n])
+    return sorted(q for q in got if q >= 0), sorted(-1 - q for q in got if q < 0)
 
 
 def plan_jfa_window(W: int, H: int, N: int, rank: int, world: int, step: int, render_scale: float = 1.0):

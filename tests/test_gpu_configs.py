@@ -58,6 +58,8 @@ def apply_schedule(ctx, sched, N, shards=1):
         ph = sub.get("rc_phase") or sched.get("rc_phase")
         if ph:
             ctx.set_tuning(f"rc_phase_L{L}", ph[L])
+    for k, v in {**sched.get("knobs", {}), **sub.get("knobs", {})}.items():
+        ctx.set_tuning(k, int(v))
 
 
 def level_offsets(N):

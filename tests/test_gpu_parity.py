@@ -420,6 +420,52 @@ def test_phase_plane_samples_are_bit_identical(RC2DGI, W, H, N, rr, scene, stora
     ctx.close()
 
 
+def speckled_scene(W, H, seed=7):
+    """The demo scene with every occluder and emitter texel given its own random k/255 colour: far more
+    than kCellPal distinct hit records per bound-table cell (the palettes overflow, hits read shade)."""
+    from radiancecascade2dglobalillumination_amd import scenes
+
+    color, emis = (np.array(a, np.float32, order="C") for a in scenes.demo(W, H))
+    rng = np.random.default_rng(seed)
+    for img in (color, emis):
+        m = np.any(img[..., :3] > 0, axis=-1)
+        img[m, :3] = rng.integers(1, 256, size=(int(m.sum()), 3)).astype(np.float32) / np.float32(255)
+    return color, emis
+
+
+@pytest.mark.parametrize("scene", ["demo", "speckled", "rand:43"])
+def test_surface_palettes_are_bit_identical(RC2DGI, scene):
+    """rc_pal (per-cell surface palettes and the march field, launch_shade_cmin; the one-probe tiles of the
+    plain field read a hit's record from its cell's palette) against the same frame without: every level
+    and every output texture bit for bit, at 4096^2 N=6 (the fused records pass needs cells of >= 64
+    texels), with the one-probe variants at L1-L5; the speckled scene overflows the palettes."""
+    W = H = 4096
+    N = 6
+    color, emis = speckled_scene(W, H) if scene == "speckled" else make_scene(scene, W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0)
+    ctx.set_keep_levels(True)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    for v in (0, 13, 20):
+        for L in range(1, N):
+            ctx.set_tuning(f"rc_variant_L{L}", v)
+        want = {}
+        for pal in (0, 1):
+            ctx.set_tuning("rc_pal", pal)
+            assert ctx.get_tuning("rc_pal") == pal
+            ctx.do_rc2dgi()
+            ctx.sync()
+            got = {f"L{L}": ctx.download_level(L) for L in range(N)}
+            got.update({k: ctx.download(k) for k in ("color", "temp", "final_gi")})
+            if pal == 0:
+                want = got
+            else:
+                for k in got:
+                    assert np.array_equal(got[k], want[k]), \
+                        f"{scene} variant {v} {k}: {np.count_nonzero(got[k] != want[k])} differ with palettes"
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,rs,radius", [
     (128, 128, 1.0, 1.5),    # fixed taps (F=1), merge fused
     (256, 128, 1.0, 2.5),    # F=2

@@ -359,3 +359,28 @@ def test_missing_exchange_row_is_detected():
             for s in shards:
                 s.jfa_step(t)
     del full
+
+
+@pytest.mark.parametrize("W,H,N,world", [(8192, 8192, 8, 8), (4096, 4096, 6, 8), (1200, 900, 6, 4), (512, 512, 6, 3),
+                                         (256, 192, 4, 2), (333, 200, 4, 5)])
+def test_group_frame_awaits_every_reader_of_the_overwritten_step(W, H, N, world):
+    """rc2dgi_do_group runs each shard on its own stream: before shard k's JumpFlood step t overwrites the
+    ping-pong buffer holding its J_{t-2}, every peer that copied rows of J_{t-2} from k (the transfers of
+    step t-1, taken from the exchange plan here) must be awaited, and so must every owner of the rows of
+    J_{t-1} that k copies before step t.  The wait sets are the ones the library's group loop uses
+    (group_step_waits, exported as rc2dgi_plan_group_waits)."""
+    S = int(np.log(max(W, H)) / np.log(2))
+    for t in range(1, S):
+        prev = R.plan_jfa_exchange(W, H, N, world, t - 1)[1] if t >= 2 else []
+        cur = R.plan_jfa_exchange(W, H, N, world, t)[1]
+        for k in range(world):
+            readers, senders = R.plan_group_waits(W, H, N, world, k, t)
+            want_r = sorted({x[3] for x in prev if x[0] == k and x[3] != k})
+            want_s = sorted({x[0] for x in cur if x[3] == k and x[0] != k})
+            assert readers == want_r, (t, k, readers, want_r)
+            assert senders == want_s, (t, k, senders, want_s)
+            assert k not in readers and k not in senders
+    # the event slot a wait names (ev_jfa[(t-1) & 1], recorded after step t-1) is not re-recorded by that
+    # peer before the wait is enqueued: the group loop enqueues step t of shards 0..n-1 in order, and a peer
+    # q < k has already recorded slot t & 1 (the other one) at step t, a peer q > k only slot (t-1) & 1 at t-1
+    assert all(((t - 1) & 1) != (t & 1) for t in range(1, S))
