@@ -279,9 +279,6 @@ def apply_schedule(g, tun, N, shards=1):
     for L in range(N):
         g.set_tuning(f"rc_order_L{L}", (sub.get("rc_order") or tun["rc_order"])[L])
         g.set_tuning(f"rc_variant_L{L}", (sub.get("rc_variant") or tun["rc_variant"])[L])
-        ph = sub.get("rc_phase") or tun.get("rc_phase")
-        if ph:  # optional: phase-plane march samples per level (rc_phase_L<n>)
-            g.set_tuning(f"rc_phase_L{L}", ph[L])
     for k, v in {**tun.get("knobs", {}), **sub.get("knobs", {})}.items():  # optional tuning knobs (rc_skip, ...)
         g.set_tuning(k, int(v))
 
@@ -485,6 +482,12 @@ def main():
     committed = schedule_path(W, H, N, a.ray_range, a.storage)
     if not a.load_tuning and not a.autotune and not a.no_autotune and os.path.exists(committed):
         a.load_tuning = committed  # the committed schedule: the one the parity tests check at this size
+    def apply_tunes():
+        for kv in a.tune:
+            k, v = kv.split("=")
+            ctx.set_tuning(k, int(v))
+
+    apply_tunes()  # (before an autotune, so it tunes under these knobs)
     if a.load_tuning:
         with open(a.load_tuning) as f:
             tun = json.load(f)
@@ -492,16 +495,14 @@ def main():
         orders = tun["rc_order"]
     else:
         orders = None if a.no_autotune else ctx.autotune(3)  # setup: schedule choice, results identical
-    for kv in a.tune:
-        k, v = kv.split("=")
-        ctx.set_tuning(k, int(v))
+    apply_tunes()  # (and after a schedule, over its knobs)
     variants = [ctx.get_tuning(f"rc_variant_L{L}") for L in range(N)]
     orders = [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)] if orders else None
     if a.save_tuning and rank == 0:
         with open(a.save_tuning, "w") as f:
             json.dump({"config": f"{W}x{H} N={N} rayRange={a.ray_range} {a.storage}",
                        "rc_order": [ctx.get_tuning(f"rc_order_L{L}") for L in range(N)], "rc_variant": variants,
-                       "rc_phase": [ctx.get_tuning(f"rc_phase_L{L}") for L in range(N)]}, f)
+                       **({"knobs": {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.tune}} if a.tune else {})}, f)
     ctx.set_timing(True)
     if a.sweep_rc:
         sweep_rc(ctx, N, a.steps, rounds=3)
@@ -570,7 +571,7 @@ def main():
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
                    "parallelism": f"replicas{world}",
                    "rc_order": orders or "default", "rc_variant": variants,
-                   "rc_phase": [ctx.get_tuning(f"rc_phase_L{L}") for L in range(N)],
+                   "rc_pal": ctx.get_tuning("rc_pal"),
                    "rc_skip": ctx.get_tuning("rc_skip"),
                    "rc_schedule": (os.path.relpath(a.load_tuning, ROOT) if a.load_tuning else
                                    ("default" if a.no_autotune else "autotune in setup"))},

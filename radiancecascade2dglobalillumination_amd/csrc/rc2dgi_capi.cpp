@@ -102,7 +102,6 @@ struct rc2dgi_ctx {
   unsigned short *dist_t = nullptr;  // 8x8-tiled copy for the "t" RC variants
   uint4 *dist_p = nullptr;           // packed copy for the "p" RC variants (k_dist_pack)
   uint4 *dist_n = nullptr;           // nibble-predicted copy for the "n" RC variants (k_dist_nib)
-  std::vector<unsigned short *> dist_ph;  // per level: phase-plane copy of distRT (tuning rc_phase_L<n>, k_dist_phase)
   unsigned short *mfield = nullptr;  // march field of the surface palettes (tuning rc_pal, launch_shade_cmin)
   float4 *cell_pal = nullptr;        // kCminDim^2 cells x kCellPalStride palette entries
   int rc_pal = 1;                    // surface palettes on (where they apply: 4096^2 .. 8192^2 square screens)
@@ -135,7 +134,6 @@ struct rc2dgi_ctx {
   std::vector<int> rc_tail;      // per level: tail compaction after this many lockstep iterations (tuning rc_tail_L<n>)
   int rc_wgproof = 1;            // tuning "rc_wgproof": workgroup-wide exit proof of the first samples
   std::vector<int> rc_mp;        // per level: directional miss proofs in the one-probe tiles (tuning rc_mp_L<n>)
-  std::vector<int> rc_phase;     // per level: march samples from the phase-plane copy (tuning rc_phase_L<n>: 0, 1, 2)
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   int jfa_coset = 1;             // tuning "jfa_coset": the first four steps in one kernel (k_jfa_coset) where they apply
@@ -231,16 +229,8 @@ void free_level_bufs(rc2dgi_ctx *c) {
   c->level_bufs.clear();
 }
 
-void free_phase_bufs(rc2dgi_ctx *c) {
-  for (unsigned short *&p : c->dist_ph) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-  }
-}
-
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
-  free_phase_bufs(c);
   c->rc_maps.clear();
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
@@ -390,8 +380,6 @@ int allocate(rc2dgi_ctx *c) {
   for (int L = 0; L < c->N; ++L) c->rc_order[L] = default_rc_order(L);
   c->rc_tail.assign(c->N, kDefaultTail);
   c->rc_mp.assign(c->N, 1);  // directional miss proofs wherever they apply (one-probe tiles, 4^L >= kDirBins)
-  c->rc_phase.assign(c->N, 0);
-  c->dist_ph.assign(c->N, nullptr);
   if (int rc = jfa_buffers(c)) return rc;
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
@@ -917,8 +905,11 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     nib |= rc_variant_nib(v);
   }
   if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
-  if (packed) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
-  if (nib) HIPCHK(c, launch_dist_nib(c->dist, c->sd.pitch, c->dist_n, c->W, c->H, st));
+  // (the packed marches run on power-of-two screens of up to 16384 columns only; elsewhere their variants
+  // launch the plain-field march, and the copies would be built for nothing)
+  const bool p2s = c->sd.powW && c->sd.powH && c->cd.powW && c->cd.powH && c->W <= 16384;
+  if (packed && p2s) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
+  if (nib && p2s) HIPCHK(c, launch_dist_nib(c->dist, c->sd.pitch, c->dist_n, c->W, c->H, st));
   // exit proofs: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
   // staging and barrier cost more than the skipped samples save (RC 0.338 vs 0.376 ms, measured)
   const bool proofs = c->rc_skip > 1 || (c->rc_skip == 1 && std::max(c->W, c->H) >= 2048);
@@ -978,13 +969,6 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
-    if (c->rc_phase[L] > 0 && dist_phase_ok(c->W, c->H, L) && rc_variant_one_probe(c->rc_variant[L])) {
-      // the level's phase-plane copy, made right before it (timed with the level)
-      if (!c->dist_ph[L]) HIPCHK(c, alloc(&c->dist_ph[L], (size_t)c->sd.pitch * c->H * sizeof(unsigned short)));
-      HIPCHK(c, launch_dist_phase(a.dist, c->sd.pitch, c->dist_ph[L], c->W, c->H, L, st));
-      a.dist_phase = c->dist_ph[L];
-      a.phase_mode = c->rc_phase[L];
-    }
 
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
@@ -1106,7 +1090,7 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   // march rolled / unrolled x linear / 8x8-tiled / packed / nibble-predicted distance field; 32x8 tiles
   // (x2 probes per lane); one probe per lane in 512- and 1024-lane workgroups
   // (RGBA16F / RGBA8 cascades build the 16x16x1 family only: the other ids would time that kernel again)
-  const int kVariantsF32[] = {0, 3, 6, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
+  const int kVariantsF32[] = {0, 1, 3, 5, 6, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
   const int kVariantsOther[] = {0, 13, 14, 15, 16, 17, 18, 19};
   const bool f32 = c->storage == RC2DGI_STORAGE_F32;
   const int *kVariants = f32 ? kVariantsF32 : kVariantsOther;
@@ -1532,17 +1516,6 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_pal = value != 0;
     return RC2DGI_OK;
   }
-  if (k == "rc_phase" || k.rfind("rc_phase_L", 0) == 0) {
-    if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "rc_phase is 0 (off), 1 (first sample), 2 (lockstep)");
-    if (k == "rc_phase") {
-      for (int &v : c->rc_phase) v = value;
-      return RC2DGI_OK;
-    }
-    const int L = std::atoi(k.c_str() + 10);
-    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
-    c->rc_phase[L] = value;
-    return RC2DGI_OK;
-  }
   if (k.rfind("rc_order_L", 0) == 0) {
     const int L = std::atoi(k.c_str() + 10);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
@@ -1608,12 +1581,6 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "rc_pal") {
     *value = c->rc_pal;
-    return RC2DGI_OK;
-  }
-  if (k.rfind("rc_phase_L", 0) == 0) {
-    const int L = std::atoi(k.c_str() + 10);
-    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
-    *value = c->rc_phase[L];
     return RC2DGI_OK;
   }
   if (k.rfind("rc_order_L", 0) == 0) {

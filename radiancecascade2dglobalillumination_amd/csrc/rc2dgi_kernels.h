@@ -114,8 +114,6 @@ struct RcLevelArgs {
   const uint4 *dist_packed = nullptr;          // packed distance field (variants "p", k_dist_pack)
   const uint4 *dist_nib = nullptr;             // nibble-predicted distance field (variants "n", k_dist_nib)
   const float4 *cell_pal = nullptr;  // surface palettes: `dist` is then the march field (launch_shade_cmin), or nullptr
-  const unsigned short *dist_phase = nullptr;  // phase-plane copy of distRT for this level (k_dist_phase), or nullptr
-  int phase_mode = 0;  // 1: the first lockstep sample of every ray reads dist_phase, 2: every lockstep sample
   const CminT *cmin = nullptr;  // coarse lower bound of the field (launch_dist_cmin); nullptr: no exit proofs
   const unsigned char *dclr = nullptr;  // directional clear distances (launch_dir_clear): the one-probe tiles prove
                                        // misses with them instead of cmin (levels with 4^L >= kDirBins)
@@ -148,14 +146,6 @@ constexpr int kDirBins = 64;
 // points reach, for cells of 2^csh texels; kDirBins x kCminDim entries (host)
 void dir_clear_boxes(int csh, int4 *boxes);
 hipError_t launch_dir_clear(const unsigned char *hitc, const int4 *boxes, unsigned char *dclr, hipStream_t st);
-
-// distRT -> its phase-plane copy for level `lg` (probe spacing s = 2^lg texels, power-of-two screens of up to
-// 16384 columns): texel (x, y) moves to column (x mod s) W/s + x div s of row (y mod s) H/s + y div s, so the
-// probes of a level, s texels apart, sample consecutive texels of one row whenever their rays sit at one t
-// (k_rc_level's first lockstep sample).  Same pitch as distRT.
-bool dist_phase_ok(int W, int H, int lg);
-hipError_t launch_dist_phase(const unsigned short *dist, int pitch, unsigned short *phase, int W, int H, int lg,
-                             hipStream_t st);
 
 // distRT -> 8x8-tiled copy (tiles row-major, ceil(W/8) tiles per row; rows padded to 8)
 hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned short *tiled, int W, int H,

@@ -104,22 +104,24 @@ struct JfaOffsets {
 // A 256-thread workgroup covers 64 x (4*JT) texels; each lane owns JT texels 4 rows apart and issues all 9*JT tap loads before the first compare (latency-bound gathers).
 constexpr int JT = 4;
 
-template <bool FIRST, bool U8>
+// RT: rows per lane (JT on large screens; 1 on small ones, where 4 rows per lane left about one wave per SIMD:
+// 1200 x 900 = 1083 workgroups, each step a few exposed round trips)
+template <bool FIRST, bool U8, int RT = JT>
 __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ src, int src_pitch,
                                                   unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                   ScreenDims s, JfaOffsets o, int row0, int row1, JfaSrc win,
                                                   int dst_row0) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j0 = row0 + blockIdx.y * (4 * JT) + (threadIdx.x >> 6);
+  const int j0 = row0 + blockIdx.y * (4 * RT) + (threadIdx.x >> 6);
   if (i >= s.W) return;
   const Axis ax{s.W, s.powW}, ay{s.H, s.powH};
   const float u = texcoord(i, ax);
   int ti[3];
 #pragma unroll
   for (int x = 0; x < 3; ++x) ti[x] = wrap_nearest(u + o.ox[x], ax);
-  unsigned seed[JT][9];
+  unsigned seed[RT][9];
 #pragma unroll
-  for (int t = 0; t < JT; ++t) {
+  for (int t = 0; t < RT; ++t) {
     const int j = min(j0 + 4 * t, row1 - 1);  // clamped rows are computed but not stored
     const float v = texcoord(j, ay);
 #pragma unroll
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
     }
   }
 #pragma unroll
-  for (int t = 0; t < JT; ++t) {
+  for (int t = 0; t < RT; ++t) {
     const int j = j0 + 4 * t;
     if (j >= row1) break;
     const float v = texcoord(j, ay);
@@ -1148,6 +1150,9 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     o.oy[k] = off_y[k];
   }
   const dim3 grid(ceil_div(s.W, 64), ceil_div(row1 - row0, 4 * JT));
+  // float-path steps on small screens: one row per lane (k_jfa_step RT)
+  const bool small = (size_t)s.W * (size_t)(row1 - row0) <= ((size_t)1 << 21);
+  const dim3 grid1(ceil_div(s.W, 64), ceil_div(row1 - row0, 4));
   JfaTaps tp;
   const bool p2 = jfa_p2_taps(s, off_x, off_y, &tp);
   // lattice order (k_jfa_p2) for whole-frame launches whose steps span several tiles (not the
@@ -1164,11 +1169,18 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
       hipLaunchKernelGGL((k_jfa_p2<false, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp,
                          row0, row1, lattice, win, dst_row0);
   } else if (s.u8) {  // RGBA8 jumpRT: quantized seed uv, the float path
-    if (first)
+    if (small) {
+      if (first)
+        hipLaunchKernelGGL((k_jfa_step<true, true, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
+      else
+        hipLaunchKernelGGL((k_jfa_step<false, true, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
+                           row1, win, dst_row0);
+    } else if (first) {
       hipLaunchKernelGGL((k_jfa_step<true, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
-    else
+    } else {
       hipLaunchKernelGGL((k_jfa_step<false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
                          row1, win, dst_row0);
+    }
   } else if (p2 && lds && !first && !win.on && tp.dx[2] == tp.dy[2] && tp.dy[2] >= 1 && tp.dy[2] <= kJfaLdsMax &&
              (row1 - row0) % (4 * JT) == 0 && s.W % 64 == 0) {
     const bool ikey = s.W == s.H && s.W <= 4096;
@@ -1189,6 +1201,12 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
       if (ikey) RC2DGI_JFA(false, true); else RC2DGI_JFA(false, false);
     }
 #undef RC2DGI_JFA
+  } else if (small) {
+    if (first)
+      hipLaunchKernelGGL((k_jfa_step<true, false, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
+    else
+      hipLaunchKernelGGL((k_jfa_step<false, false, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
+                         row1, win, dst_row0);
   } else if (first) {
     hipLaunchKernelGGL((k_jfa_step<true, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
   } else {
@@ -1567,45 +1585,6 @@ int rc_order_plan(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, in
 
 size_t dist_packed_bytes(int W, int H) { return (size_t)pack_per_row(W) * H * sizeof(uint4); }
 
-
-// Phase-plane copy (launch_dist_phase): one workgroup per input row, read whole into LDS, written permuted as
-// output row (y mod s) H/s + y div s, column X' <- input column (X' mod W/s) s + X' div (W/s).  Both passes
-// are whole coalesced rows; the LDS reads stride by s texels.
-__global__ __launch_bounds__(256) void k_dist_phase(const unsigned short *__restrict__ dist, int pitch,
-                                                    unsigned short *__restrict__ out, int W, int H, int lg, int lgw,
-                                                    int lgh) {
-  __shared__ unsigned short row[16384];
-  const int y = blockIdx.x;
-  const unsigned short *src = dist + (size_t)y * pitch;
-  for (int x = (int)threadIdx.x * 8; x < W; x += 256 * 8)  // 16-byte pieces (W is a multiple of 8 here)
-    *reinterpret_cast<uint4 *>(row + x) = *reinterpret_cast<const uint4 *>(src + x);
-  __syncthreads();
-  const int s = 1 << lg, yo = ((y & (s - 1)) << (lgh - lg)) | (y >> lg);
-  unsigned short *dst = out + (size_t)yo * pitch;
-  const int cw = lgw - lg;  // log2 of the columns per plane
-  for (int xo = (int)threadIdx.x * 2; xo < W; xo += 256 * 2) {
-    const int x0 = ((xo & ((1 << cw) - 1)) << lg) | (xo >> cw), x1 = (((xo + 1) & ((1 << cw) - 1)) << lg) | ((xo + 1) >> cw);
-    *reinterpret_cast<unsigned *>(dst + xo) = (unsigned)row[x0] | ((unsigned)row[x1] << 16);
-  }
-}
-
-static int ilog2(int v) {
-  int l = 0;
-  while ((1 << l) < v) ++l;
-  return l;
-}
-
-bool dist_phase_ok(int W, int H, int lg) {
-  return W >= 16 && W <= 16384 && H >= 1 && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && lg >= 1 && (1 << lg) <= W &&
-         (1 << lg) <= H;
-}
-
-hipError_t launch_dist_phase(const unsigned short *dist, int pitch, unsigned short *phase, int W, int H, int lg,
-                             hipStream_t st) {
-  if (!dist_phase_ok(W, H, lg) || pitch % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_dist_phase, dim3(H), dim3(256), 0, st, dist, pitch, phase, W, H, lg, ilog2(W), ilog2(H));
-  return hipGetLastError();
-}
 
 hipError_t launch_dist_pack(const unsigned short *dist, int pitch, uint4 *packed, int W, int H, hipStream_t st) {
   const int ppr = pack_per_row(W);

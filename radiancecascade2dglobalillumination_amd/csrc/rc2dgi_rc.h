@@ -33,9 +33,6 @@ struct RcParams {
   int cscr;             // the exit proof tests the screen edge too
   int tailk;            // tail compaction after this many lockstep iterations (0: off)
   int wgp;              // workgroup-wide exit proof of the first samples
-  const unsigned short *dph;  // phase-plane copy of distRT for this level (k_dist_phase), nullptr: off
-  int phm;                    // 1: the first lockstep sample reads dph, 2: every lockstep sample
-  int phcw, phch;             // log2 of the columns / rows per phase plane (log2(W) - level, log2(H) - level)
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
@@ -308,6 +305,9 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
   }
 }
 
+#ifndef RC2DGI_FARVOTE
+#define RC2DGI_FARVOTE 1  // k_rc_level: top-level workgroups without a ray on screen skip the table (A/B: 0, 2)
+#endif
 #ifndef RC2DGI_EARLY_UPPER
 #define RC2DGI_EARLY_UPPER 1  // k_rc_level: upper-cascade samples before the hit records arrive (A/B: -D...=0)
 #endif
@@ -383,7 +383,14 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // miss proof goes to the queue at once (no lockstep iterations).
   __shared__ uint2 s_q[TLC ? NT * NR : 1];
   __shared__ unsigned s_qn;
-  const bool tl = TLC && P.tailk != 0;
+  bool tl = TLC && P.tailk != 0;  // (cleared with the whole workgroup when no ray starts on screen: FV)
+  // Far-interval vote (FV, the top level's one-probe tiles at t0 >= 1/4): after the far-interval test below,
+  // a workgroup none of whose rays starts on screen skips the bound table, its barrier and the tail queue
+  // (every barrier it skips, all its waves skip: the vote is workgroup-wide).  FV 2 also issues the table's
+  // load only after the vote.
+  constexpr int FV = (TLC && TOP) ? RC2DGI_FARVOTE : 0;
+  const bool fv = FV > 0 && P.t0 >= 0.25f;
+  __shared__ unsigned s_vote[FV ? NT / 64 : 1];
 #ifdef RC2DGI_DIAG_LDS_PAD  // diagnostic build: one workgroup per CU (LDS-limited residency)
   __shared__ unsigned s_pad[RC2DGI_DIAG_LDS_PAD];
   if (P.level == 99) s_pad[threadIdx.x] = 0u;
@@ -419,11 +426,12 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr int CM4 = CMN * (int)sizeof(CminT) / 16;  // 16-byte pieces of the table
   constexpr int CPT = CMS ? (CM4 + NT - 1) / NT : 1;  // per thread
   float4 cmv[CPT];
-  if (cm || dp) {
+  auto load_table = [&]() {
 #pragma unroll
     for (int j = 0; j < CPT; ++j)
       if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4) cmv[j] = ctab[threadIdx.x + j * NT];
-  }
+  };
+  if ((cm || dp) && !(FV == 2 && fv)) load_table();
 
   const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
   const int cx = cx0 + (int)(threadIdx.x % TX);
@@ -546,10 +554,27 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       }
     }
   }
+  bool skip = false;  // FV: no ray of the workgroup takes a sample
+  if (FV && fv) {
+    bool mine = false;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) mine |= t[k] < kDone;
+    const unsigned long long b = __ballot(mine);
+    if (lane == 0) s_vote[wv] = b != 0ull ? 1u : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    unsigned any = 0;
+#pragma unroll
+    for (int w = 0; w < (FV ? NT / 64 : 1); ++w) any |= s_vote[w];
+    skip = any == 0u;
+    if (FV == 2 && !skip && (cm || dp)) load_table();
+  }
+  tl = tl && !skip;
   // The bound table to LDS and the workgroup barrier, as late as their first use: the table's load was
   // issued first (vmcnt retires in order, so this waits for it only, not for the staging loads in
   // flight over the march), and its latency overlaps the ray setup above.
-  if (cm || dp || tl) {
+  if ((cm || dp || tl) && !skip) {
     if (cm || dp) {
 #pragma unroll
       for (int j = 0; j < CPT; ++j)
@@ -669,13 +694,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   const int itend = tl ? max(0, min(P.tailk, RC2DGI_DIAG_MAX_ITERS)) : RC2DGI_DIAG_MAX_ITERS;
   RC_SECTION("march");
   RC_TSTAMP(4);
-  // Phase-plane samples (P.dph, k_dist_phase): the probes of a level are 2^L texels apart, so at one t the
-  // lanes of a wave sample texels 2^L apart -- each its own 128-byte line in distRT, consecutive texels of one
-  // row of the copy, where texel (x, y) sits at column (x mod 2^L) W/2^L + x div 2^L of row
-  // (y mod 2^L) H/2^L + y div 2^L.  The lockstep march's first sample (every ray at its t0) reads the copy
-  // (phm 1), or every lockstep sample does (phm 2); the same q either way.
-  constexpr bool PHC = BOFF && P2S && TLC;
-  const bool phon = PHC && P.dph != nullptr;
   // BOFF with P2S: floor(p * 2W) & (2W - 2) = 2 (floor(p W) & (W - 1)) (p W and p 2W are exact)
   const float sWx = (BOFF && P2S) ? 2.0f * P.sWf : P.sWf;
   const int wmask = (BOFF && P2S) ? 2 * P.s.W - 2 : P.s.W - 1;
@@ -780,16 +798,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         for (int k = 0; k < NR; ++k)
           if (ek[k]) q[k] = ld_dist_esc(dist, (unsigned)idx[k] << 1);
       }
-    } else if (PHC && phon && (P.phm == 2 || it == it0)) {
-      const unsigned pm = (1u << P.level) - 1u;
-#pragma unroll
-      for (int k = 0; k < NR; ++k) {  // the same texels in the phase-plane copy (dead rays: texel 0)
-        const unsigned col = (unsigned)cix[k] >> 1, row = (unsigned)ciy[k];
-        const unsigned xo = ((col & pm) << P.phcw) | (col >> P.level), yo = ((row & pm) << P.phch) | (row >> P.level);
-        const unsigned off = __umul24(yo, (unsigned)(2 * P.s.pitch)) + 2u * xo;
-        q[k] = ld_dist(P.dph, live[k] ? off : 0u);
-      }
-      if constexpr (NR == 4) asm volatile("" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]));
     } else {
 #pragma unroll
       for (int k = 0; k < NR; ++k)  // dead rays re-read texel 0 (one cached line); 32-bit byte offsets
@@ -1117,16 +1125,11 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   if (P.cmin && P.cscr && !P.dexit) return hipErrorInvalidValue;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
-  P.dph = (a.dist_phase && a.phase_mode > 0 && p2s && dist_phase_ok(P.s.W, P.s.H, a.level)) ? a.dist_phase : nullptr;
-  P.phm = a.phase_mode;
   // palettes: the plain field's march (DL 0) on power-of-two screens whose byte offsets fit 27 bits
   P.cpal = (a.cell_pal && DL == 0 && p2s && (size_t)P.s.pitch * P.s.H <= ((size_t)1 << 26)) ? a.cell_pal : nullptr;
   P.lgw = 0;
   while ((1 << P.lgw) < P.s.pitch) ++P.lgw;
   if (P.cpal && (1 << P.lgw) != P.s.pitch) P.cpal = nullptr;
-  P.phcw = P.phch = 0;
-  while ((1 << (P.phcw + a.level)) < P.s.W) ++P.phcw;
-  while ((1 << (P.phch + a.level)) < P.s.H) ++P.phch;
 #define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \
   hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL >= 2 ? 0 : DL)), GI, Z0V>), \
                      dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),   \

@@ -7,5 +7,5 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_co
   --timeout-method thread -m gpu -k "surface_palettes or every_rc_variant or committed_bench or storage_schedule or c1_app" \
   > gpurun_out/r04/t5.log 2>&1 || { tail -30 gpurun_out/r04/t5.log; exit 1; }
 tail -2 gpurun_out/r04/t5.log
-LIBS="build/ab/librc2dgi_noearly.so radiancecascade2dglobalillumination_amd/librc2dgi.so" ROUNDS=3 bash scripts/ab_lib.sh || exit 1
+LIBS="build/ab/librc2dgi_noearly.so build/ab/librc2dgi_fv0.so build/ab/librc2dgi_fv2.so radiancecascade2dglobalillumination_amd/librc2dgi.so" ROUNDS=3 bash scripts/ab_lib.sh || exit 1
 BENCH_ARGS="--size 1200 --height 900" CFGS="base rc_skip=2 rc_skip=3" ROUNDS=2 bash scripts/ab_knobs.sh || exit 1

@@ -55,9 +55,6 @@ def apply_schedule(ctx, sched, N, shards=1):
     for L in range(N):
         ctx.set_tuning(f"rc_order_L{L}", (sub.get("rc_order") or sched["rc_order"])[L])
         ctx.set_tuning(f"rc_variant_L{L}", (sub.get("rc_variant") or sched["rc_variant"])[L])
-        ph = sub.get("rc_phase") or sched.get("rc_phase")
-        if ph:
-            ctx.set_tuning(f"rc_phase_L{L}", ph[L])
     for k, v in {**sched.get("knobs", {}), **sub.get("knobs", {})}.items():
         ctx.set_tuning(k, int(v))
 

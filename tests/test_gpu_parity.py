@@ -391,35 +391,6 @@ def test_every_rc_variant_is_bit_identical(RC2DGI, W, H, N, rr, scene, storage):
     ctx.close()
 
 
-@pytest.mark.parametrize("W,H,N,rr,scene", [(256, 128, 5, 2.0, "rand:41"), (512, 512, 6, 2.0, "demo"),
-                                            (1024, 256, 6, 8.0, "rand:42")])
-@pytest.mark.parametrize("storage", ["f32", "f16"])
-def test_phase_plane_samples_are_bit_identical(RC2DGI, W, H, N, rr, scene, storage):
-    """rc_phase_L<n> (the lockstep march reads the level's phase-plane copy of distRT, k_dist_phase) on every
-    level of every one-probe tile variant, first sample only (1) and every lockstep sample (2): the same
-    texels, so the same bits; the levels whose tiles are not one-probe ignore it."""
-    color, emis = make_scene(scene, W, H)
-    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr, **mode_params(storage)), color, emis,
-                      keep_levels=True)
-    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr, storage=storage)
-    ctx.set_keep_levels(True)
-    ctx.upload("color", color)
-    ctx.upload("emissive", emis)
-    for mode in (1, 2):
-        ctx.set_tuning("rc_phase", mode)
-        assert ctx.get_tuning(f"rc_phase_L{N - 1}") == mode
-        for v in (0, 6, 13, 20) if storage == "f32" else (0, 13):
-            ctx.set_tuning("rc_variant", v)
-            ctx.do_rc2dgi()
-            ctx.sync()
-            for L in range(N):
-                g = ctx.download_level(L)
-                assert np.array_equal(g, fr.gi_levels[L]), \
-                    f"rc_phase {mode} variant {v} level {L}: {np.count_nonzero(g != fr.gi_levels[L])}"
-    assert np.array_equal(ctx.download("color"), fr.color_out)
-    ctx.close()
-
-
 def speckled_scene(W, H, seed=7):
     """The demo scene with every occluder and emitter texel given its own random k/255 colour: far more
     than kCellPal distinct hit records per bound-table cell (the palettes overflow, hits read shade)."""
