@@ -187,6 +187,15 @@ int rc2dgi_get_tuning(rc2dgi_ctx *ctx, const char *key, int *value);
  * as stored by its pass (costs N extra cascade textures and one copy per level). */
 int rc2dgi_set_keep_levels(rc2dgi_ctx *ctx, int enable);
 int rc2dgi_download_level(rc2dgi_ctx *ctx, int level, void *host, int pitch_bytes, int format);
+/* the march's side tables of the last frame (no reference counterpart; for checking them): which =
+ * RC2DGI_TAB_HITC (64 x 64 bytes: 1 where a cell holds a texel the hit test passes), _CMIN (64 x 64 bytes,
+ * lower bounds k / 512), _DCLR (64 bins x 64 x 64 bytes, clear steps), _DBOXES (64 bins x 64 steps x 4 ints),
+ * _CELLPAL (64 x 64 cells x 16 float4 palette entries), _MFIELD (H rows x W uint16, the march field).
+ * Copies min(bytes, table size) bytes; returns the table size in bytes (or a negative status; a table not
+ * built by the last frame is RC2DGI_E_STATE). */
+enum { RC2DGI_TAB_HITC = 0, RC2DGI_TAB_CMIN = 1, RC2DGI_TAB_DCLR = 2, RC2DGI_TAB_DBOXES = 3, RC2DGI_TAB_CELLPAL = 4,
+       RC2DGI_TAB_MFIELD = 5 };
+int rc2dgi_download_table(rc2dgi_ctx *ctx, int which, void *host, int bytes);
 
 /* ---- on-device scene producer: the painted inputs without a host upload.
  * rc2dgi_paint(ctx, COLOR | EMISSIVE, clear, prims, n) is

@@ -1283,6 +1283,28 @@ int rc2dgi_device_buffer(rc2dgi_ctx *c, int which, void **dev, int *pitch_bytes)
   return RC2DGI_OK;
 }
 
+int rc2dgi_download_table(rc2dgi_ctx *c, int which, void *host, int bytes) {
+  if (!c || bytes < 0 || (bytes > 0 && !host)) return RC2DGI_E_ARG;
+  RC2DGI_USABLE(c);
+  const void *src = nullptr;
+  size_t n = 0;
+  const size_t cells = (size_t)kCminDim * kCminDim;
+  switch (which) {
+    case RC2DGI_TAB_HITC: src = c->hitc; n = cells; break;
+    case RC2DGI_TAB_CMIN: src = c->cmin; n = cells * sizeof(CminT); break;
+    case RC2DGI_TAB_DCLR: src = c->dclr; n = (size_t)kDirBins * cells; break;
+    case RC2DGI_TAB_DBOXES: src = c->dboxes; n = (size_t)kDirBins * kCminDim * sizeof(int4); break;
+    case RC2DGI_TAB_CELLPAL: src = c->cell_pal; n = cells * kCellPalStride * sizeof(float4); break;
+    case RC2DGI_TAB_MFIELD: src = c->mfield; n = (size_t)c->sd.pitch * c->H * sizeof(unsigned short); break;
+    default: return fail(c, RC2DGI_E_ARG, "bad table id");
+  }
+  if (!src) return fail(c, RC2DGI_E_STATE, "table not built");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (bytes > 0) HIPCHK(c, hipMemcpy(host, src, std::min(n, (size_t)bytes), hipMemcpyDeviceToHost));
+  return (int)std::min(n, (size_t)0x7FFFFFFF);
+}
+
 int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
                       int n) {
   if (tiles_x <= 0 || tiles_y <= 0 || tile_w <= 0 || tile_h <= 0 || ngrp <= 0 || n < 0 ||

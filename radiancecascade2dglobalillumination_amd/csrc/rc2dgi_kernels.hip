@@ -736,18 +736,26 @@ __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restri
   // nothing is reached
   const unsigned long long voff = __ballot(ly0 > ly1);
   const int nsteps = voff ? (int)__builtin_ctzll(voff) : NS;
-  // per cell of the row (wave-uniform loop), every step at once, one lane each: the first step whose box
-  // meets a hit cell, unless the box has left the grid sideways (so have the later steps) or vertically first
+  // Lane s, for every cell cx of the row at once (bit cx): hm -- the box [cx + bl.x, cx + bl.y] meets a hit
+  // column of orow (orow dilated by the box's column offsets), om -- the box lies wholly off the grid
+  // sideways.  Then per cell (wave-uniform loop), every step at once: the first step whose box meets a hit
+  // cell, unless the box has left the grid sideways (so have the later steps) or vertically first.
+  unsigned long long hm = 0, om = 0;
+  for (int d = bl.x; d <= bl.y; ++d)
+    hm |= d >= 0 ? (d < 64 ? orow >> d : 0ull) : (d > -64 ? orow << -d : 0ull);
+  // off: cx + bl.y < 0 or cx + bl.x > 63
+  const int lo = -bl.y, hi = D - 1 - bl.x;  // on-grid cells: lo <= cx <= hi
+  if (lo > D - 1 || hi < 0 || lo > hi) {
+    om = ~0ull;
+  } else {
+    const int a = max(0, lo), b = min(D - 1, hi);
+    const unsigned long long on = (b - a == 63 ? ~0ull : ((1ull << (b - a + 1)) - 1ull)) << a;
+    om = ~on;
+  }
+  hm &= ~om;
   int clear = 255;
   for (int cx = 0; cx < D; ++cx) {
-    const int x0 = max(0, cx + bl.x), x1 = min(D - 1, cx + bl.y);
-    const bool off = x0 > x1;
-    bool hit = false;
-    if (!off) {
-      const unsigned long long mask = (x1 - x0 == 63 ? ~0ull : ((1ull << (x1 - x0 + 1)) - 1ull)) << x0;
-      hit = (orow & mask) != 0;
-    }
-    const unsigned long long hb = __ballot(hit), ob = __ballot(off);
+    const unsigned long long hb = __ballot((hm >> cx) & 1ull), ob = __ballot((om >> cx) & 1ull);
     const int first_hit = hb ? (int)__builtin_ctzll(hb) : NS;
     const int first_off = min(nsteps, ob ? (int)__builtin_ctzll(ob) : NS);
     if (lane == cx) clear = first_hit < first_off ? first_hit : 255;

@@ -305,6 +305,12 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
   }
 }
 
+#ifndef RC2DGI_TABLE_WINDOW
+#define RC2DGI_TABLE_WINDOW 1  // k_rc_level: load only the bound-table cells a workgroup's rays can reach (A/B: 0)
+#endif
+#ifndef RC2DGI_EARLY_REC
+#define RC2DGI_EARLY_REC 0  // k_rc_level: palette records of the lockstep-finished rays before the staging writes
+#endif
 #ifndef RC2DGI_FARVOTE
 #define RC2DGI_FARVOTE 1  // k_rc_level: top-level workgroups without a ray on screen skip the table (A/B: 0, 2)
 #endif
@@ -426,14 +432,42 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr int CM4 = CMN * (int)sizeof(CminT) / 16;  // 16-byte pieces of the table
   constexpr int CPT = CMS ? (CM4 + NT - 1) / NT : 1;  // per thread
   float4 cmv[CPT];
+  const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
+  // Table window (RC2DGI_TABLE_WINDOW): only the cells the workgroup's rays can sample are loaded (into their
+  // own places of the LDS table; the other entries are never read by a live sample).  A ray moves at most t1
+  // (uv) along each axis from its probe, so its samples lie in the tile's probe box grown by t1, plus two
+  // texels for the approximate float arithmetic here; a window reaching the last column / row also takes
+  // column / row 0 (a sample at u = 1 reads texel 0: REPEAT), here by starting the window at 0.  16-byte
+  // pieces of 16 cells, kCminDim / 16 per row.  L1 / L2 load a few pieces instead of all 256.
+  constexpr int PPR = kCminDim / 16;
+  int wr0 = 0, wp0 = 0, wnp = PPR, wnpc = CM4;  // first row, first piece, pieces per row, pieces
+  if (RC2DGI_TABLE_WINDOW && (cm || dp)) {
+    const float bx0 = ((((float)cx0 + 0.5f) * (float)P.bsc) * P.invCRx - P.t1) * P.sWf - 2.0f;
+    const float bx1 = ((((float)(cx0 + TX) - 0.5f) * (float)P.bsc) * P.invCRx + P.t1) * P.sWf + 2.0f;
+    const float by0 = ((((float)cy0 + 0.5f) * (float)P.bsc) * P.invCRy - P.t1) * P.sHf - 2.0f;
+    const float by1 = ((((float)(cy0 + THY) - 0.5f) * (float)P.bsc) * P.invCRy + P.t1) * P.sHf + 2.0f;
+    const bool wx = bx1 >= P.sWf - 1.0f, wy = by1 >= P.sHf - 1.0f;  // reaches the last column / row
+    const int c0 = wx ? 0 : max(0, (int)bx0) >> P.csh, c1 = min(kCminDim - 1, (int)fminf(bx1, P.sWf - 1.0f) >> P.csh);
+    const int r0 = wy ? 0 : max(0, (int)by0) >> P.csh, r1 = min(kCminDim - 1, (int)fminf(by1, P.sHf - 1.0f) >> P.csh);
+    wr0 = __builtin_amdgcn_readfirstlane(r0);
+    wp0 = __builtin_amdgcn_readfirstlane(c0 >> 4);
+    wnp = __builtin_amdgcn_readfirstlane((c1 >> 4) - (c0 >> 4) + 1);
+    wnpc = __builtin_amdgcn_readfirstlane(r1 - r0 + 1) * wnp;
+  }
+  int pidx[CPT];  // piece of the table this thread moves, -1: none
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int e = (int)threadIdx.x + j * NT;
+    const int rr = e / wnp;
+    pidx[j] = e < wnpc ? (wr0 + rr) * PPR + wp0 + (e - rr * wnp) : -1;
+  }
   auto load_table = [&]() {
 #pragma unroll
     for (int j = 0; j < CPT; ++j)
-      if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4) cmv[j] = ctab[threadIdx.x + j * NT];
+      if (pidx[j] >= 0) cmv[j] = ctab[pidx[j]];
   };
   if ((cm || dp) && !(FV == 2 && fv)) load_table();
 
-  const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
   const int cx = cx0 + (int)(threadIdx.x % TX);
   const int cyb = cy0 + (int)(threadIdx.x / TX);
   const bool xok = cx < P.bdx;
@@ -578,8 +612,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     if (cm || dp) {
 #pragma unroll
       for (int j = 0; j < CPT; ++j)
-        if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4)
-          reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
+        if (pidx[j] >= 0) reinterpret_cast<float4 *>(s_cm)[pidx[j]] = cmv[j];
     }
 #ifdef RC2DGI_DIAG_TIMING
     if (cm || dp)  // (diagnostic: the table's words have arrived -- not the staging loads behind them)
@@ -918,11 +951,19 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // that the round trip overlaps the staging's LDS writes and the barrier (L0 0.126 -> 0.123 ms); in the
   // one-probe tiles the same placement cost L4 / L5 3-6 us (the loads join the queue behind the march's
   // gathers), so they load at the merge (profiles/r03/ab/late_loads.txt).
+  // (RC2DGI_EARLY_REC, A/B: the one-probe tiles with palettes load the records of the rays that ended in the
+  // lockstep march here too; the rays finished in the tail load theirs at the merge)
+  constexpr bool EREC = RC2DGI_EARLY_REC && PALC;
+  bool recd[EREC ? NR : 1];
   float4 hr[NR];
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
     hr[k] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
     if (!TLC && hit_idx[k] >= 0) hr[k] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
+    if constexpr (EREC) {
+      recd[k] = P.cpal && !(tl && t[k] < kDone);
+      if (recd[k] && hit_idx[k] >= 0) hr[k] = hit_record(shade, P.cpal, hit_idx[k], P.lgw, P.csh);
+    }
   }
   RC_TSTAMP(6);
   RC_SECTION("stage_write");
@@ -956,7 +997,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #ifdef RC2DGI_DIAG_NOHIT  // timing-only ablation build: no hit-record loads (WRONG results)
       if (hit_idx[k] >= 0) hr[k] = make_float4(0.5f, 0.5f, 0.5f, 1.0f);
 #else
-      if (hit_idx[k] >= 0) hr[k] = PALC ? hit_record(shade, P.cpal, hit_idx[k], P.lgw, P.csh) : shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
+      if (hit_idx[k] >= 0 && !(EREC && recd[EREC ? k : 0]))
+        hr[k] = PALC ? hit_record(shade, P.cpal, hit_idx[k], P.lgw, P.csh) : shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
 #endif
   }
 

@@ -112,6 +112,7 @@ def load_library(path: Optional[str] = None):
                                      ctypes.c_int),
         "rc2dgi_plan_jfa_window": ([ctypes.POINTER(_Config), ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ip],
                                    ctypes.c_int),
+        "rc2dgi_download_table": ([vp, ctypes.c_int, vp, ctypes.c_int], ctypes.c_int),
         "rc2dgi_plan_group_waits": ([ctypes.POINTER(_Config), ctypes.c_int, ctypes.c_int, ctypes.c_int, ip,
                                      ctypes.c_int], ctypes.c_int),
     }
@@ -325,6 +326,22 @@ class RC2DGI:
         self._check(self._L.rc2dgi_download_level(self._h, level, out.ctypes.data_as(ctypes.c_void_p), cw * 16,
                                                   FMT_RGBA32F), f"download_level {level}")
         return out
+
+    TABLES = {"hitc": (0, np.uint8), "cmin": (1, np.uint8), "dclr": (2, np.uint8), "dboxes": (3, np.int32),
+              "cellpal": (4, np.float32), "mfield": (5, np.uint16)}
+
+    def download_table(self, name: str) -> np.ndarray:
+        """The march's side tables of the last frame (rc2dgi_download_table): hitc / cmin (64, 64), dclr
+        (64 bins, 64, 64), dboxes (64 bins, 64 steps, 4), cellpal (64, 64, 16, 4), mfield (H, pitch)."""
+        which, dt = self.TABLES[name]
+        n = self._L.rc2dgi_download_table(self._h, which, None, 0)
+        self._check(n if n < 0 else 0, f"download_table {name}")
+        out = np.empty(n // np.dtype(dt).itemsize, dt)
+        self._check(min(0, self._L.rc2dgi_download_table(self._h, which, out.ctypes.data_as(ctypes.c_void_p), n)),
+                    f"download_table {name}")
+        shapes = {"hitc": (64, 64), "cmin": (64, 64), "dclr": (64, 64, 64), "dboxes": (64, 64, 4),
+                  "cellpal": (64, 64, 16, 4), "mfield": (self.screen_height, -1)}
+        return out.reshape(shapes[name])
 
     # ---------------------------------------------------------------- the pass chain
     def do_rc2dgi(self) -> None:

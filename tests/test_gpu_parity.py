@@ -717,3 +717,83 @@ def test_miss_proofs_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene, storage):
                 assert np.array_equal(g, fr.gi_levels[L]), \
                     f"variant {v} tail {tail} level {L}: {np.count_nonzero(np.any(g != fr.gi_levels[L], axis=-1))} differ"
     ctx.close()
+
+
+def dir_clear_cpu(hitc, boxes):
+    """k_dir_clear restated (rc2dgi_kernels.hip): per angular bin j and cell (cy, cx) of the 64 x 64 grid, the
+    first step s whose box (boxes[j, s] = x0, x1, y0, y1 cell offsets, clipped to the grid) holds a hit cell,
+    if that comes before the first step whose box leaves the grid (vertically: the row's first such step;
+    sideways: the cell's), else 255."""
+    D = hitc.shape[0]
+    P = np.zeros((D + 1, D + 1), np.int64)
+    P[1:, 1:] = hitc.astype(np.int64).cumsum(0).cumsum(1)
+    out = np.full((boxes.shape[0], D, D), 255, np.uint8)
+    cx = np.arange(D)[:, None]
+    for j in range(boxes.shape[0]):
+        B = boxes[j].astype(np.int64)
+        x0 = np.maximum(0, cx + B[None, :, 0])
+        x1 = np.minimum(D - 1, cx + B[None, :, 1])
+        xoff = x0 > x1  # (cells, steps)
+        for cy in range(D):
+            ly0 = np.maximum(0, cy + B[:, 2])
+            ly1 = np.minimum(D - 1, cy + B[:, 3])
+            voff = ly0 > ly1
+            nsteps = int(np.argmax(voff)) if voff.any() else B.shape[0]
+            a0, a1 = np.minimum(ly0, D - 1), np.maximum(ly1, 0)
+            c0, c1 = np.clip(x0, 0, D - 1), np.clip(x1, 0, D - 1)
+            s = (P[a1[None, :] + 1, c1 + 1] - P[a0[None, :], c1 + 1] - P[a1[None, :] + 1, c0] + P[a0[None, :], c0])
+            hit = (s > 0) & ~xoff & ~voff[None, :]
+            first_hit = np.where(hit.any(1), hit.argmax(1), B.shape[0])
+            first_off = np.minimum(nsteps, np.where(xoff.any(1), xoff.argmax(1), B.shape[0]))
+            out[j, cy] = np.where(first_hit < first_off, first_hit, 255)
+    return out
+
+
+@pytest.mark.parametrize("scene", ["demo", "speckled"])
+def test_side_tables_match_their_restatement(RC2DGI, scene):
+    """The march's side tables of a 4096^2 frame against CPU restatements from the frame's own distRT and
+    inputs: the hit-cell flags and bound table (k_shade_cmin: REPEAT-wrap texels in the last cell row /
+    column), the directional clear steps (k_dir_clear, on the downloaded hit flags and the host's step boxes),
+    and the surface palettes: the march field equals distRT wherever the hit test fails, holds a palette entry
+    (or 15: none) where it passes, and every entry used holds exactly that texel's record (emission with alpha
+    1, else albedo with _Reflectivity)."""
+    W = H = 4096
+    color, emis = speckled_scene(W, H) if scene == "speckled" else make_scene(scene, W, H)
+    ctx = RC2DGI(W, H, cascade_count=6, ray_range=2.0)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    assert ctx.get_tuning("rc_pal") == 1
+    ctx.do_rc2dgi()
+    ctx.sync()
+    d = ctx.download("dist")  # RGBA: R, G = the bytes of q (packUNorm16)
+    q = (np.rint(d[..., 0] * 255).astype(np.uint32) << 8) | np.rint(d[..., 1] * 255).astype(np.uint32)
+    hittable = q <= 65  # decode_dist(q) < 0.001 (exhaustive: tests/test_kernels_cpu.py)
+    C = W // 64
+    qe = np.concatenate([q, q[:, :1]], 1)
+    qe = np.concatenate([qe, qe[:1, :]], 0)  # REPEAT wrap onto column / row 0
+    cmin_q = np.full((64, 64), 0xFFFF, np.uint32)
+    for cy in range(64):
+        for cx in range(64):
+            y1 = (cy + 1) * C + (1 if cy == 63 else 0)
+            x1 = (cx + 1) * C + (1 if cx == 63 else 0)
+            cmin_q[cy, cx] = qe[cy * C:y1, cx * C:x1].min()
+    hitc = (cmin_q <= 65).astype(np.uint8)
+    assert np.array_equal(ctx.download_table("hitc"), hitc)
+    dmin = (cmin_q.astype(np.float64) / 65535).astype(np.float32)
+    want_cmin = np.where(cmin_q <= 65, 0, np.minimum(np.floor(dmin * np.float32(512)), 255)).astype(np.uint8)
+    assert np.array_equal(ctx.download_table("cmin"), want_cmin)
+    assert np.array_equal(ctx.download_table("dclr"), dir_clear_cpu(hitc, ctx.download_table("dboxes")))
+    m = ctx.download_table("mfield")[:, :W].astype(np.uint32)
+    assert np.array_equal(m[~hittable], q[~hittable])
+    assert m[hittable].max(initial=0) <= 15
+    e, c = emis[..., :3], color[..., :3]
+    lit = np.sqrt(e[..., 0] * e[..., 0] + e[..., 1] * e[..., 1] + e[..., 2] * e[..., 2]) > 0
+    rec = np.where(lit[..., None], np.concatenate([e, np.ones_like(e[..., :1])], -1),
+                   np.concatenate([c, np.zeros_like(c[..., :1])], -1))  # _Reflectivity 0
+    pal = ctx.download_table("cellpal")
+    ys, xs = np.nonzero(hittable & (m < 15))
+    got = pal[ys // C, xs // C, m[ys, xs]]
+    assert np.array_equal(got.view(np.uint32), rec[ys, xs].view(np.uint32))
+    if scene == "speckled":
+        assert np.count_nonzero(hittable & (m == 15)) > 0  # palettes overflowed: those hits read shade
+    ctx.close()
