@@ -36,6 +36,7 @@ struct RcParams {
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
+  int tpoison;                // the bound table's entries outside the loaded window set to 255 (tests)
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   unsigned long long *stats;  // diagnostic builds: [16 levels][16] counters (rc2dgi_diag_stats)
 #endif
@@ -434,18 +435,36 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   float4 cmv[CPT];
   const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
   // Table window (RC2DGI_TABLE_WINDOW): only the cells the workgroup's rays can sample are loaded (into their
-  // own places of the LDS table; the other entries are never read by a live sample).  A ray moves at most t1
-  // (uv) along each axis from its probe, so its samples lie in the tile's probe box grown by t1, plus two
-  // texels for the approximate float arithmetic here; a window reaching the last column / row also takes
-  // column / row 0 (a sample at u = 1 reads texel 0: REPEAT), here by starting the window at 0.  16-byte
-  // pieces of 16 cells, kCminDim / 16 per row.  L1 / L2 load a few pieces instead of all 256.
+  // own places of the LDS table; the other entries are never read by a live sample): the bounding box of the
+  // rays' segments from the tile's probes, plus two texels for the approximate float arithmetic here; a
+  // window reaching the last column / row also takes column / row 0 (a sample at u = 1 reads texel 0:
+  // REPEAT), here by starting the window at 0.  16-byte pieces of 16 cells, kCminDim / 16 per row.  L1 / L2
+  // load a few pieces instead of all 256, L4 a wedge of its direction bin's table.
   constexpr int PPR = kCminDim / 16;
   int wr0 = 0, wp0 = 0, wnp = PPR, wnpc = CM4;  // first row, first piece, pieces per row, pieces
   if (RC2DGI_TABLE_WINDOW && (cm || dp)) {
-    const float bx0 = ((((float)cx0 + 0.5f) * (float)P.bsc) * P.invCRx - P.t1) * P.sWf - 2.0f;
-    const float bx1 = ((((float)(cx0 + TX) - 0.5f) * (float)P.bsc) * P.invCRx + P.t1) * P.sWf + 2.0f;
-    const float by0 = ((((float)cy0 + 0.5f) * (float)P.bsc) * P.invCRy - P.t1) * P.sHf - 2.0f;
-    const float by1 = ((((float)(cy0 + THY) - 0.5f) * (float)P.bsc) * P.invCRy + P.t1) * P.sHf + 2.0f;
+    // the rays are straight: sample positions lie in the probe box moved by t (dx aspy, dy aspx), t in
+    // [t0, t1], over the workgroup's ND directions (wave-uniform scalar loads)
+    float dx0 = 0.0f, dx1 = 0.0f, dy0 = 0.0f, dy1 = 0.0f;
+#pragma unroll
+    for (int r = 0; r < ND; ++r) {
+      const float2 d = ld_uniform(dirs + bi0 * 4 + r);
+      const float ax = d.x * P.aspy, ay = d.y * P.aspx;
+      dx0 = fminf(dx0, fminf(ax * P.t0, ax * P.t1));
+      dx1 = fmaxf(dx1, fmaxf(ax * P.t0, ax * P.t1));
+      dy0 = fminf(dy0, fminf(ay * P.t0, ay * P.t1));
+      dy1 = fmaxf(dy1, fmaxf(ay * P.t0, ay * P.t1));
+    }
+    if (!Z0 && !TLC) {  // the workgroup-wide proof (WGC below) reads the probe box grown by t0 on all sides
+      dx0 = fminf(dx0, -P.t0);
+      dx1 = fmaxf(dx1, P.t0);
+      dy0 = fminf(dy0, -P.t0);
+      dy1 = fmaxf(dy1, P.t0);
+    }
+    const float bx0 = ((((float)cx0 + 0.5f) * (float)P.bsc) * P.invCRx + dx0) * P.sWf - 2.0f;
+    const float bx1 = ((((float)(cx0 + TX) - 0.5f) * (float)P.bsc) * P.invCRx + dx1) * P.sWf + 2.0f;
+    const float by0 = ((((float)cy0 + 0.5f) * (float)P.bsc) * P.invCRy + dy0) * P.sHf - 2.0f;
+    const float by1 = ((((float)(cy0 + THY) - 0.5f) * (float)P.bsc) * P.invCRy + dy1) * P.sHf + 2.0f;
     const bool wx = bx1 >= P.sWf - 1.0f, wy = by1 >= P.sHf - 1.0f;  // reaches the last column / row
     const int c0 = wx ? 0 : max(0, (int)bx0) >> P.csh, c1 = min(kCminDim - 1, (int)fminf(bx1, P.sWf - 1.0f) >> P.csh);
     const int r0 = wy ? 0 : max(0, (int)by0) >> P.csh, r1 = min(kCminDim - 1, (int)fminf(by1, P.sHf - 1.0f) >> P.csh);
@@ -610,6 +629,16 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // flight over the march), and its latency overlaps the ray setup above.
   if ((cm || dp || tl) && !skip) {
     if (cm || dp) {
+      if (P.tpoison) {  // (tuning rc_table_poison, tests: every entry outside the window proves every sample)
+#pragma unroll
+        for (int j = 0; j < CPT; ++j)
+          if ((int)threadIdx.x + j * NT < CM4)
+            reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = make_float4(__uint_as_float(~0u), __uint_as_float(~0u),
+                                                                                __uint_as_float(~0u), __uint_as_float(~0u));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      }
 #pragma unroll
       for (int j = 0; j < CPT; ++j)
         if (pidx[j] >= 0) reinterpret_cast<float4 *>(s_cm)[pidx[j]] = cmv[j];
@@ -1167,6 +1196,7 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   if (P.cmin && P.cscr && !P.dexit) return hipErrorInvalidValue;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
+  P.tpoison = a.table_poison;
   // palettes: the plain field's march (DL 0) on power-of-two screens whose byte offsets fit 27 bits
   P.cpal = (a.cell_pal && DL == 0 && p2s && (size_t)P.s.pitch * P.s.H <= ((size_t)1 << 26)) ? a.cell_pal : nullptr;
   P.lgw = 0;
