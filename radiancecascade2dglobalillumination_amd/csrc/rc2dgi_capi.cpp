@@ -134,6 +134,7 @@ struct rc2dgi_ctx {
   std::vector<int> rc_tail;      // per level: tail compaction after this many lockstep iterations (tuning rc_tail_L<n>)
   int rc_wgproof = 1;            // tuning "rc_wgproof": workgroup-wide exit proof of the first samples
   std::vector<int> rc_mp;        // per level: directional miss proofs in the one-probe tiles (tuning rc_mp_L<n>)
+  std::vector<int> rc_noproof;   // per level: no bound table / exit proofs at this level (tuning rc_noproof_L<n>)
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   int jfa_coset = 1;             // tuning "jfa_coset": the first four steps in one kernel (k_jfa_coset) where they apply
@@ -380,6 +381,7 @@ int allocate(rc2dgi_ctx *c) {
   for (int L = 0; L < c->N; ++L) c->rc_order[L] = default_rc_order(L);
   c->rc_tail.assign(c->N, kDefaultTail);
   c->rc_mp.assign(c->N, 1);  // directional miss proofs wherever they apply (one-probe tiles, 4^L >= kDirBins)
+  c->rc_noproof.assign(c->N, 0);
   if (int rc = jfa_buffers(c)) return rc;
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
@@ -917,7 +919,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   // directional proofs on there and the level's direction table binnable (dp_ok)
   bool mps = false;
   for (int L = 0; L < c->N; ++L)
-    mps |= c->rc_mp[L] != 0 && (1 << (2 * L)) >= kDirBins && rc_variant_one_probe(c->rc_variant[L]) &&
+    mps |= c->rc_mp[L] != 0 && !c->rc_noproof[L] && (1 << (2 * L)) >= kDirBins && rc_variant_one_probe(c->rc_variant[L]) &&
            L < (int)c->dp_ok.size() && c->dp_ok[L];
   mps = mps && proofs;
   // surface records and the bound table in one pass over distRT where its cells are >= 64 texels; with the
@@ -963,8 +965,8 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.dist_tiled = c->dist_t;
     a.dist_packed = c->dist_p;
     a.dist_nib = c->dist_n;
-    a.cmin = proofs ? c->cmin : nullptr;
-    a.dclr = (mps && c->rc_mp[L] && L < (int)c->dp_ok.size() && c->dp_ok[L]) ? c->dclr : nullptr;
+    a.cmin = (proofs && !c->rc_noproof[L]) ? c->cmin : nullptr;
+    a.dclr = (mps && c->rc_mp[L] && !c->rc_noproof[L] && L < (int)c->dp_ok.size() && c->dp_ok[L]) ? c->dclr : nullptr;
     // the screen-edge test pays where rays are long (t1 >= 1/8 of the screen: L4 / L5 at N = 6)
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
@@ -1538,6 +1540,12 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_pal = value != 0;
     return RC2DGI_OK;
   }
+  if (k.rfind("rc_noproof_L", 0) == 0) {
+    const int L = std::atoi(k.c_str() + 12);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    c->rc_noproof[L] = value != 0;
+    return RC2DGI_OK;
+  }
   if (k.rfind("rc_order_L", 0) == 0) {
     const int L = std::atoi(k.c_str() + 10);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
@@ -1603,6 +1611,12 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "rc_pal") {
     *value = c->rc_pal;
+    return RC2DGI_OK;
+  }
+  if (k.rfind("rc_noproof_L", 0) == 0) {
+    const int L = std::atoi(k.c_str() + 12);
+    if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
+    *value = c->rc_noproof[L];
     return RC2DGI_OK;
   }
   if (k.rfind("rc_order_L", 0) == 0) {
