@@ -120,6 +120,8 @@ struct RcLevelArgs {
   int cmin_screen = 0;          // the exit proof also tests the screen edge (worth it for long rays)
   int tail_k = 0;               // tail compaction after this many lockstep march iterations (0: off)
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
+  int split = 0;                // split levels (k_rc_level SPL): 1 march only, 2 merge only (16x16x1 float4)
+  int4 *hitbuf = nullptr;       // their per-probe hits (4 ints per cascade texel)
 };
 
 int dist_cmin_shift(int W, int H);
