@@ -108,6 +108,8 @@ struct rc2dgi_ctx {
   // split levels (tuning rc_split, a bit per level): the level's march runs on a stream of its own as soon as
   // the side tables are built, its merge in level order on the frame stream (k_rc_level SPL)
   int rc_split = 0;
+  // levels 1 and 0 in one kernel (tuning rc_pair, launch_rc_pair10): G_1 is never written
+  int rc_pair = 0;
   std::vector<int4 *> hitbuf;           // per level: the march's hits, one int4 per cascade texel
   std::vector<hipStream_t> split_st;    // per level
   std::vector<hipEvent_t> split_ev;     // per level: end of its march; [N]: side tables built
@@ -982,6 +984,10 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     if (int rc = split_resources(c, split)) return rc;
     HIPCHK(c, hipEventRecord(c->split_ev[c->N], st));
   }
+  // levels 1 and 0 paired: whole frames of float4 power-of-two cascades (rc_pair_ok), neither level split
+  const bool pair = c->rc_pair && c->world == 1 && !(split & 3u) && rc_pair_ok(c->sd, c->cd, c->N) &&
+                    c->rc_noproof[0] == c->rc_noproof[1];
+  RcLevelArgs pair1;  // level 1's arguments, launched with level 0
   bool gi1final = false;
   for (int pass = split ? 0 : 1; pass < 2; ++pass)
   for (int L = c->N - 1; L >= 0; --L) {
@@ -1018,6 +1024,18 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
 
+    if (pair && L == 1) {  // (G_2 stays the upper: no buffer swap; G_1's level_bufs copy is not made)
+      pair1 = a;
+      continue;
+    }
+    if (pair && L == 0) {
+      HIPCHK(c, launch_rc_pair10(pair1, a, c->sd, c->cd, st));
+      if (c->keep_levels)
+        HIPCHK(c, hipMemcpyAsync(c->level_bufs[0], dstGI, (size_t)c->cd.pitch * c->CH * gi_bytes(c),
+                                 hipMemcpyDeviceToDevice, st));
+      gi1final = !gi1final;
+      continue;
+    }
     const bool spl = split >> L & 1;
     a.split = spl ? (pass == 0 ? 1 : 2) : 0;
     a.hitbuf = spl ? c->hitbuf[L] : nullptr;
@@ -1596,6 +1614,10 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_pal = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "rc_pair") {
+    c->rc_pair = value != 0;
+    return RC2DGI_OK;
+  }
   if (k == "rc_split") {
     if (value < 0 || value >= (1 << 16)) return fail(c, RC2DGI_E_ARG, "rc_split is a bit mask of levels");
     c->rc_split = value;
@@ -1672,6 +1694,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "rc_pal") {
     *value = c->rc_pal;
+    return RC2DGI_OK;
+  }
+  if (k == "rc_pair") {
+    *value = c->rc_pair;
     return RC2DGI_OK;
   }
   if (k == "rc_split") {

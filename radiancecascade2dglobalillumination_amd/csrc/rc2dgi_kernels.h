@@ -209,6 +209,11 @@ inline float rc_ray_end(int level, int N, float ray_range) {
 
 // one RadianceCascades.fs level
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);
+// levels 1 and 0 in one kernel (tuning rc_pair, k_rc_pair10): a1 = level 1 (its upper: G_2), a0 = level 0 (its
+// out: G_0); G_1 is never written.  Float4 cascades, power-of-two screens and cascades (CW >= 64, CH >= 32), N >= 3,
+// whole frames.  hipErrorInvalidValue (nothing launched) otherwise.
+bool rc_pair_ok(ScreenDims s, CascadeDims c, int N);
+hipError_t launch_rc_pair10(const RcLevelArgs &a1, const RcLevelArgs &a0, ScreenDims s, CascadeDims c, hipStream_t st);
 
 // Blur.fs into blur_out, then the default-shader blended copy-back into gi (RC2DGI.cs:367-387)
 hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st,

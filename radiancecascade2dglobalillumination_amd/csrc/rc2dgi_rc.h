@@ -1144,6 +1144,9 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   return hipGetLastError();
 }
 
+// the level's kernel parameters (everything but the tile-shape dependent fields launch_rc_tiles sets)
+RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c);
+
 // per translation unit dispatchers of the tile variants (rc2dgi_rc_*.hip)
 hipError_t launch_rc_f32_rolled(const RcLevelArgs &a, RcParams P, hipStream_t st);
 hipError_t launch_rc_f32_unrolled(const RcLevelArgs &a, RcParams P, hipStream_t st);
