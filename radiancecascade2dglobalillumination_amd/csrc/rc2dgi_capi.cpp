@@ -994,6 +994,10 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     if (pass == 0 && !(split >> L & 1)) continue;
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
     float4 *dstGI = gi1final ? c->gi2 : c->gi1;
+    // paired levels: G_2 goes to the spare texture, so that G_0 lands in the reference's finalGI (RC2DGI.cs:365)
+    // while the pair still reads G_2; the texture G_1 would occupy keeps its old contents (never read)
+    if (pair && L == 2) dstGI = c->gi_spare;
+    if (pair && L == 1) srcGI = c->gi_spare;
     if (pass == 1 && LT && L + 1 < c->N) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
     RcLevelArgs a;
     a.upper = (L == c->N - 1) ? nullptr : srcGI;
@@ -1024,8 +1028,9 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
 
-    if (pair && L == 1) {  // (G_2 stays the upper: no buffer swap; G_1's level_bufs copy is not made)
+    if (pair && L == 1) {  // (launched with level 0; G_1's level_bufs copy is not made)
       pair1 = a;
+      gi1final = !gi1final;
       continue;
     }
     if (pair && L == 0) {
