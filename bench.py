@@ -572,8 +572,6 @@ def main():
                    "parallelism": f"replicas{world}",
                    "rc_order": orders or "default", "rc_variant": variants,
                    "rc_pal": ctx.get_tuning("rc_pal"),
-                   "rc_split": ctx.get_tuning("rc_split"),
-                   "rc_pair": ctx.get_tuning("rc_pair"),
                    "rc_skip": ctx.get_tuning("rc_skip"),
                    "rc_schedule": (os.path.relpath(a.load_tuning, ROOT) if a.load_tuning else
                                    ("default" if a.no_autotune else "autotune in setup"))},

@@ -105,14 +105,6 @@ struct rc2dgi_ctx {
   unsigned short *mfield = nullptr;  // march field of the surface palettes (tuning rc_pal, launch_shade_cmin)
   float4 *cell_pal = nullptr;        // kCminDim^2 cells x kCellPalStride palette entries
   int rc_pal = 1;                    // surface palettes on (where they apply: 4096^2 .. 8192^2 square screens)
-  // split levels (tuning rc_split, a bit per level): the level's march runs on a stream of its own as soon as
-  // the side tables are built, its merge in level order on the frame stream (k_rc_level SPL)
-  int rc_split = 0;
-  // levels 1 and 0 in one kernel (tuning rc_pair, launch_rc_pair10): G_1 is never written
-  int rc_pair = 0;
-  std::vector<int4 *> hitbuf;           // per level: the march's hits, one int4 per cascade texel
-  std::vector<hipStream_t> split_st;    // per level
-  std::vector<hipEvent_t> split_ev;     // per level: end of its march; [N]: side tables built
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
   unsigned char *hitc = nullptr;     // per bound-table cell: holds a texel that passes the hit test
@@ -240,10 +232,6 @@ void free_level_bufs(rc2dgi_ctx *c) {
 
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
-  for (int4 *&p : c->hitbuf) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-  }
   c->rc_maps.clear();
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
@@ -605,10 +593,6 @@ int rc2dgi_destroy(rc2dgi_ctx *c) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : c->ev_level)
     if (ev) (void)hipEventDestroy(ev);
-  for (auto &ev : c->split_ev)
-    if (ev) (void)hipEventDestroy(ev);
-  for (auto &s : c->split_st)
-    if (s) (void)hipStreamDestroy(s);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return RC2DGI_OK;
@@ -906,27 +890,6 @@ int do_phase1(rc2dgi_ctx *c, const FramePlan &plan) {
   return rc == RC2DGI_OK ? phase1_end(c) : rc;
 }
 
-// the split levels' hit buffers, streams and events (made on first use)
-int split_resources(rc2dgi_ctx *c, unsigned split) {
-  if (c->split_ev.size() != (size_t)c->N + 1) {
-    for (auto &ev : c->split_ev)
-      if (ev) (void)hipEventDestroy(ev);
-    c->split_ev.assign(c->N + 1, nullptr);
-    for (auto &ev : c->split_ev) HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  }
-  if (c->split_st.size() < (size_t)c->N) {
-    const size_t n0 = c->split_st.size();
-    c->split_st.resize(c->N, nullptr);
-    for (size_t L = n0; L < c->split_st.size(); ++L)
-      HIPCHK(c, hipStreamCreateWithFlags(&c->split_st[L], hipStreamNonBlocking));
-  }
-  if (c->hitbuf.size() != (size_t)c->N) c->hitbuf.resize(c->N, nullptr);
-  for (int L = 0; L < c->N; ++L)
-    if ((split >> L & 1) && !c->hitbuf[L])
-      HIPCHK(c, alloc(&c->hitbuf[L], (size_t)c->cd.pitch * c->CH * sizeof(int4)));
-  return RC2DGI_OK;
-}
-
 // phase 2: cascades, blur, merge (RC2DGI.cs:342-404)
 int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   HIPCHK(c, hipSetDevice(c->device));
@@ -975,30 +938,11 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
   }
   if (mps) HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
-  // split levels: float4 cascades, one process, the 16x16x1 plain-field tiles (variants 0 / 13)
-  unsigned split = 0;
-  if (c->rc_split && c->world == 1 && c->storage == RC2DGI_STORAGE_F32)
-    for (int L = 0; L < c->N && L < 16; ++L)
-      if ((c->rc_split >> L & 1) && (c->rc_variant[L] == 0 || c->rc_variant[L] == 13)) split |= 1u << L;
-  if (split) {
-    if (int rc = split_resources(c, split)) return rc;
-    HIPCHK(c, hipEventRecord(c->split_ev[c->N], st));
-  }
-  // levels 1 and 0 paired: whole frames of float4 power-of-two cascades (rc_pair_ok), neither level split
-  const bool pair = c->rc_pair && c->world == 1 && !(split & 3u) && rc_pair_ok(c->sd, c->cd, c->N) &&
-                    c->rc_noproof[0] == c->rc_noproof[1];
-  RcLevelArgs pair1;  // level 1's arguments, launched with level 0
   bool gi1final = false;
-  for (int pass = split ? 0 : 1; pass < 2; ++pass)
   for (int L = c->N - 1; L >= 0; --L) {
-    if (pass == 0 && !(split >> L & 1)) continue;
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
     float4 *dstGI = gi1final ? c->gi2 : c->gi1;
-    // paired levels: G_2 goes to the spare texture, so that G_0 lands in the reference's finalGI (RC2DGI.cs:365)
-    // while the pair still reads G_2; the texture G_1 would occupy keeps its old contents (never read)
-    if (pair && L == 2) dstGI = c->gi_spare;
-    if (pair && L == 1) srcGI = c->gi_spare;
-    if (pass == 1 && LT && L + 1 < c->N) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
+    if (LT && L + 1 < c->N) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
     RcLevelArgs a;
     a.upper = (L == c->N - 1) ? nullptr : srcGI;
     a.out = dstGI;
@@ -1028,33 +972,10 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
 
-    if (pair && L == 1) {  // (launched with level 0; G_1's level_bufs copy is not made)
-      pair1 = a;
-      gi1final = !gi1final;
-      continue;
-    }
-    if (pair && L == 0) {
-      HIPCHK(c, launch_rc_pair10(pair1, a, c->sd, c->cd, st));
-      if (c->keep_levels)
-        HIPCHK(c, hipMemcpyAsync(c->level_bufs[0], dstGI, (size_t)c->cd.pitch * c->CH * gi_bytes(c),
-                                 hipMemcpyDeviceToDevice, st));
-      gi1final = !gi1final;
-      continue;
-    }
-    const bool spl = split >> L & 1;
-    a.split = spl ? (pass == 0 ? 1 : 2) : 0;
-    a.hitbuf = spl ? c->hitbuf[L] : nullptr;
-    hipStream_t ls = pass == 0 ? c->split_st[L] : st;
-    if (pass == 0) HIPCHK(c, hipStreamWaitEvent(ls, c->split_ev[c->N], 0));
-    if (pass == 1 && spl) HIPCHK(c, hipStreamWaitEvent(st, c->split_ev[L], 0));
     for (auto &r : plan.level[L].iv) {
       a.p0 = r.first;
       a.p1 = r.second;
-      HIPCHK(c, launch_rc_level(a, c->sd, c->cd, ls));
-    }
-    if (pass == 0) {
-      HIPCHK(c, hipEventRecord(c->split_ev[L], ls));
-      continue;
+      HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
     }
     if (c->keep_levels)
       HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], dstGI, (size_t)c->cd.pitch * c->CH * gi_bytes(c),
@@ -1619,15 +1540,6 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_pal = value != 0;
     return RC2DGI_OK;
   }
-  if (k == "rc_pair") {
-    c->rc_pair = value != 0;
-    return RC2DGI_OK;
-  }
-  if (k == "rc_split") {
-    if (value < 0 || value >= (1 << 16)) return fail(c, RC2DGI_E_ARG, "rc_split is a bit mask of levels");
-    c->rc_split = value;
-    return RC2DGI_OK;
-  }
   if (k.rfind("rc_noproof_L", 0) == 0) {
     const int L = std::atoi(k.c_str() + 12);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
@@ -1699,14 +1611,6 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "rc_pal") {
     *value = c->rc_pal;
-    return RC2DGI_OK;
-  }
-  if (k == "rc_pair") {
-    *value = c->rc_pair;
-    return RC2DGI_OK;
-  }
-  if (k == "rc_split") {
-    *value = c->rc_split;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_noproof_L", 0) == 0) {

@@ -120,8 +120,6 @@ struct RcLevelArgs {
   int cmin_screen = 0;          // the exit proof also tests the screen edge (worth it for long rays)
   int tail_k = 0;               // tail compaction after this many lockstep march iterations (0: off)
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
-  int split = 0;                // split levels (k_rc_level SPL): 1 march only, 2 merge only (16x16x1 float4)
-  int4 *hitbuf = nullptr;       // their per-probe hits (4 ints per cascade texel)
 };
 
 int dist_cmin_shift(int W, int H);
@@ -209,11 +207,6 @@ inline float rc_ray_end(int level, int N, float ray_range) {
 
 // one RadianceCascades.fs level
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);
-// levels 1 and 0 in one kernel (tuning rc_pair, k_rc_pair10): a1 = level 1 (its upper: G_2), a0 = level 0 (its
-// out: G_0); G_1 is never written.  Float4 cascades, power-of-two screens and cascades (CW >= 64, CH >= 32), N >= 3,
-// whole frames.  hipErrorInvalidValue (nothing launched) otherwise.
-bool rc_pair_ok(ScreenDims s, CascadeDims c, int N);
-hipError_t launch_rc_pair10(const RcLevelArgs &a1, const RcLevelArgs &a0, ScreenDims s, CascadeDims c, hipStream_t st);
 
 // Blur.fs into blur_out, then the default-shader blended copy-back into gi (RC2DGI.cs:367-387)
 hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st,

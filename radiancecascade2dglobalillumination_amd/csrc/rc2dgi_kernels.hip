@@ -1379,7 +1379,7 @@ unsigned long long *diag_stats_buffer() {
 }
 #endif
 
-RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c) {
+hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
   RcParams P;
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   P.stats = diag_stats_buffer();
@@ -1407,11 +1407,6 @@ RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c) {
   P.t0 = ((float)start / (float)maxValue) * a.ray_range;
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
-  return P;
-}
-
-hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
-  const RcParams P = rc_level_params(a, s, c);
   hipError_t e;
   if (c.gi_u8)
     e = launch_rc_u8(a, P, st);  // RGBA8 cascades: the 16x16x1 family only

@@ -6,8 +6,6 @@
 #include "rc2dgi_device.h"
 #include "rc2dgi_kernels.h"
 
-#include <type_traits>
-
 namespace rc2dgi {
 
 static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
@@ -38,7 +36,6 @@ struct RcParams {
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
-  int4 *hitbuf;               // split levels (SPL): the level's hits, 4 per probe texel (cascade pitch)
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   unsigned long long *stats;  // diagnostic builds: [16 levels][16] counters (rc2dgi_diag_stats)
 #endif
@@ -319,11 +316,7 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
 // DL: distance-field layout the march reads: 0 pitch-linear uint16, 1 8x8-tiled (TILED), 2 packed
 // 14-texel row packets (`dpk`, see kPackTexels; power-of-two screens <= 16384).
 // Z0: level 0 on a power-of-two screen (t0 = 0): the first march iteration is shared by a probe's rays
-// SPL: split levels (rc_split, small screens): 1 = march only -- every ray's hit (hit_idx) goes to P.hitbuf at
-// its probe's texel, no staging, no merge, no store; 2 = merge only -- the hits come from P.hitbuf, no table and
-// no march.  The marches of all levels depend on distRT only, so they run concurrently (one stream per level),
-// and the merges follow level by level; a level's results are the same bits either way.
-template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false, int SPL = 0>
+template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false>
 __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
@@ -357,7 +350,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #ifdef RC2DGI_DIAG_NOMERGE
   constexpr bool STG = false;  // timing-only ablation build: no upper staging, no merge (WRONG results)
 #else
-  constexpr bool STG = !TOP && SPL != 1;  // stage and merge the level-(L+1) cascade
+  constexpr bool STG = !TOP;  // stage and merge the level-(L+1) cascade
 #endif
   __shared__ typename GI::S s_up[STG ? NSTAGE : 1];
   // Exit proofs.  The march's last sample of a ray that misses only decides that the ray ends: it
@@ -383,8 +376,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // miss proof goes to the queue at once (no lockstep iterations).
   __shared__ uint2 s_q[TLC ? NT * NR : 1];
   __shared__ unsigned s_qn;
-  static_assert(SPL == 0 || (NR == 4 && !Z0), "split levels: one probe and one direction block per lane");
-  const bool tl = TLC && P.tailk != 0 && SPL != 2;
+  const bool tl = TLC && P.tailk != 0;
 #ifdef RC2DGI_DIAG_LDS_PAD  // diagnostic build: one workgroup per CU (LDS-limited residency)
   __shared__ unsigned s_pad[RC2DGI_DIAG_LDS_PAD];
   if (P.level == 99) s_pad[threadIdx.x] = 0u;
@@ -411,8 +403,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // than s cells (kclr = cell texels / texels per unit t).  The test of a ray's first sample proves most
   // misses before any gather (at L4 on the demo scene 72 % of the rays; samples per ray 2.10 -> 1.24 with
   // the per-sample test, scripts/dirproof_model.py).
-  const bool dp = TLC && P.dclr != nullptr && SPL != 2;
-  const bool cm = CMS && P.cmin != nullptr && !dp && SPL != 2;
+  const bool dp = TLC && P.dclr != nullptr;
+  const bool cm = CMS && P.cmin != nullptr && !dp;
   // (one bin per workgroup: bi0 * kDirBins / 4^L, exact for 4^L >= kDirBins; as a shift, since the product
   // overflows 32 bits from level 13 on)
   static_assert(kDirBins == 64, "the bin shift below assumes 64 = 4^3 bins");
@@ -507,11 +499,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     pok[p] = xok && cy < P.p1;
     oy[p] = div_res(((float)cy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P2S || P.c.powH);
   }
-  // split levels, merge only: this probe's hits, loaded now (consumed after the staging, SPL below)
-  int4 hpre = make_int4(-1, -1, -1, -1);
-  if constexpr (SPL == 2) {
-    if (pok[0]) hpre = P.hitbuf[(size_t)((bi0 >> P.level) * P.bdy + cyb) * P.c.pitch + (bi0 & (P.bsc - 1)) * P.bdx + cx];
-  }
   const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
 
   // ---- SampleRadianceSDF (RadianceCascades.fs:60-92), NR rays in lockstep; ray k = p*ND + r
@@ -536,7 +523,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr float kDone = __builtin_inff();
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
-    t[k] = SPL != 2 && pok[k / ND] && !(P.t0 > P.t1) ? P.t0 : kDone;
+    t[k] = pok[k / ND] && !(P.t0 > P.t1) ? P.t0 : kDone;
     hit_idx[k] = -1;
   }
   // Far intervals (t0 >= 1/4: the top levels, where most rays start beyond the screen edge): a ray
@@ -932,22 +919,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     for (int k = 0; k < NR; ++k)
       if (t[k] < kDone) hit_idx[k] = (int)s_q[qpos[k]].x;
   }
-  if constexpr (SPL != 0) {  // split levels: the hits to / from P.hitbuf, at the probe's texel (pixelIndex)
-    if (pok[0]) {
-      const int i = (bi0 & (P.bsc - 1)) * P.bdx + cx, j = (bi0 >> P.level) * P.bdy + cyb;
-      int4 *h = P.hitbuf + (size_t)j * P.c.pitch + i;
-      if constexpr (SPL == 1) {
-        *h = make_int4(hit_idx[0], hit_idx[1], hit_idx[2], hit_idx[3]);
-      } else {
-        (void)h;
-        hit_idx[0] = hpre.x;
-        hit_idx[1] = hpre.y;
-        hit_idx[2] = hpre.z;
-        hit_idx[3] = hpre.w;
-      }
-    }
-    if constexpr (SPL == 1) return;
-  }
   if constexpr (TLC) {  // (see hr above)
 #pragma unroll
     for (int k = 0; k < NR; ++k)
@@ -1111,27 +1082,6 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
                      reinterpret_cast<typename GI::T *>(a.out), DL == 1 ? a.dist_tiled : a.dist, a.shade,     \
                      a.dirs, a.sky, DL == 3 ? a.dist_nib : a.dist_packed)
   const bool top = a.level == a.N - 1;
-  P.hitbuf = a.hitbuf;
-  if (a.split) {  // split levels (SPL): the plain-field 16x16x1 float4 kernels only (variants 0, 13)
-    if constexpr (TX == 16 && TY == 16 && PY == 1 && PD == 1 && DL == 0 && std::is_same<GI, GiF32>::value) {
-      if (!a.hitbuf || (a.split != 1 && a.split != 2)) return hipErrorInvalidValue;
-#define RC2DGI_RCS(TOPV, P2V, S)                                                                                   \
-  hipLaunchKernelGGL((k_rc_level<16, 16, 1, 1, TOPV, P2V, UNR, 0, GiF32, false, S>), dim3(nwg), dim3(256), 0, st, P, \
-                     reinterpret_cast<const float4 *>(a.upper), reinterpret_cast<float4 *>(a.out), a.dist, a.shade,     \
-                     a.dirs, a.sky, a.dist_packed)
-      if (a.split == 1) {
-        if (top) { if (p2s) RC2DGI_RCS(true, true, 1); else RC2DGI_RCS(true, false, 1); }
-        else { if (p2s) RC2DGI_RCS(false, true, 1); else RC2DGI_RCS(false, false, 1); }
-      } else {
-        if (top) { if (p2s) RC2DGI_RCS(true, true, 2); else RC2DGI_RCS(true, false, 2); }
-        else { if (p2s) RC2DGI_RCS(false, true, 2); else RC2DGI_RCS(false, false, 2); }
-      }
-#undef RC2DGI_RCS
-      return hipGetLastError();
-    } else {
-      return hipErrorInvalidValue;
-    }
-  }
   if (top) {
     if (p2s) RC2DGI_RC(true, true, false); else RC2DGI_RC(true, false, false);
   } else if (p2s) {
@@ -1143,9 +1093,6 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
 #undef RC2DGI_RC
   return hipGetLastError();
 }
-
-// the level's kernel parameters (everything but the tile-shape dependent fields launch_rc_tiles sets)
-RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c);
 
 // per translation unit dispatchers of the tile variants (rc2dgi_rc_*.hip)
 hipError_t launch_rc_f32_rolled(const RcLevelArgs &a, RcParams P, hipStream_t st);

@@ -437,119 +437,6 @@ def test_surface_palettes_are_bit_identical(RC2DGI, scene):
     ctx.close()
 
 
-@pytest.mark.parametrize("W,H,N,rr,scene", [(256, 192, 5, 2.0, "rand:40"), (333, 200, 4, 8.0, "demo"),
-                                            (512, 512, 6, 2.0, "demo"), (1200, 900, 6, 2.0, "demo")])
-def test_split_levels_match_the_oracle(RC2DGI, W, H, N, rr, scene):
-    """rc_split (a level's march on a stream of its own into a hit buffer, its merge in level order,
-    k_rc_level SPL 1 / 2): every level against the oracle, for every split mask shape (all levels, the
-    upper half, single levels) and both one-probe variants it takes; run twice (the hit buffers of one
-    frame are not read by the next)."""
-    color, emis = make_scene(scene, W, H)
-    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr), color, emis, keep_levels=True)
-    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
-    ctx.set_keep_levels(True)
-    ctx.upload("color", color)
-    ctx.upload("emissive", emis)
-    full = (1 << N) - 1
-    for v in (0, 13):
-        ctx.set_tuning("rc_variant", v)
-        for mask in (full, full & ~((1 << (N // 2)) - 1), 1, 1 << (N - 1), 0b10):
-            ctx.set_tuning("rc_split", mask)
-            assert ctx.get_tuning("rc_split") == mask
-            for rep in range(2):
-                ctx.do_rc2dgi()
-                ctx.sync()
-                for L in range(N):
-                    g = ctx.download_level(L)
-                    assert np.array_equal(g, fr.gi_levels[L]), \
-                        f"variant {v} split {mask:#x} run {rep} L{L}: {np.count_nonzero(g != fr.gi_levels[L])}"
-                assert np.array_equal(ctx.download("color"), fr.color_out)
-    ctx.close()
-
-
-@pytest.mark.parametrize("W,H,N,rr,scene,refl", [(256, 128, 5, 2.0, "rand:44", 0.0), (128, 128, 3, 8.0, "demo", 0.0),
-                                                 (512, 512, 6, 2.0, "demo", 0.0), (256, 256, 4, 4.0, "rand:45", 0.5),
-                                                 (1024, 512, 6, 2.0, "rand:46", 0.0)])
-def test_paired_levels_match_the_oracle(RC2DGI, W, H, N, rr, scene, refl):
-    """rc_pair (levels 1 and 0 in one kernel, k_rc_pair10: the level-0 tile computes its level-1 footprint
-    into LDS, G_1 is never written): G_0, every level above 1 and the merged frame against the oracle, with
-    the exit proofs on and off (rc_skip), twice."""
-    color, emis = make_scene(scene, W, H)
-    fr = oracle.frame(oracle.Params(W=W, H=H, N=N, ray_range=rr, reflectivity=refl), color, emis, keep_levels=True)
-    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
-    ctx.set_shader_value("_Reflectivity", refl)
-    ctx.set_keep_levels(True)
-    ctx.upload("color", color)
-    ctx.upload("emissive", emis)
-    ctx.set_tuning("rc_pair", 1)
-    assert ctx.get_tuning("rc_pair") == 1
-    for skip in (0, 2):
-        ctx.set_tuning("rc_skip", skip)
-        for rep in range(2):
-            ctx.do_rc2dgi()
-            ctx.sync()
-            for L in [0] + list(range(2, N)):
-                g = ctx.download_level(L)
-                assert np.array_equal(g, fr.gi_levels[L]), \
-                    f"rc_skip {skip} run {rep} L{L}: {np.count_nonzero(g != fr.gi_levels[L])} differ"
-            assert np.array_equal(ctx.download("color"), fr.color_out)
-    ctx.close()
-
-
-def test_paired_levels_at_4096_are_bit_identical(RC2DGI):
-    """rc_pair at 4096^2 N=6 under the committed schedule (palettes, miss proofs): G_0 and the outputs equal
-    to the unpaired frame's, bit for bit."""
-    W = H = 4096
-    N = 6
-    color, emis = make_scene("demo", W, H)
-    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0)
-    ctx.set_keep_levels(True)
-    ctx.upload("color", color)
-    ctx.upload("emissive", emis)
-    want = None
-    for pair in (0, 1):
-        ctx.set_tuning("rc_pair", pair)
-        ctx.do_rc2dgi()
-        ctx.sync()
-        got = {f"L{L}": ctx.download_level(L) for L in [0] + list(range(2, N))}
-        got.update({k: ctx.download(k) for k in ("color", "temp", "final_gi")})
-        if want is None:
-            want = got
-            continue
-        for k in got:
-            assert np.array_equal(got[k], want[k]), f"{k}: {np.count_nonzero(got[k] != want[k])} differ"
-    ctx.close()
-
-
-@pytest.mark.parametrize("scene", ["demo", "speckled"])
-def test_split_levels_with_palettes_are_bit_identical(RC2DGI, scene):
-    """rc_split at 4096^2 N=6 (surface palettes and miss proofs on): every level and output texture equal to
-    the unsplit frame's, bit for bit."""
-    W = H = 4096
-    N = 6
-    color, emis = speckled_scene(W, H) if scene == "speckled" else make_scene(scene, W, H)
-    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0)
-    ctx.set_keep_levels(True)
-    ctx.upload("color", color)
-    ctx.upload("emissive", emis)
-    for L in range(1, N):
-        ctx.set_tuning(f"rc_variant_L{L}", 13)
-    want = None
-    for mask in (0, 0b111110, 0b111111):
-        ctx.set_tuning("rc_split", mask)
-        ctx.do_rc2dgi()
-        ctx.sync()
-        got = {f"L{L}": ctx.download_level(L) for L in range(N)}
-        got.update({k: ctx.download(k) for k in ("color", "temp", "final_gi")})
-        if want is None:
-            want = got
-            continue
-        for k in got:
-            assert np.array_equal(got[k], want[k]), \
-                f"{scene} split {mask:#x} {k}: {np.count_nonzero(got[k] != want[k])} differ"
-    ctx.close()
-
-
 @pytest.mark.parametrize("W,H,rs,radius", [
     (128, 128, 1.0, 1.5),    # fixed taps (F=1), merge fused
     (256, 128, 1.0, 2.5),    # F=2
