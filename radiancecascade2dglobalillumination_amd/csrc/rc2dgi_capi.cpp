@@ -291,7 +291,10 @@ const int kOrderCandidates[][4] = {{0, 0, 0, 0},  {2, 2, 8, 0},  {4, 4, 4, 0},  
                                    {1, 1, 8, 2},   {1, 2, 32, 2},  {1, 1, 4, 2},   {1, 2, 4, 2},   {1, 4, 2, 2},
                                    {1, 8, 4, 2},   {1, 1, 64, 2},  {1, 2, 64, 2},  {1, 1, 128, 2}, {1, 8, 8, 2},
                                    {1, 3, 8, 2},   {1, 6, 8, 2},   {1, 3, 16, 2},  {1, 6, 4, 2},   {1, 12, 4, 2},
-                                   {1, 16, 2, 2},  {1, 3, 32, 2},  {1, 6, 16, 2}};
+                                   {1, 16, 2, 2},  {1, 3, 32, 2},  {1, 6, 16, 2},
+                                   // round 4 (order grids, profiles/r04/ab/orders_grid*.txt)
+                                   {1, 1, 4, 1},   {2, 32, 32, 0}, {8, 32, 4, 1},  {8, 2, 4, 0},   {8, 32, 64, 0},
+                                   {1, 3, 2, 2}};
 
 // jumpRT1 / jumpRT2 for the sharding: full-size textures, or (world > 1, >= 2 JFA steps) the
 // strip windows of the JumpFlood exchange (rows [y0 - m, y1 + m) of the strip) and its two
