@@ -551,16 +551,16 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
 }
 
 // k_shade and k_dist_cmin in one pass over distRT, for square power-of-two screens with cells of >= 64
-// texels (W = H = kCminDim << csh, csh >= 6: 4096^2 and up).  One workgroup per cell; wave w takes rows
-// w, w + 4, ... of it, a lane one column of each 64-column run, 16 rows at a time (each load instruction
-// one contiguous run: 128 B of distance, 1 KB of emission or albedo).  Same records, same bound table and
+// texels (W = H = kCminDim << csh, csh >= 6: 4096^2 and up).  One workgroup of NTH lanes per cell; wave w
+// takes rows w, w + NW, ... of it (NW = NTH / 64 waves), a lane one column of each 64-column run, 64 / NW rows
+// at a time (each load instruction one contiguous run: 128 B of distance, 1 KB of emission or albedo).  Same records, same bound table and
 // flags as the two kernels (the cell minimum includes the REPEAT-wrap texels of the last row / column).
 // PAL: also the cell's surface palette and the march field (see kCellPal): the distinct records of the
 // cell's hittable texels in cpal[cell * kCellPal + i] (deduplicated in LDS; two waves inserting one record
 // at once may both add it -- a wasted entry, never a wrong one), and mf = distRT with every hittable texel's
 // q replaced by its palette entry i (kCellPal: no entry left, the march reads its record from shade).
-template <bool PAL>
-__global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__restrict__ dist,
+template <bool PAL, int NTH = 256>
+__global__ __launch_bounds__(NTH) void k_shade_cmin(const unsigned short *__restrict__ dist,
                                                     const float4 *__restrict__ color, const float4 *__restrict__ emis,
                                                     float4 *__restrict__ shade, ScreenDims s, float reflectivity,
                                                     int csh, CminT *__restrict__ cmin, unsigned char *__restrict__ hitc,
@@ -578,23 +578,24 @@ __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__rest
   }
   float4 *const gpal = PAL ? cpal + (size_t)(blockIdx.y * kCminDim + blockIdx.x) * kCellPalStride : nullptr;
   unsigned m = 0xFFFFu;
-  const size_t rstep = (size_t)4 * s.pitch;  // a wave's consecutive rows are 4 apart
+  constexpr int NW = NTH / 64, RPW = 64 / NW;  // waves; a wave's rows of a 64-row block (NW apart)
+  const size_t rstep = (size_t)NW * s.pitch;
   for (int c = lane; c < cw; c += 64) {
     for (int rb = 0; rb < cw; rb += 64) {
       // the wave's 16 rows of this 64-row block: every distance load in flight at once, then the records
       // of the hittable texels 8 rows at a time (two round trips, not one per 4 rows)
       const size_t base = (size_t)(y0 + rb + w) * s.pitch + x0 + c;
-      unsigned q[16];
+      unsigned q[RPW];
 #pragma unroll
-      for (int t = 0; t < 16; ++t) q[t] = dist[base + t * rstep];
+      for (int t = 0; t < RPW; ++t) q[t] = dist[base + t * rstep];
       unsigned hm = 0;
 #pragma unroll
-      for (int t = 0; t < 16; ++t) {
+      for (int t = 0; t < RPW; ++t) {
         m = min(m, q[t]);
         hm |= decode_dist(q[t]) < 0.001f ? 1u << t : 0u;
       }
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < RPW / 8; ++h) {
         // (with palettes the skip is wave-uniform: the palette code below needs every lane of the wave)
         if (PAL ? __ballot((hm >> (8 * h) & 0xFFu) != 0u) == 0ull : !(hm >> (8 * h) & 0xFFu)) {
           if (PAL) {
@@ -672,17 +673,18 @@ __global__ __launch_bounds__(256) void k_shade_cmin(const unsigned short *__rest
   }
   // REPEAT wrap (k_dist_cmin): samples at u = 1 / v = 1 read column 0 / row 0
   if (x0 + cw == s.W)
-    for (int e = (int)threadIdx.x; e < cw; e += 256) m = min(m, (unsigned)dist[(size_t)(y0 + e) * s.pitch]);
+    for (int e = (int)threadIdx.x; e < cw; e += NTH) m = min(m, (unsigned)dist[(size_t)(y0 + e) * s.pitch]);
   if (y0 + cw == s.H)
-    for (int e = (int)threadIdx.x; e < cw; e += 256) m = min(m, (unsigned)dist[x0 + e]);
+    for (int e = (int)threadIdx.x; e < cw; e += NTH) m = min(m, (unsigned)dist[x0 + e]);
   if (x0 + cw == s.W && y0 + cw == s.H && threadIdx.x == 0) m = min(m, (unsigned)dist[0]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, o, 64));
-  __shared__ unsigned s_m[4];
+  __shared__ unsigned s_m[NW];
   if (lane == 0) s_m[w] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-    m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
+#pragma unroll
+    for (int i = 1; i < NW; ++i) m = min(m, s_m[i]);
     const float d = decode_dist(m);
     if (hitc) hitc[blockIdx.y * kCminDim + blockIdx.x] = d < 0.001f ? 1 : 0;
     cmin[blockIdx.y * kCminDim + blockIdx.x] = d >= 0.001f ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
@@ -1631,7 +1633,7 @@ hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, co
                              unsigned short *mf, float4 *cpal) {
   if (!shade_cmin_fused_ok(s.W, s.H, s.pitch)) return hipErrorInvalidValue;
   if (mf && cpal)
-    hipLaunchKernelGGL(k_shade_cmin<true>, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, color, emis, shade, s,
+    hipLaunchKernelGGL((k_shade_cmin<true, 512>), dim3(kCminDim, kCminDim), dim3(512), 0, st, dist, color, emis, shade, s,
                        reflectivity, dist_cmin_shift(s.W, s.H), cmin, hitc, mf, cpal);
   else
     hipLaunchKernelGGL(k_shade_cmin<false>, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, color, emis, shade, s,
