@@ -1094,9 +1094,10 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
   // march rolled / unrolled x linear / 8x8-tiled / packed / nibble-predicted distance field; 32x8 tiles
   // (x2 probes per lane); one probe per lane in 512- and 1024-lane workgroups
-  // (RGBA16F / RGBA8 cascades build the 16x16x1 family only: the other ids would time that kernel again)
+  // (RGBA16F / RGBA8 cascades build the 16x16x1 family and three low-level shapes: the other ids would time
+  // the default kernel again)
   const int kVariantsF32[] = {0, 1, 3, 5, 6, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
-  const int kVariantsOther[] = {0, 13, 14, 15, 16, 17, 18, 19};
+  const int kVariantsOther[] = {0, 1, 3, 6, 13, 14, 15, 16, 17, 18, 19};
   const bool f32 = c->storage == RC2DGI_STORAGE_F32;
   const int *kVariants = f32 ? kVariantsF32 : kVariantsOther;
   const int nv = f32 ? (int)(sizeof(kVariantsF32) / sizeof(int)) : (int)(sizeof(kVariantsOther) / sizeof(int));

@@ -1411,9 +1411,9 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.reflectivity = a.reflectivity;
   hipError_t e;
   if (c.gi_u8)
-    e = launch_rc_u8(a, P, st);  // RGBA8 cascades: the 16x16x1 family only
+    e = launch_rc_u8(a, P, st);  // RGBA8 cascades: the 16x16x1 family and 16x8x2, 32x8x1, 32x8x2
   else if (c.gi_f16)
-    e = launch_rc_f16(a, P, st);  // RGBA16F cascades: the 16x16x1 family only
+    e = launch_rc_f16(a, P, st);  // RGBA16F cascades: the 16x16x1 family and 16x8x2, 32x8x1, 32x8x2
   else if (a.variant >= 20 && a.variant < rc_variant_count())
     e = launch_rc_f32_wide(a, P, st);
   else if (a.variant >= 13 && a.variant < rc_variant_count())

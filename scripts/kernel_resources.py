@@ -24,8 +24,8 @@ for line in err.splitlines():
     if cur and m:
         rows[cur][m.group(1).strip()] = int(m.group(2))
 for name, r in rows.items():
-    t = re.search(r"k_rc_levelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELb([01])ELi(\d+)ELi(\d+)ENS_5(\w+?)ELb([01])(?:ELi(\d+))?", name)
+    t = re.search(r"k_rc_levelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELb([01])ELi(\d+)ELi(\d+)ENS_\d(\w+?)ELb([01])", name)
     tag = (f"{t.group(1)}x{t.group(2)}x{t.group(3)} pd{t.group(4)} top{t.group(5)} p2s{t.group(6)} unr{t.group(7)} "
-           f"dl{t.group(8)} {t.group(9)} z0{t.group(10)} spl{t.group(11) or 0}") if t else name[:60]
+           f"dl{t.group(8)} {t.group(9)} z0{t.group(10)}") if t else name[:60]
     print(f"{tag:55s} sgpr {r.get('TotalSGPRs')} vgpr {r.get('VGPRs')} scratch {r.get('ScratchSize [bytes/lane]')} "
           f"lds {r.get('LDS Size [bytes/block]')} occ {r.get('Occupancy [waves/SIMD]')}")
