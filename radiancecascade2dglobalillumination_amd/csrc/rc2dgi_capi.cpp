@@ -346,9 +346,7 @@ int allocate(rc2dgi_ctx *c) {
   c->mpitch = ((c->W + 63) / 64) * 2;
   HIPCHK(c, alloc(&c->occ, (size_t)c->mpitch * c->H * sizeof(unsigned)));
   HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
-  HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
-  HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
-  HIPCHK(c, alloc(&c->dist_n, dist_nib_bytes(c->W, c->H)));
+  // (the re-laid-out distRT copies of the "t" / "p" / "n" variants are made on first use, do_phase2)
   HIPCHK(c, alloc(&c->shade, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->cmin, (size_t)kCminDim * kCminDim * sizeof(CminT)));
   HIPCHK(c, alloc(&c->hitc, (size_t)kCminDim * kCminDim));
@@ -909,10 +907,14 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     packed |= rc_variant_packed(v);
     nib |= rc_variant_nib(v);
   }
+  if (tiled && !c->dist_t)
+    HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
   if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
   // (the packed marches run on power-of-two screens of up to 16384 columns only; elsewhere their variants
   // launch the plain-field march, and the copies would be built for nothing)
   const bool p2s = c->sd.powW && c->sd.powH && c->cd.powW && c->cd.powH && c->W <= 16384;
+  if (packed && p2s && !c->dist_p) HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
+  if (nib && p2s && !c->dist_n) HIPCHK(c, alloc(&c->dist_n, dist_nib_bytes(c->W, c->H)));
   if (packed && p2s) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
   if (nib && p2s) HIPCHK(c, launch_dist_nib(c->dist, c->sd.pitch, c->dist_n, c->W, c->H, st));
   // exit proofs: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
