@@ -1103,9 +1103,13 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   const bool f32 = c->storage == RC2DGI_STORAGE_F32;
   const int *kVariants = f32 ? kVariantsF32 : kVariantsOther;
   const int nv = f32 ? (int)(sizeof(kVariantsF32) / sizeof(int)) : (int)(sizeof(kVariantsOther) / sizeof(int));
-  std::vector<float> best(c->N, 1e30f);
+  std::vector<float> best(c->N, 1e30f), bestp(c->N, 1e30f);
   std::vector<int> pick(c->rc_order), pickv(c->rc_variant);
+  std::vector<int> pickp(c->rc_order), pickpv(c->rc_variant);  // the best of the variants that need no distRT copy
   std::vector<float> lv(c->N);
+  // which distRT copy a variant reads (0: none, 1 tiled, 2 packed, 3 nibble): the copy is built once per frame and
+  // timed with the top level, so the per-level picks below do not see it
+  auto copy_kind = [](int v) { return rc_variant_tiled(v) ? 1 : rc_variant_packed(v) ? 2 : rc_variant_nib(v) ? 3 : 0; };
   for (int k = 0; k < nv * nc; ++k) {
     const int v = kVariants[k / nc], o = k % nc;
     for (int L = 0; L < c->N; ++L) {
@@ -1124,12 +1128,58 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
       if (f > 0)
         for (int L = 0; L < c->N; ++L) acc[L] = std::min(acc[L], lv[L]);
     }
-    for (int L = 0; L < c->N; ++L)
+    for (int L = 0; L < c->N; ++L) {
       if (acc[L] < best[L]) {
         best[L] = acc[L];
         pick[L] = c->rc_order[L];
         pickv[L] = c->rc_variant[L];
       }
+      if (copy_kind(v) == 0 && acc[L] < bestp[L]) {
+        bestp[L] = acc[L];
+        pickp[L] = c->rc_order[L];
+        pickpv[L] = c->rc_variant[L];
+      }
+    }
+  }
+  // the schedule's RC pass (every level, the copies included)
+  auto pass_ms = [&](const std::vector<int> &ord, const std::vector<int> &var, float *ms) -> int {
+    c->rc_order = ord;
+    c->rc_variant = var;
+    float m = 1e30f;
+    for (int f = 0; f <= frames; ++f) {
+      int rc = rc2dgi_do(c);
+      if (rc == RC2DGI_OK) rc = rc2dgi_pass_times(c, nullptr, 0, lv.data(), c->N);
+      if (rc != RC2DGI_OK) return rc;
+      float t = 0.0f;
+      for (float x : lv) t += x;
+      if (f > 0) m = std::min(m, t);
+    }
+    *ms = m;
+    return RC2DGI_OK;
+  };
+  // a copy kind pays only if its levels gain more than the copy costs: try each kind's levels on their best
+  // copy-free picks instead
+  for (int kind = 1; kind <= 3; ++kind) {
+    bool used = false;
+    for (int L = 0; L < c->N; ++L) used |= copy_kind(pickv[L]) == kind;
+    if (!used) continue;
+    std::vector<int> o2(pick), v2(pickv);
+    for (int L = 0; L < c->N; ++L)
+      if (copy_kind(pickv[L]) == kind) {
+        o2[L] = pickp[L];
+        v2[L] = pickpv[L];
+      }
+    float t1 = 0.0f, t2 = 0.0f;
+    int rc = pass_ms(pick, pickv, &t1);
+    if (rc == RC2DGI_OK) rc = pass_ms(o2, v2, &t2);
+    if (rc != RC2DGI_OK) {
+      c->timing = timing;
+      return rc;
+    }
+    if (t2 < t1) {
+      pick = o2;
+      pickv = v2;
+    }
   }
   c->rc_order = pick;
   c->rc_variant = pickv;
