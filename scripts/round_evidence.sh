@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 evidence on one box, in one call: the GPU suite, the headline bench with its rocprofv3 kernel stats
+# Round-end evidence on one box, in one call: the GPU suite, the headline bench with its rocprofv3 kernel stats
 # and PMC traffic (scripts/round_profile.sh), one line per BASELINE config and storage mode, the C3 strips and
-# the C4 batch lines.  Results under gpurun_out/ (copied into profiles/r04/final by hand).
+# the C4 batch lines.  Results under gpurun_out/ (copied into profiles/r<NN>/final by hand).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out; export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
