@@ -406,7 +406,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--sweep-rc", action="store_true",
                     help="time every RC tile variant per level (interleaved rounds) instead of the bench line")
-    ap.add_argument("--scene", default="demo", help="demo | random:<seed>")
+    ap.add_argument("--scene", default="demo", help="demo | random:<seed> | dense:<seed> (>= 25 %% occluders)")
     ap.add_argument("--batch", type=int, default=0,
                     help="scenes per GPU, one context each (BASELINE configs[4] batch mode)")
     ap.add_argument("--batch-streams", type=int, default=1,
@@ -472,8 +472,14 @@ def main():
     N = a.cascades
     if a.scene == "demo":
         color, emis = scenes.demo(W, H, t=3.0 + 0.25 * rank)  # one independent scene per rank
+        scene_desc = f"reference demo scene painted at {W}x{H}"
     else:
-        color, emis = scenes.random_scene(W, H, seed=int(a.scene.split(":")[1]) + rank)
+        kind, seed = a.scene.split(":")
+        cov = {"random": 0.05, "dense": 0.35}[kind]  # dense: >= 25 % of the texels occluders
+        color, emis = scenes.random_scene(W, H, seed=int(seed) + rank, coverage=cov)
+        scene_desc = f"random scene {kind}:{seed} at {W}x{H}"
+    # fraction of occluder texels (ScreenUV.fs: any colour channel above zero)
+    coverage = float(np.count_nonzero(np.any(color[..., :3] > 0, axis=-1)) / (W * H))
     ctx = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local, storage=a.storage)
     CW, CH = ctx.cascade_resolution
     # inputs resident in HBM before the timed region
@@ -566,8 +572,9 @@ def main():
         "vs_baseline": None,
         "dtype": {"f32": "f32", "f16": "f32 (RGBA16F cascade storage)",
                   "rgba8": "f32 arithmetic, RGBA8 render textures (8-bit blends / filtering)"}[a.storage],
-        "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
+        "data": f"synthetic ({scene_desc}, resident in HBM)",
         "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}", "screen": [W, H],
+                   "scene": a.scene, "occluder_coverage": round(coverage, 4),
                    "cascade_resolution": [CW, CH], "cascade_count": N, "ray_range": a.ray_range,
                    "parallelism": f"replicas{world}",
                    "rc_order": orders or "default", "rc_variant": variants,

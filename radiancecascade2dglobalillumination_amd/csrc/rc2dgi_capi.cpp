@@ -104,6 +104,8 @@ struct rc2dgi_ctx {
   uint4 *dist_n = nullptr;           // nibble-predicted copy for the "n" RC variants (k_dist_nib)
   unsigned short *mfield = nullptr;  // march field of the surface palettes (tuning rc_pal, launch_shade_cmin)
   float4 *cell_pal = nullptr;        // kCminDim^2 cells x kCellPalStride palette entries
+  // which side tables the last frame built (rc2dgi_download_table answers RC2DGI_E_STATE for the others)
+  bool built_hitc = false, built_cmin = false, built_dclr = false, built_pal = false;
   int rc_pal = 1;                    // surface palettes on (where they apply: 4096^2 .. 8192^2 square screens)
   float4 *shade = nullptr;           // surface records of the hittable texels (k_shade)
   CminT *cmin = nullptr;             // coarse lower bound of distRT for the march's exit proofs (k_dist_cmin)
@@ -254,6 +256,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->hitc = c->dclr = nullptr;
   c->mfield = nullptr;
   c->cell_pal = nullptr;
+  c->built_hitc = c->built_cmin = c->built_dclr = c->built_pal = false;
   c->dboxes = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
   c->dirs = nullptr;
@@ -327,6 +330,41 @@ int jfa_buffers(rc2dgi_ctx *c) {
   return RC2DGI_OK;
 }
 
+// The distRT copies the schedule's variants read ("t" / "p" / "n") and the surface-palette tables (rc_pal),
+// allocated when the schedule or the knobs are set (rc2dgi_set_tuning, rc2dgi_autotune with all = true,
+// allocate), never inside a frame: hipMalloc may synchronise the device, and an out-of-memory then surfaces
+// at the call that asked for the buffer instead of mid-enqueue (rc2dgi_do_group enqueues several devices).
+int prepare_side_buffers(rc2dgi_ctx *c, bool all = false) {
+  if (!c->dist) return RC2DGI_OK;  // not allocated yet (allocate() calls this again)
+  bool tiled = all, packed = all, nib = all;
+  for (int v : c->rc_variant) {
+    tiled |= rc_variant_tiled(v);
+    packed |= rc_variant_packed(v);
+    nib |= rc_variant_nib(v);
+  }
+  // (the packed marches run on power-of-two screens of up to 16384 columns only)
+  const bool p2s = c->sd.powW && c->sd.powH && c->cd.powW && c->cd.powH && c->W <= 16384;
+  if (tiled && !c->dist_t)
+    HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
+  if (packed && p2s && !c->dist_p) HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
+  if (nib && p2s && !c->dist_n) HIPCHK(c, alloc(&c->dist_n, dist_nib_bytes(c->W, c->H)));
+  const bool pal = c->rc_pal && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch) &&
+                   (size_t)c->sd.pitch * c->H <= ((size_t)1 << 26);
+  if (pal && (!c->mfield || !c->cell_pal)) {
+    hipError_t e = c->mfield ? hipSuccess : alloc(&c->mfield, (size_t)c->sd.pitch * c->H * sizeof(unsigned short));
+    if (e == hipSuccess && !c->cell_pal)
+      e = alloc(&c->cell_pal, (size_t)kCminDim * kCminDim * kCellPalStride * sizeof(float4));
+    if (e != hipSuccess) {  // both or neither
+      for (void *q : {(void *)c->mfield, (void *)c->cell_pal})
+        if (q) (void)hipFree(q);
+      c->mfield = nullptr;
+      c->cell_pal = nullptr;
+      return hip_fail(c, e, "surface palette tables");
+    }
+  }
+  return RC2DGI_OK;
+}
+
 // (re)allocate every render texture for the current W, H, N (RC2DGI.cs:79-98)
 int allocate(rc2dgi_ctx *c) {
   free_buffers(c);
@@ -346,7 +384,7 @@ int allocate(rc2dgi_ctx *c) {
   c->mpitch = ((c->W + 63) / 64) * 2;
   HIPCHK(c, alloc(&c->occ, (size_t)c->mpitch * c->H * sizeof(unsigned)));
   HIPCHK(c, alloc(&c->dist, ns * sizeof(unsigned short)));
-  // (the re-laid-out distRT copies of the "t" / "p" / "n" variants are made on first use, do_phase2)
+  // (the re-laid-out distRT copies of the "t" / "p" / "n" variants: prepare_side_buffers, when a schedule reads them)
   HIPCHK(c, alloc(&c->shade, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->cmin, (size_t)kCminDim * kCminDim * sizeof(CminT)));
   HIPCHK(c, alloc(&c->hitc, (size_t)kCminDim * kCminDim));
@@ -384,6 +422,7 @@ int allocate(rc2dgi_ctx *c) {
   c->rc_mp.assign(c->N, 1);  // directional miss proofs wherever they apply (one-probe tiles, 4^L >= kDirBins)
   c->rc_noproof.assign(c->N, 0);
   if (int rc = jfa_buffers(c)) return rc;
+  if (int rc = prepare_side_buffers(c)) return rc;
   if (c->keep_levels) {
     c->level_bufs.assign(c->N, nullptr);
     for (auto &p : c->level_bufs) HIPCHK(c, alloc(&p, nc * gsz));
@@ -907,14 +946,13 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     packed |= rc_variant_packed(v);
     nib |= rc_variant_nib(v);
   }
-  if (tiled && !c->dist_t)
-    HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
-  if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
   // (the packed marches run on power-of-two screens of up to 16384 columns only; elsewhere their variants
   // launch the plain-field march, and the copies would be built for nothing)
   const bool p2s = c->sd.powW && c->sd.powH && c->cd.powW && c->cd.powH && c->W <= 16384;
-  if (packed && p2s && !c->dist_p) HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
-  if (nib && p2s && !c->dist_n) HIPCHK(c, alloc(&c->dist_n, dist_nib_bytes(c->W, c->H)));
+  // (the copies were allocated when the schedule was set: prepare_side_buffers; a frame never allocates)
+  if ((tiled && !c->dist_t) || (packed && p2s && !c->dist_p) || (nib && p2s && !c->dist_n))
+    return fail(c, RC2DGI_E_STATE, "distRT copy of the schedule not prepared");
+  if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
   if (packed && p2s) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
   if (nib && p2s) HIPCHK(c, launch_dist_nib(c->dist, c->sd.pitch, c->dist_n, c->W, c->H, st));
   // exit proofs: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
@@ -931,10 +969,11 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   // surface palettes also the march field the plain-field levels read (launch_shade_cmin)
   const bool fused = proofs && c->shade_fused && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch);
   const bool pal = fused && c->rc_pal && (size_t)c->sd.pitch * c->H <= ((size_t)1 << 26);
-  if (pal && !c->mfield) {
-    HIPCHK(c, alloc(&c->mfield, (size_t)c->sd.pitch * c->H * sizeof(unsigned short)));
-    HIPCHK(c, alloc(&c->cell_pal, (size_t)kCminDim * kCminDim * kCellPalStride * sizeof(float4)));
-  }
+  if (pal && (!c->mfield || !c->cell_pal)) return fail(c, RC2DGI_E_STATE, "surface palette tables not prepared");
+  c->built_hitc = mps;
+  c->built_cmin = proofs;
+  c->built_dclr = mps;
+  c->built_pal = pal;
   if (fused) {
     HIPCHK(c, launch_shade_cmin(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, c->cmin,
                                 mps ? c->hitc : nullptr, st, pal ? c->mfield : nullptr, pal ? c->cell_pal : nullptr));
@@ -1091,6 +1130,7 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   RC2DGI_USABLE(c);
   if (c->world > 1) return fail(c, RC2DGI_E_STATE, "autotune an unsharded context (the orders carry over)");
   if (frames < 1) frames = 1;
+  if (int rc = prepare_side_buffers(c, true)) return rc;  // every copy a candidate variant reads
   const int timing = c->timing;
   c->timing = 1;
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
@@ -1347,16 +1387,17 @@ int rc2dgi_download_table(rc2dgi_ctx *c, int which, void *host, int bytes) {
   const void *src = nullptr;
   size_t n = 0;
   const size_t cells = (size_t)kCminDim * kCminDim;
+  bool built = true;  // (what the last frame built: do_phase2's flags; the step boxes are static)
   switch (which) {
-    case RC2DGI_TAB_HITC: src = c->hitc; n = cells; break;
-    case RC2DGI_TAB_CMIN: src = c->cmin; n = cells * sizeof(CminT); break;
-    case RC2DGI_TAB_DCLR: src = c->dclr; n = (size_t)kDirBins * cells; break;
-    case RC2DGI_TAB_DBOXES: src = c->dboxes; n = (size_t)kDirBins * kCminDim * sizeof(int4); break;
-    case RC2DGI_TAB_CELLPAL: src = c->cell_pal; n = cells * kCellPalStride * sizeof(float4); break;
-    case RC2DGI_TAB_MFIELD: src = c->mfield; n = (size_t)c->sd.pitch * c->H * sizeof(unsigned short); break;
+    case RC2DGI_TAB_HITC: src = c->hitc; n = cells; built = built && c->built_hitc; break;
+    case RC2DGI_TAB_CMIN: src = c->cmin; n = cells * sizeof(CminT); built = built && c->built_cmin; break;
+    case RC2DGI_TAB_DCLR: src = c->dclr; n = (size_t)kDirBins * cells; built = built && c->built_dclr; break;
+    case RC2DGI_TAB_DBOXES: src = c->dboxes; n = (size_t)kDirBins * kCminDim * sizeof(int4); built = true; break;
+    case RC2DGI_TAB_CELLPAL: src = c->cell_pal; n = cells * kCellPalStride * sizeof(float4); built = built && c->built_pal; break;
+    case RC2DGI_TAB_MFIELD: src = c->mfield; n = (size_t)c->sd.pitch * c->H * sizeof(unsigned short); built = built && c->built_pal; break;
     default: return fail(c, RC2DGI_E_ARG, "bad table id");
   }
-  if (!src) return fail(c, RC2DGI_E_STATE, "table not built");
+  if (!src || !built) return fail(c, RC2DGI_E_STATE, "table not built by the last frame");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (bytes > 0) HIPCHK(c, hipMemcpy(host, src, std::min(n, (size_t)bytes), hipMemcpyDeviceToHost));
@@ -1533,12 +1574,12 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     if (value < 0 || value >= rc_variant_count()) return fail(c, RC2DGI_E_ARG, "rc_variant out of range");
     if (k == "rc_variant") {
       for (int &v : c->rc_variant) v = value;
-      return RC2DGI_OK;
+      return prepare_side_buffers(c);
     }
     const int L = std::atoi(k.c_str() + 12);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
     c->rc_variant[L] = value;
-    return RC2DGI_OK;
+    return prepare_side_buffers(c);
   }
   if (k == "blur_path") {
     if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "blur_path out of range");
@@ -1594,7 +1635,7 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
   }
   if (k == "rc_pal") {
     c->rc_pal = value != 0;
-    return RC2DGI_OK;
+    return prepare_side_buffers(c);
   }
   if (k.rfind("rc_noproof_L", 0) == 0) {
     const int L = std::atoi(k.c_str() + 12);

@@ -556,7 +556,7 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
 // at a time (each load instruction one contiguous run: 128 B of distance, 1 KB of emission or albedo).  Same records, same bound table and
 // flags as the two kernels (the cell minimum includes the REPEAT-wrap texels of the last row / column).
 // PAL: also the cell's surface palette and the march field (see kCellPal): the distinct records of the
-// cell's hittable texels in cpal[cell * kCellPal + i] (deduplicated in LDS; two waves inserting one record
+// cell's hittable texels in cpal[cell * kCellPalStride + i] (deduplicated in LDS; two waves inserting one record
 // at once may both add it -- a wasted entry, never a wrong one), and mf = distRT with every hittable texel's
 // q replaced by its palette entry i (kCellPal: no entry left, the march reads its record from shade).
 template <bool PAL, int NTH = 256>

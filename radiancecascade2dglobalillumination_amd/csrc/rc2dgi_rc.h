@@ -374,9 +374,14 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // as few waves as they fill; the owners read the hit texels back.  Each ray's march is unchanged
   // (same samples, same iteration cap), so the results are too.  P.tailk < 0: every ray left after the
   // miss proof goes to the queue at once (no lockstep iterations).
-  __shared__ uint2 s_q[TLC ? NT * NR : 1];
+#ifdef RC2DGI_EXP_EB
+  constexpr bool EB = TLC;
+#else
+  constexpr bool EB = false;
+#endif
+  __shared__ uint2 s_q[(TLC && !EB) ? NT * NR : 1];
   __shared__ unsigned s_qn;
-  const bool tl = TLC && P.tailk != 0;
+  const bool tl = TLC && !EB && P.tailk != 0;
 #ifdef RC2DGI_DIAG_LDS_PAD  // diagnostic build: one workgroup per CU (LDS-limited residency)
   __shared__ unsigned s_pad[RC2DGI_DIAG_LDS_PAD];
   if (P.level == 99) s_pad[threadIdx.x] = 0u;
@@ -488,6 +493,27 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
   };
   if constexpr (!Z0) stage_loads();
+  // the staged footprint to LDS (after the march, or -- EB -- before the workgroup's only barrier)
+  auto stage_write = [&]() {
+    if (STG) {
+#pragma unroll
+      for (int j = 0; j < DPW; ++j) {
+#pragma unroll
+        for (int q = 0; q < QPD; ++q) {
+          const int e = lane + 64 * (wch + WPD * q), t = j * QPD + q;
+          const int k = (wdir + j * NW) * FP + e;
+          if ((WPD == 1 && 64 * (q + 1) <= FP) || e < FP) {
+            if constexpr (NWD == 1)
+              s_up[k] = GI::stage(stx[t], 0u, 0u, 0u);
+            else if constexpr (NWD == 2)
+              s_up[k] = GI::stage(stx[t], sty[t], 0u, 0u);
+            else
+              s_up[k] = GI::stage(stx[t], sty[t], stz[t], stw[t]);
+          }
+        }
+      }
+    }
+  };
 
   const float cxf = (float)cx;
   const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);  // rayOrigin / _CascadeResolution
@@ -543,13 +569,14 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // The bound table to LDS and the workgroup barrier, as late as their first use: the table's load was
   // issued first (vmcnt retires in order, so this waits for it only, not for the staging loads in
   // flight over the march), and its latency overlaps the ray setup above.
-  if (cm || dp || tl) {
+  if (cm || dp || tl || (EB && STG)) {
     if (cm || dp) {
 #pragma unroll
       for (int j = 0; j < CPT; ++j)
         if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4)
           reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
     }
+    if (EB) stage_write();
 #ifdef RC2DGI_DIAG_TIMING
     if (cm || dp)  // (diagnostic: the table's words have arrived -- not the staging loads behind them)
       for (int j = 0; j < CPT; ++j) asm volatile("" ::"v"(cmv[j].x), "v"(cmv[j].w));
@@ -603,6 +630,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #endif
 #ifdef RC2DGI_DIAG_STATS
   unsigned diag_slots = 0, diag_samples = 0;
+  bool diag_sampled[NR];
+  for (int k = 0; k < NR; ++k) diag_sampled[k] = false;
 #endif
   constexpr int it0 = Z0 ? 1 : 0;
   if constexpr (Z0) {
@@ -749,6 +778,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #ifdef RC2DGI_DIAG_STATS
     diag_slots += NR;
     for (int k = 0; k < NR; ++k) diag_samples += live[k] ? 1u : 0u;
+    for (int k = 0; k < NR; ++k) diag_sampled[k] = diag_sampled[k] || live[k];
 #endif
     unsigned q[NR];
     if constexpr (PACKED) {
@@ -798,6 +828,15 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     atomicAdd(&P.stats[P.level * 3 + 0], (unsigned long long)diag_slots);
     atomicAdd(&P.stats[P.level * 3 + 1], (unsigned long long)diag_samples);
     if ((threadIdx.x & 63) == 0) atomicAdd(&P.stats[P.level * 3 + 2], 1ull);
+    // [64 + 4 level]: rays with >= 1 sample, probes (lanes) with one, waves with one, rays ending in a hit
+    unsigned nr = 0, nh = 0;
+    for (int k = 0; k < NR; ++k) nr += diag_sampled[k] ? 1u : 0u;
+    for (int k = 0; k < NR; ++k) nh += hit_idx[k] >= 0 ? 1u : 0u;
+    atomicAdd(&P.stats[64 + P.level * 4 + 0], (unsigned long long)nr);
+    atomicAdd(&P.stats[64 + P.level * 4 + 1], nr ? 1ull : 0ull);
+    const bool wany = __any(nr != 0u);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&P.stats[64 + P.level * 4 + 2], wany ? 1ull : 0ull);
+    atomicAdd(&P.stats[64 + P.level * 4 + 3], (unsigned long long)nh);
   }
 #endif
 
@@ -895,25 +934,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   RC_TSTAMP(6);
   RC_SECTION("stage_write");
-  if (STG) {
-#pragma unroll
-    for (int j = 0; j < DPW; ++j) {
-#pragma unroll
-      for (int q = 0; q < QPD; ++q) {
-        const int e = lane + 64 * (wch + WPD * q), t = j * QPD + q;
-        const int k = (wdir + j * NW) * FP + e;
-        if ((WPD == 1 && 64 * (q + 1) <= FP) || e < FP) {
-          if constexpr (NWD == 1)
-            s_up[k] = GI::stage(stx[t], 0u, 0u, 0u);
-          else if constexpr (NWD == 2)
-            s_up[k] = GI::stage(stx[t], sty[t], 0u, 0u);
-          else
-            s_up[k] = GI::stage(stx[t], sty[t], stz[t], stw[t]);
-        }
-      }
-    }
-  }
-  if (STG || tl) __syncthreads();
+  if (!EB) stage_write();
+  if ((STG && !EB) || tl) __syncthreads();
   if (tl) {  // hit texels of this lane's rays that finished in the tail
 #pragma unroll
     for (int k = 0; k < NR; ++k)

@@ -25,6 +25,12 @@ def main():
     L.rc2dgi_diag_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
     ctx = RC2DGI(W, W, cascade_count=N, ray_range=rr)
     ctx.set_tuning("rc_skip", skip)
+    sched = os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning", f"{W}x{W}_N{N}_rr{rr:g}_f32.json")
+    if os.path.exists(sched):  # the committed schedule (tile shapes set the wave composition)
+        tun = json.load(open(sched))
+        for lv in range(N):
+            ctx.set_tuning(f"rc_order_L{lv}", tun["rc_order"][lv])
+            ctx.set_tuning(f"rc_variant_L{lv}", tun["rc_variant"][lv])
     c, e = scenes.demo(W, W)
     ctx.upload("color", c)
     ctx.upload("emissive", e)
@@ -42,6 +48,10 @@ def main():
         out[f"L{lv}"] = {"samples_per_ray": round(samples / rays, 3), "slot_iters_per_ray": round(slots / rays, 3),
                          "lockstep_efficiency": round(samples / max(slots, 1), 3),
                          "wave_iterations": round(slots / max(waves * 64 * 4, 1), 2)}
+        b = buf.reshape(-1)[64 + 4 * lv:64 + 4 * lv + 4]
+        out[f"L{lv}"].update({"rays_sampled": round(int(b[0]) / rays, 4), "probes_sampled": round(int(b[1]) / (W * W), 4),
+                              "waves_sampled": round(int(b[2]) / max(waves, 1), 4),
+                              "rays_hit_pre_tail": round(int(b[3]) / rays, 4)})
     print(json.dumps({"size": W, "N": N, "ray_range": rr, "rc_skip": skip, "levels": out}))
 
 

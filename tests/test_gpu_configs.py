@@ -127,7 +127,11 @@ def check_frame(ctx, p, color, emis, stride=1, what=""):
 def run_config(R, W, H, N, rr, sched, scene):
     from radiancecascade2dglobalillumination_amd import scenes
 
-    color, emis = scenes.demo(W, H) if scene == "demo" else scenes.random_scene(W, H, int(scene.split(":")[1]))
+    if scene == "demo":
+        color, emis = scenes.demo(W, H)
+    else:  # random:<seed> (5 % occluders) or dense:<seed> (bench.py --scene: >= 25 %)
+        kind, seed = scene.split(":")
+        color, emis = scenes.random_scene(W, H, int(seed), coverage={"random": 0.05, "dense": 0.35}[kind])
     p = oracle.Params(W=W, H=H, N=N, ray_range=rr)
     ctx = R.RC2DGI(W, H, cascade_count=N, ray_range=rr)
     if sched is not None:
@@ -149,6 +153,19 @@ def test_committed_bench_schedule_full_size(R, W, N, rr):
     for L in range(N):
         assert ctx.get_tuning(f"rc_variant_L{L}") == sched["rc_variant"][L]
     check_frame(ctx, p, color, emis, stride=1, what=f"{W}^2 N={N} rr={rr:g} committed schedule")
+    ctx.close()
+
+
+@pytest.mark.parametrize("scene", ["random:1", "dense:2"])
+def test_committed_headline_schedule_other_scenes(R, scene):
+    """The headline schedule (4096^2, N=6, rayRange 2; tuned on the demo frame) on scenes it was not tuned
+    on: a random scene (5 % occluders) and a dense one (>= 25 %), every texel of every level and of the
+    merge bit-exact.  The exit proofs, directional proofs, surface palettes and workgroup orders are all
+    content-dependent; the bench times these scenes too (bench.py --scene, profiles/r05/scenes.jsonl)."""
+    W, N, rr = 4096, 6, 2.0
+    sched = committed_schedule(W, W, N, rr)
+    ctx, p, color, emis = run_config(R, W, W, N, rr, sched, scene)
+    check_frame(ctx, p, color, emis, stride=1, what=f"headline schedule on {scene}")
     ctx.close()
 
 

@@ -409,7 +409,8 @@ def test_surface_palettes_are_bit_identical(RC2DGI, scene):
     """rc_pal (per-cell surface palettes and the march field, launch_shade_cmin; the one-probe tiles of the
     plain field read a hit's record from its cell's palette) against the same frame without: every level
     and every output texture bit for bit, at 4096^2 N=6 (the fused records pass needs cells of >= 64
-    texels), with the one-probe variants at L1-L5; the speckled scene overflows the palettes."""
+    texels), with the one-probe variants at L1-L5 (256-, 512- and 1024-lane tiles); the speckled scene
+    overflows the palettes."""
     W = H = 4096
     N = 6
     color, emis = speckled_scene(W, H) if scene == "speckled" else make_scene(scene, W, H)
@@ -417,7 +418,7 @@ def test_surface_palettes_are_bit_identical(RC2DGI, scene):
     ctx.set_keep_levels(True)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
-    for v in (0, 13, 20):
+    for v in (0, 13, 20, 22, 24):  # (22 / 24: the 1024-lane tiles, staged by two waves per direction)
         for L in range(1, N):
             ctx.set_tuning(f"rc_variant_L{L}", v)
         want = {}
@@ -796,4 +797,14 @@ def test_side_tables_match_their_restatement(RC2DGI, scene):
     assert np.array_equal(got.view(np.uint32), rec[ys, xs].view(np.uint32))
     if scene == "speckled":
         assert np.count_nonzero(hittable & (m == 15)) > 0  # palettes overflowed: those hits read shade
+    # a table the last frame did not build is RC2DGI_E_STATE (the buffers outlive the knob that built them)
+    from radiancecascade2dglobalillumination_amd import RC2DGIError
+    ctx.set_tuning("rc_pal", 0)
+    ctx.do_rc2dgi()
+    ctx.sync()
+    for name in ("mfield", "cellpal"):
+        with pytest.raises(RC2DGIError) as ei:
+            ctx.download_table(name)
+        assert ei.value.code == -6, name
+    ctx.download_table("dclr")  # (still built: directional proofs stay on)
     ctx.close()
