@@ -374,14 +374,9 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // as few waves as they fill; the owners read the hit texels back.  Each ray's march is unchanged
   // (same samples, same iteration cap), so the results are too.  P.tailk < 0: every ray left after the
   // miss proof goes to the queue at once (no lockstep iterations).
-#ifdef RC2DGI_EXP_EB
-  constexpr bool EB = TLC;
-#else
-  constexpr bool EB = false;
-#endif
-  __shared__ uint2 s_q[(TLC && !EB) ? NT * NR : 1];
+  __shared__ uint2 s_q[TLC ? NT * NR : 1];
   __shared__ unsigned s_qn;
-  const bool tl = TLC && !EB && P.tailk != 0;
+  const bool tl = TLC && P.tailk != 0;
 #ifdef RC2DGI_DIAG_LDS_PAD  // diagnostic build: one workgroup per CU (LDS-limited residency)
   __shared__ unsigned s_pad[RC2DGI_DIAG_LDS_PAD];
   if (P.level == 99) s_pad[threadIdx.x] = 0u;
@@ -493,7 +488,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
   };
   if constexpr (!Z0) stage_loads();
-  // the staged footprint to LDS (after the march, or -- EB -- before the workgroup's only barrier)
+  // the staged footprint to LDS, after the march
   auto stage_write = [&]() {
     if (STG) {
 #pragma unroll
@@ -569,14 +564,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // The bound table to LDS and the workgroup barrier, as late as their first use: the table's load was
   // issued first (vmcnt retires in order, so this waits for it only, not for the staging loads in
   // flight over the march), and its latency overlaps the ray setup above.
-  if (cm || dp || tl || (EB && STG)) {
+  if (cm || dp || tl) {
     if (cm || dp) {
 #pragma unroll
       for (int j = 0; j < CPT; ++j)
         if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4)
           reinterpret_cast<float4 *>(s_cm)[threadIdx.x + j * NT] = cmv[j];
     }
-    if (EB) stage_write();
 #ifdef RC2DGI_DIAG_TIMING
     if (cm || dp)  // (diagnostic: the table's words have arrived -- not the staging loads behind them)
       for (int j = 0; j < CPT; ++j) asm volatile("" ::"v"(cmv[j].x), "v"(cmv[j].w));
@@ -934,8 +928,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   RC_TSTAMP(6);
   RC_SECTION("stage_write");
-  if (!EB) stage_write();
-  if ((STG && !EB) || tl) __syncthreads();
+  stage_write();
+  if (STG || tl) __syncthreads();
   if (tl) {  // hit texels of this lane's rays that finished in the tail
 #pragma unroll
     for (int k = 0; k < NR; ++k)
