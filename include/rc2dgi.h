@@ -270,12 +270,18 @@ int rc2dgi_plan_group_waits(const rc2dgi_config *cfg, int world, int rank, int s
 int rc2dgi_plan_jfa_window(const rc2dgi_config *cfg, int rank, int world, int step, int *buf, int *row0);
 
 /* Schedule introspection (no GPU): the RC workgroup order `code` (tuning key rc_order_L<n>:
- * px | py << 8 | dg << 16 | mode << 24, mode 0 patches, 1 oriented patches, 2 bands along the
- * rays) over a grid of tiles_x x tiles_y probe tiles of tile_w x tile_h probes and ngrp direction
+ * px | py << 8 | dg << 16 | mode << 24 | lc << 26, mode 0 patches, 1 oriented patches, 2 bands along
+ * the rays; lc the XCD interleave of rc2dgi_plan_wg_map) over a grid of tiles_x x tiles_y probe tiles of tile_w x tile_h probes and ngrp direction
  * groups.  Writes, for logical workgroups 0..n-1, the probe tile and direction group each one
  * traces; returns 0, or a negative status for bad arguments. */
 int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
                       int n);
+/* The device's workgroup map for the same geometry: for dispatched workgroups 0..n-1 (n = tiles_x * tiles_y *
+ * ngrp; the hardware deals them round-robin to the 8 XCDs), the probe tile and direction group each one traces,
+ * after the XCD split of the logical order -- each XCD one contiguous eighth of it, or with code bits 26-30
+ * = lc > 0 chunks of 2^lc consecutive logical workgroups dealt round-robin to the XCDs. */
+int rc2dgi_plan_wg_map(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
+                       int n);
 
 #ifdef __cplusplus
 }

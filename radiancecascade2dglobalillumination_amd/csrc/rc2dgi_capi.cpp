@@ -1138,8 +1138,8 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   // (x2 probes per lane); one probe per lane in 512- and 1024-lane workgroups
   // (RGBA16F / RGBA8 cascades build the 16x16x1 family and three low-level shapes: the other ids would time
   // the default kernel again)
-  const int kVariantsF32[] = {0, 1, 3, 5, 6, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
-  const int kVariantsOther[] = {0, 1, 3, 6, 13, 14, 15, 16, 17, 18, 19};
+  const int kVariantsF32[] = {0, 1, 3, 5, 6, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25};
+  const int kVariantsOther[] = {0, 1, 3, 6, 13, 14, 15, 16, 17, 18, 19, 25};
   const bool f32 = c->storage == RC2DGI_STORAGE_F32;
   const int *kVariants = f32 ? kVariantsF32 : kVariantsOther;
   const int nv = f32 ? (int)(sizeof(kVariantsF32) / sizeof(int)) : (int)(sizeof(kVariantsOther) / sizeof(int));
@@ -1150,6 +1150,19 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   // which distRT copy a variant reads (0: none, 1 tiled, 2 packed, 3 nibble): the copy is built once per frame and
   // timed with the top level, so the per-level picks below do not see it
   auto copy_kind = [](int v) { return rc_variant_tiled(v) ? 1 : rc_variant_packed(v) ? 2 : rc_variant_nib(v) ? 3 : 0; };
+  // per level the kTop fastest (time, order, variant) of stage 1, for the XCD interleave stage below
+  constexpr int kTop = 4;
+  struct Cand {
+    float t;
+    int order, variant;
+  };
+  std::vector<std::vector<Cand>> top(c->N);
+  auto keep_top = [&](int L, float t, int o, int v) {
+    auto &T = top[L];
+    T.push_back({t, o, v});
+    std::sort(T.begin(), T.end(), [](const Cand &a, const Cand &b) { return a.t < b.t; });
+    if ((int)T.size() > kTop) T.pop_back();
+  };
   for (int k = 0; k < nv * nc; ++k) {
     const int v = kVariants[k / nc], o = k % nc;
     for (int L = 0; L < c->N; ++L) {
@@ -1169,6 +1182,7 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
         for (int L = 0; L < c->N; ++L) acc[L] = std::min(acc[L], lv[L]);
     }
     for (int L = 0; L < c->N; ++L) {
+      keep_top(L, acc[L], c->rc_order[L], c->rc_variant[L]);
       if (acc[L] < best[L]) {
         best[L] = acc[L];
         pick[L] = c->rc_order[L];
@@ -1178,6 +1192,43 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
         bestp[L] = acc[L];
         pickp[L] = c->rc_order[L];
         pickpv[L] = c->rc_variant[L];
+      }
+    }
+  }
+  // Stage 2, the XCD interleave (order code bits 26-30, rc2dgi_plan_wg_map): each level's kTop stage-1 picks with
+  // chunks of 2^lc logical workgroups dealt round-robin to the XCDs.  A level's march cost follows the
+  // occluders; a contiguous eighth of the order per XCD leaves the XCDs unevenly loaded (4096^2 N=6 demo:
+  // L4 0.445 -> 0.389 ms, profiles/r05/ab/xcd_interleave_grid.jsonl).
+  for (int rank = 0; rank < kTop; ++rank) {
+    for (int lc = 1; lc <= 9; ++lc) {
+      for (int L = 0; L < c->N; ++L) {
+        const Cand &cd = top[L][std::min(rank, (int)top[L].size() - 1)];
+        c->rc_order[L] = (cd.order & ~(31 << 26)) | (lc << 26);
+        c->rc_variant[L] = cd.variant;
+      }
+      std::vector<float> acc(c->N, 1e30f);
+      for (int f = 0; f <= frames; ++f) {
+        int rc = rc2dgi_do(c);
+        if (rc == RC2DGI_OK) rc = rc2dgi_pass_times(c, nullptr, 0, lv.data(), c->N);
+        if (rc != RC2DGI_OK) {
+          c->timing = timing;
+          return rc;
+        }
+        if (f > 0)
+          for (int L = 0; L < c->N; ++L) acc[L] = std::min(acc[L], lv[L]);
+      }
+      for (int L = 0; L < c->N; ++L) {
+        const int v = c->rc_variant[L];
+        if (acc[L] < best[L]) {
+          best[L] = acc[L];
+          pick[L] = c->rc_order[L];
+          pickv[L] = v;
+        }
+        if (copy_kind(v) == 0 && acc[L] < bestp[L]) {
+          bestp[L] = acc[L];
+          pickp[L] = c->rc_order[L];
+          pickpv[L] = v;
+        }
       }
     }
   }
@@ -1410,6 +1461,14 @@ int rc2dgi_plan_order(int code, int tiles_x, int tiles_y, int tile_w, int tile_h
       n > tiles_x * tiles_y * ngrp || (n && (!tiles || !groups)))
     return RC2DGI_E_ARG;
   return rc_order_plan(code, tiles_x, tiles_y, tile_w, tile_h, ngrp, tiles, groups, n);
+}
+
+int rc2dgi_plan_wg_map(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
+                      int n) {
+  if (tiles_x <= 0 || tiles_y <= 0 || tile_w <= 0 || tile_h <= 0 || ngrp <= 0 || n < 0 ||
+      n > tiles_x * tiles_y * ngrp || (n && (!tiles || !groups)))
+    return RC2DGI_E_ARG;
+  return rc_wg_map_plan(code, tiles_x, tiles_y, tile_w, tile_h, ngrp, tiles, groups, n);
 }
 
 int rc2dgi_plan_jfa_exchange(const rc2dgi_config *cfg, int world, int step, int *info, int *xfers, int max_xfers) {

@@ -155,6 +155,8 @@ hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned shor
 // 0..n-1 -> (tile, direction group), tiles of tile_w x tile_h probes
 int rc_order_plan(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
                   int n);
+int rc_wg_map_plan(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
+                  int n);
 
 int rc_variant_count();
 const char *rc_variant_name(int v);

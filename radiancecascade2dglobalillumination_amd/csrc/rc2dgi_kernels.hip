@@ -1317,6 +1317,22 @@ static std::vector<uint2> rc_logical_order(int code, int tiles_x, int tiles_y, i
   return out;
 }
 
+// XCD interleave of the logical order (order code bits 26-30 = lc > 0): chunks of 2^lc consecutive logical
+// workgroups are dealt round-robin to the 8 XCDs, so every XCD works over the whole frame instead of one
+// eighth of it (xcd_logical_id: a contiguous eighth each -- the occluders, hence the march, are not spread
+// evenly over those eighths); a chunk keeps its locality in one L2.  Whole rounds of 8 chunks only; the
+// remainder keeps the contiguous split.  A bijection for any n.
+static int xcd_chunk_logical(int p, int n, int lc) {
+  if (lc == 0) return xcd_logical_id(p, n);
+  const long long C = 1ll << lc, round = 8 * C;
+  const int full = (int)((long long)n / round * round);
+  if (p < full) {
+    const int x = p & 7, s = p >> 3;
+    return (int)(((long long)(s >> lc)) * round + (long long)x * C + (s & (C - 1)));
+  }
+  return full + xcd_logical_id(p - full, n - full);
+}
+
 // the host-built workgroup map for one launch geometry (built once, then reused): physical
 // workgroup -> XCD chunk of the logical order (xcd_logical_id) -> (tile x | y << 16, group)
 const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int ngrp, int code, int tile_w,
@@ -1324,7 +1340,7 @@ const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int
   if (!cache) return nullptr;
   {  // an order code that does not tile this geometry runs tile-major: share the code-0 map
     const int opx = code & 0xFF, opy = (code >> 8) & 0xFF, odg = (code >> 16) & 0xFF;
-    if (odg <= 0 || opx <= 0 || opy <= 0 || ngrp % odg) code = 0;
+    if (odg <= 0 || opx <= 0 || opy <= 0 || ngrp % odg) code &= 31 << 26;  // (keeps the XCD interleave)
   }
   for (auto &e : cache->entries)
     if (e.nwg == nwg && e.tiles_x == tiles_x && e.tiles_y == tiles_y && e.ngrp == ngrp && e.code == code &&
@@ -1333,8 +1349,9 @@ const uint2 *rc_wg_map(RcMapCache *cache, int nwg, int tiles_x, int tiles_y, int
   const std::vector<uint2> lo = rc_logical_order(code, tiles_x, tiles_y, ngrp, tile_w, tile_h);
   if ((int)lo.size() != nwg) return nullptr;
   std::vector<uint2> m(nwg);
+  const int lc = (code >> 26) & 31;  // XCD interleave (order code bits 26-30, xcd_chunk_logical)
   for (int p = 0; p < nwg; ++p) {
-    const uint2 v = lo[xcd_logical_id(p, nwg)];
+    const uint2 v = lo[xcd_chunk_logical(p, nwg, lc)];
     const int ty = (int)v.x / tiles_x, tx = (int)v.x - ty * tiles_x;
     m[p] = make_uint2((unsigned)tx | ((unsigned)ty << 16), v.y);
   }
@@ -1357,7 +1374,7 @@ static const char *kRcVariantNames[] = {"16x16x1", "16x8x2",   "16x16x2",  "32x8
                                         "8x8x1",   "32x8x2",   "16x16x1d2", "16x16x1d4", "16x8x1d2",
                                         "32x8x1d2", "16x8x1d4", "8x8x1d4", "16x16x1u", "16x16x1ut", "16x16x1t",
                                         "16x16x1up", "16x16x1un", "16x16x1p", "16x16x1n",
-                                        "32x16x1", "16x32x1", "32x32x1", "32x16x1u", "32x32x1u"};
+                                        "32x16x1", "16x32x1", "32x32x1", "32x16x1u", "32x32x1u", "16x16x1top"};
 int rc_variant_count() { return (int)(sizeof(kRcVariantNames) / sizeof(kRcVariantNames[0])); }
 bool rc_variant_tiled(int v) { return v == 14 || v == 15; }
 bool rc_variant_packed(int v) { return v == 16 || v == 18; }
@@ -1410,7 +1427,9 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
   hipError_t e;
-  if (c.gi_u8)
+  if (a.variant == 25)
+    e = launch_rc_top(a, P, st);  // the barrier-free top level (any storage; elsewhere variant 13)
+  else if (c.gi_u8)
     e = launch_rc_u8(a, P, st);  // RGBA8 cascades: the 16x16x1 family and 16x8x2, 32x8x1, 32x8x2
   else if (c.gi_f16)
     e = launch_rc_f16(a, P, st);  // RGBA16F cascades: the 16x16x1 family and 16x8x2, 32x8x1, 32x8x2
@@ -1581,6 +1600,18 @@ hipError_t launch_dist_tile(const unsigned short *dist, int pitch, unsigned shor
   hipLaunchKernelGGL(k_dist_tile, dim3(ceil_div(tpr, 64), ceil_div(H, 4)), dim3(256), 0, st, dist, pitch, tiled, tpr,
                      W, H);
   return hipGetLastError();
+}
+
+int rc_wg_map_plan(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,
+                   int n) {
+  const std::vector<uint2> lo = rc_logical_order(code, tiles_x, tiles_y, ngrp, tile_w, tile_h);
+  const int nwg = (int)lo.size(), lc = (code >> 26) & 31;
+  for (int p = 0; p < n && p < nwg; ++p) {
+    const uint2 v = lo[xcd_chunk_logical(p, nwg, lc)];
+    tiles[p] = (int)v.x;
+    groups[p] = (int)v.y;
+  }
+  return 0;
 }
 
 int rc_order_plan(int code, int tiles_x, int tiles_y, int tile_w, int tile_h, int ngrp, int *tiles, int *groups,

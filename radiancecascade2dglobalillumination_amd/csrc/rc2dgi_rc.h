@@ -305,6 +305,12 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
   }
 }
 
+// Timing-only ablation builds (-DRC2DGI_DIAG_ABL=bits; WRONG results): 1 sky terms constant, 2 directions and
+// exit terms constant, 4 no proof table (no load, no barrier), 8 workgroup map from blockIdx (tile-major)
+#ifndef RC2DGI_DIAG_ABL
+#define RC2DGI_DIAG_ABL 0
+#endif
+
 // ISA section markers (scripts/isa_mix.py builds with -DRC2DGI_ISA_SECTIONS to split the kernel's
 // instruction mix into staging / march / tail / merge; the product build has none)
 #ifdef RC2DGI_ISA_SECTIONS
@@ -329,6 +335,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   unsigned long long rc_ts[9];
 #endif
   RC_TSTAMP(0);
+#ifdef RC2DGI_DIAG_TIMING
+  unsigned long long rc_rt0 = 0;
+  if (threadIdx.x == 0) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rc_rt0));
+#endif
   constexpr int NT = TX * TY, THY = TY * PY, ND = 4 * PD, NR = ND * PY;
   constexpr bool TILED = DL == 1, PACKED = DL == 2 || DL == 3;
   // plain 16-bit field: the march carries byte offsets into it (twice the texel index; the
@@ -384,7 +394,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
   // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
+#if RC2DGI_DIAG_ABL & 8
+  const uint2 wgm = make_uint2(((blockIdx.x / (unsigned)P.bsc / (unsigned)P.bsc) % (unsigned)P.tiles_x) |
+                                   (((blockIdx.x / (unsigned)P.bsc / (unsigned)P.bsc) / (unsigned)P.tiles_x) << 16),
+                               blockIdx.x % (unsigned)(P.bsc * P.bsc / PD));
+#else
   const uint2 wgm = ld_uniform(P.wg_map + blockIdx.x);
+#endif
   const int tx = (int)(wgm.x & 0xFFFFu), ty = (int)(wgm.x >> 16), dgi = (int)wgm.y;
 #ifdef RC2DGI_DIAG_TIMING
   asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(wgm.x), "s"(wgm.y));  // the map has arrived
@@ -403,8 +419,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // than s cells (kclr = cell texels / texels per unit t).  The test of a ray's first sample proves most
   // misses before any gather (at L4 on the demo scene 72 % of the rays; samples per ray 2.10 -> 1.24 with
   // the per-sample test, scripts/dirproof_model.py).
-  const bool dp = TLC && P.dclr != nullptr;
-  const bool cm = CMS && P.cmin != nullptr && !dp;
+  const bool dp = TLC && P.dclr != nullptr && !(RC2DGI_DIAG_ABL & 4);
+  const bool cm = CMS && P.cmin != nullptr && !dp && !(RC2DGI_DIAG_ABL & 4);
   // (one bin per workgroup: bi0 * kDirBins / 4^L, exact for 4^L >= kDirBins; as a shift, since the product
   // overflows 32 bits from level 13 on)
   static_assert(kDirBins == 64, "the bin shift below assumes 64 = 4^3 bins");
@@ -526,7 +542,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   float rdx[ND], rdy[ND];
 #pragma unroll
   for (int r = 0; r < ND; ++r) {
+#if RC2DGI_DIAG_ABL & 2
+    const float2 d = make_float2(0.6f + 0.01f * (float)r, 0.8f - 0.01f * (float)(bi0 & 7));
+#else
     const float2 d = ld_uniform(dirs + bi0 * 4 + r);
+#endif
     rdx[r] = d.x;
     rdy[r] = d.y;
     if constexpr (TLC) {  // VGPR copies: the wave-uniform directions otherwise pin 8 SGPRs over the march
@@ -675,7 +695,12 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       struct E4 {
         float4 e[4];
       };
+#if RC2DGI_DIAG_ABL & 2
+      E4 e4;
+      for (int k = 0; k < 4; ++k) e4.e[k] = make_float4(1.5f, 1.5f, 1.0f + 0.001f * (float)k, 1.0f);
+#else
       const E4 e4 = ld_uniform(reinterpret_cast<const E4 *>(P.dexit + bi0 * 4));  // one 64-byte scalar load
+#endif
 #pragma unroll
       for (int k = 0; k < NR; ++k) tend[k] = exit_bound(t1n, dp || P.cscr, e4.e[k % ND], ox, oy[k / ND]);
     }
@@ -1029,7 +1054,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
             rad.z = rad.z + up.z * rad.w;
             rad.w = rad.w * up.w;
           } else {
+#if RC2DGI_DIAG_ABL & 1
+            const float4 sk = make_float4(0.1f * (float)(ai & 3), 0.2f, 0.3f, 0.0f);
+#else
             const float4 sk = ld_uniform(sky + ai);  // top cascade: analytic sky, tabulated per angleIndex
+#endif
             rad.x = rad.x + sk.x;
             rad.y = rad.y + sk.y;
             rad.z = rad.z + sk.z;
@@ -1047,6 +1076,16 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
 #ifdef RC2DGI_DIAG_TIMING
   RC_TSTAMP(8);
+  if (threadIdx.x == 0 && P.level < 6) {
+    // per XCD (hardware XCC_ID): the last workgroup end and (inverted) the first start on the global 100 MHz
+    // clock, rows 8 + level of the [16][16] table: the spread of the XCDs' finishing times is the imbalance
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    unsigned long long rt;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt));
+    atomicMax(&P.stats[(8 + P.level) * 16 + (xcc & 7)], rt);
+    atomicMax(&P.stats[(8 + P.level) * 16 + 8 + (xcc & 7)], ~rc_rt0);
+  }
   if ((threadIdx.x & 63) == 0) {  // spread over kDiagSlots copies (one hot address would serialize the atomics)
     unsigned long long *st = P.stats + 256 + ((size_t)(blockIdx.x * (TX * TY / 64) + (threadIdx.x >> 6)) % kDiagSlots) * 256;
     for (int i = 0; i < 8; ++i) atomicAdd(&st[P.level * 16 + i], rc_ts[i + 1] - rc_ts[i]);
@@ -1116,5 +1155,6 @@ hipError_t launch_rc_f32_unrolled(const RcLevelArgs &a, RcParams P, hipStream_t 
 hipError_t launch_rc_f32_wide(const RcLevelArgs &a, RcParams P, hipStream_t st);
 hipError_t launch_rc_f16(const RcLevelArgs &a, RcParams P, hipStream_t st);
 hipError_t launch_rc_u8(const RcLevelArgs &a, RcParams P, hipStream_t st);
+hipError_t launch_rc_top(const RcLevelArgs &a, RcParams P, hipStream_t st);  // variant 25 (rc2dgi_rc_top.hip)
 
 }  // namespace rc2dgi

@@ -62,6 +62,16 @@ def main():
         out["levels"][f"L{lv}"] = {"ms": round(lv_ms[lv], 4), "waves": waves, "cycles_per_wave": cyc}
         print(f"L{lv} {lv_ms[lv]:.3f} ms waves {waves}: " + " ".join(f"{s} {cyc[s]:.0f}" for s in SECTIONS + ['total']),
               file=sys.stderr)
+    # per XCD: first workgroup start / last end on the 100 MHz clock (rows 8 + level), relative to the level's start
+    for lv in range(min(N, 6)):
+        row = buf[8 + lv]
+        ends = [int(row[x]) for x in range(8)]
+        starts = [(~int(row[8 + x])) & 0xFFFFFFFFFFFFFFFF for x in range(8)]
+        if min(ends) == 0:
+            continue
+        span = [round((e - s0) / 100.0, 2) for e, s0 in zip(ends, starts)]  # us, each on its own XCD's clock
+        out["levels"][f"L{lv}"]["xcd_span_us"] = span
+        print(f"L{lv} XCD span first start -> last end (us): {span}", file=sys.stderr)
     print(json.dumps(out), flush=True)
     ctx.close()
 

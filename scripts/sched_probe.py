@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--tune", action="append", default=[])
+    ap.add_argument("--xcd-chunks", default="", help="comma list of log2 XCD interleave chunks (order code bits 26-30) "
+                    "to combine with every order candidate (0 = the contiguous split)")
     ap.add_argument("cands", nargs="+")
     a = ap.parse_args()
     import bench
@@ -62,10 +64,14 @@ def main():
         L, vs, os_ = c.split(":")
         L = int(L)
         ol = [str(x) for x in autotune_orders()] if os_ == "all" else os_.split(",")
-        for v, o in itertools.product(vs.split(","), ol):
+        chunks = [int(x) for x in a.xcd_chunks.split(",")] if a.xcd_chunks else [None]
+        for v, o, lc in itertools.product(vs.split(","), ol, chunks):
             v = tun["rc_variant"][L] if v == "c" else int(v)
             o = tun["rc_order"][L] if o == "c" else int(o)
-            per_level.setdefault(L, []).append((v, o))
+            if lc is not None:
+                o = (o & ~(31 << 26)) | (lc << 26)
+            if (v, o) not in per_level.setdefault(L, []):
+                per_level[L].append((v, o))
     times = {(L, v, o): [] for L, cs in per_level.items() for v, o in cs}
     for _ in range(a.rounds):
         for L, cs in per_level.items():

@@ -144,6 +144,44 @@ def test_rc_workgroup_order_is_a_bijection():
         assert len(seen) == n and all(0 <= t < tx * ty and 0 <= d < ng for t, d in seen), (tx, ty, ng, px, py, dg, ori)
 
 
+def _plan_wg_map(lib, code, tx, ty, ng, tw=16, th=16):
+    import ctypes
+
+    n = tx * ty * ng
+    tiles, groups = (ctypes.c_int * n)(), (ctypes.c_int * n)()
+    assert lib.rc2dgi_plan_wg_map(code, tx, ty, tw, th, ng, tiles, groups, n) == 0
+    return list(zip(tiles, groups))
+
+
+def test_xcd_interleaved_workgroup_map_is_a_bijection():
+    """The device map (rc2dgi_plan_wg_map: the XCD split of the logical order, order code bits 26-30 = lc) visits
+    every (tile, direction group) exactly once for any count -- whole rounds of 8 chunks interleaved, the
+    remainder split contiguously -- and lc = 0 is the contiguous split (each XCD, dispatch id mod 8, one eighth)."""
+    import itertools
+
+    from radiancecascade2dglobalillumination_amd import _build, load_library
+
+    _build.build()
+    lib = load_library()
+    for tx, ty, ng, lc, base in itertools.product([1, 3, 8, 16], [1, 5, 16], [1, 4, 64], [0, 1, 2, 5, 9],
+                                                 [0, 4 | 8 << 8 | 4 << 16, 2 | 2 << 8 | 2 << 16 | 1 << 24]):
+        n = tx * ty * ng
+        m = _plan_wg_map(lib, base | lc << 26, tx, ty, ng)
+        assert len(set(m)) == n and all(0 <= t < tx * ty and 0 <= d < ng for t, d in m), (tx, ty, ng, lc, base)
+        lo = _plan_order(lib, base | lc << 26, tx, ty, ng)
+        assert sorted(m) == sorted(lo)
+    # contiguous split: XCD x (dispatch ids x, x + 8, ...) walks logical workgroups [x n / 8, (x + 1) n / 8)
+    tx, ty, ng = 16, 16, 16
+    n = tx * ty * ng
+    lo = _plan_order(lib, 4 | 8 << 8 | 4 << 16, tx, ty, ng)
+    m = _plan_wg_map(lib, 4 | 8 << 8 | 4 << 16, tx, ty, ng)
+    assert [m[p] for p in range(3, n, 8)] == lo[3 * n // 8:4 * n // 8]
+    # interleaved (lc = 4): XCD 3's k-th chunk of 16 is logical chunk 8 k + 3
+    m = _plan_wg_map(lib, 4 | 8 << 8 | 4 << 16 | 4 << 26, tx, ty, ng)
+    x3 = [m[p] for p in range(3, n, 8)]
+    assert x3 == [lo[(k // 16) * 128 + 3 * 16 + k % 16] for k in range(n // 8)]
+
+
 def test_oriented_order_lays_patches_along_the_rays():
     """Oriented order: a chunk of direction groups near the x axis walks px-wide patches, one near
     the y axis px-tall patches (RC level with 16 direction groups, 16 x 16 tiles)."""
