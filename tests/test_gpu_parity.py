@@ -418,7 +418,7 @@ def test_surface_palettes_are_bit_identical(RC2DGI, scene):
     ctx.set_keep_levels(True)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
-    for v in (0, 13, 20, 22, 24):  # (22 / 24: the 1024-lane tiles, staged by two waves per direction)
+    for v in (0, 13, 20, 22, 24, 25):  # (22 / 24: 1024-lane tiles, two waves per direction; 25: k_rc_top at L5)
         for L in range(1, N):
             ctx.set_tuning(f"rc_variant_L{L}", v)
         want = {}
