@@ -21,6 +21,7 @@ def main():
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     rr = float(sys.argv[3]) if len(sys.argv) > 3 else 2.0
     skip = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # tuning rc_skip (exit proofs)
+    scene = sys.argv[5] if len(sys.argv) > 5 else "demo"  # demo | random:<seed> | dense:<seed> (bench.py --scene)
     L = load_library()
     L.rc2dgi_diag_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
     ctx = RC2DGI(W, W, cascade_count=N, ray_range=rr)
@@ -31,7 +32,11 @@ def main():
         for lv in range(N):
             ctx.set_tuning(f"rc_order_L{lv}", tun["rc_order"][lv])
             ctx.set_tuning(f"rc_variant_L{lv}", tun["rc_variant"][lv])
-    c, e = scenes.demo(W, W)
+    if scene == "demo":
+        c, e = scenes.demo(W, W)
+    else:
+        kind, seed = scene.split(":")
+        c, e = scenes.random_scene(W, W, int(seed), coverage={"random": 0.05, "dense": 0.35}[kind])
     ctx.upload("color", c)
     ctx.upload("emissive", e)
     buf = np.zeros((16, 16), np.uint64)
@@ -52,7 +57,7 @@ def main():
         out[f"L{lv}"].update({"rays_sampled": round(int(b[0]) / rays, 4), "probes_sampled": round(int(b[1]) / (W * W), 4),
                               "waves_sampled": round(int(b[2]) / max(waves, 1), 4),
                               "rays_hit_pre_tail": round(int(b[3]) / rays, 4)})
-    print(json.dumps({"size": W, "N": N, "ray_range": rr, "rc_skip": skip, "levels": out}))
+    print(json.dumps({"size": W, "N": N, "ray_range": rr, "rc_skip": skip, "scene": scene, "levels": out}))
 
 
 if __name__ == "__main__":

@@ -62,16 +62,28 @@ def main():
         out["levels"][f"L{lv}"] = {"ms": round(lv_ms[lv], 4), "waves": waves, "cycles_per_wave": cyc}
         print(f"L{lv} {lv_ms[lv]:.3f} ms waves {waves}: " + " ".join(f"{s} {cyc[s]:.0f}" for s in SECTIONS + ['total']),
               file=sys.stderr)
-    # per XCD: first workgroup start / last end on the 100 MHz clock (rows 8 + level), relative to the level's start
-    for lv in range(min(N, 6)):
-        row = buf[8 + lv]
-        ends = [int(row[x]) for x in range(8)]
-        starts = [(~int(row[8 + x])) & 0xFFFFFFFFFFFFFFFF for x in range(8)]
-        if min(ends) == 0:
+    # per-workgroup records (start / end on the 100 MHz clock, XCC id): per XCD the busy span and the summed
+    # workgroup time, each XCD on its own clock
+    L.rc2dgi_diag_raw.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+    raw = np.zeros(8 * (1 << 17) * 2, np.uint64)
+    L.rc2dgi_diag_raw(raw.ctypes.data, raw.size)
+    for lv in range(min(N, 8)):
+        rec = raw[(lv << 17) * 2:((lv + 1) << 17) * 2].reshape(-1, 2)
+        rec = rec[rec[:, 1] != 0]
+        if not len(rec):
             continue
-        span = [round((e - s0) / 100.0, 2) for e, s0 in zip(ends, starts)]  # us, each on its own XCD's clock
-        out["levels"][f"L{lv}"]["xcd_span_us"] = span
-        print(f"L{lv} XCD span first start -> last end (us): {span}", file=sys.stderr)
+        xcc = (rec[:, 0] >> np.uint64(60)).astype(int)
+        t0 = (rec[:, 0] & np.uint64(0xFFFFFFFFFF)).astype(np.int64)
+        t1 = (rec[:, 1] & np.uint64(0xFFFFFFFFFF)).astype(np.int64)
+        spans, busy = [], []
+        for x in range(8):
+            m = xcc == x
+            if m.any():
+                spans.append(round(float(t1[m].max() - t0[m].min()) / 100.0, 1))
+                busy.append(round(float((t1[m] - t0[m]).sum()) / 100.0 / 1000.0, 2))
+        out["levels"][f"L{lv}"]["xcd_span_us"] = spans
+        out["levels"][f"L{lv}"]["xcd_wg_time_ms"] = busy
+        print(f"L{lv} per XCD: span us {spans}  summed workgroup ms {busy}", file=sys.stderr)
     print(json.dumps(out), flush=True)
     ctx.close()
 
