@@ -139,7 +139,7 @@ struct rc2dgi_ctx {
   std::vector<int> rc_noproof;   // per level: no bound table / exit proofs at this level (tuning rc_noproof_L<n>)
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
-  int jfa_coset = 1;             // tuning "jfa_coset": the first four steps in one kernel (k_jfa_coset) where they apply
+  int jfa_coset = 1;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
@@ -817,11 +817,12 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
   hipStream_t st = c->stream;
   if (!c->strip) {
     // the first four steps in one kernel (k_jfa_coset): the ScreenUV mask -> J_3
-    int cs = c->jfa_coset ? jfa_coset_steps(c->sd, c->S) : 0;
+    const int lat = (c->jfa_coset == 2 && c->W <= 4096) ? 32 : 16;  // (the float-key build of lat 32 spills)
+    int cs = c->jfa_coset ? jfa_coset_steps(c->sd, c->S, lat) : 0;
     for (int q = 0; q < cs; ++q)
       if (!plan.jfa[q].is_full()) cs = 0;
     if (t < cs) {
-      if (t == 0) HIPCHK(c, launch_jfa_coset(c->occ, c->mpitch, jfa_out(c, cs - 1), c->sd, st));
+      if (t == 0) HIPCHK(c, launch_jfa_coset(c->occ, c->mpitch, jfa_out(c, cs - 1), c->sd, st, lat));
       return RC2DGI_OK;
     }
     unsigned *out = jfa_out(c, t);
@@ -1659,7 +1660,8 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     return RC2DGI_OK;
   }
   if (k == "jfa_coset") {
-    c->jfa_coset = value != 0;
+    if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "jfa_coset is 0 (off), 1 (4 steps), 2 (5 steps)");
+    c->jfa_coset = value;
     return RC2DGI_OK;
   }
   if (k == "shade_fused") {

@@ -66,8 +66,10 @@ bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTa
 
 // the first four steps in one kernel (k_jfa_coset): 4 where they apply (square power-of-two screens of
 // 512 texels or more), else 0.  launch_jfa_coset reads the ScreenUV mask and writes J_3.
-int jfa_coset_steps(ScreenDims s, int S);
-hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, ScreenDims s, hipStream_t st);
+// (lat 16: steps 0-3 in one kernel; lat 32: steps 0-4)
+int jfa_coset_steps(ScreenDims s, int S, int lat = 16);
+hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, ScreenDims s, hipStream_t st,
+                            int lat = 16);
 
 // device copies of the host-built workgroup maps of k_rc_level, one per launch geometry
 struct RcMapCache {

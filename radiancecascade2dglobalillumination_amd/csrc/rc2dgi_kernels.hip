@@ -388,21 +388,32 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
 // mask (step 0's input), runs the four steps in LDS and writes J_3 -- each texel read and written
 // once, no intermediate image in HBM.  A thread owns texel u of segment a at every lattice row b, so
 // every tap row is a compile-time LDS offset.  Same taps, order and keys as k_jfa_p2.
-constexpr int kCosetW = 32, kCosetL = 16, kCosetPlane = kCosetW * kCosetL;  // segment, lattice side, texels per lattice row
-// threads: one per (segment a, texel u), all 16 lattice rows each (the float keys spill a few row
-// coordinates at 128 VGPRs; splitting the rows over two threads to avoid it measured slower at 8192^2:
-// 0.72 vs 0.58 ms)
-template <bool IKEY> constexpr int coset_threads() { return kCosetPlane; }
-template <bool IKEY>
-__global__ __launch_bounds__(coset_threads<IKEY>()) __attribute__((amdgpu_waves_per_eu(4))) void k_jfa_coset(
+// Lattice side LAT = 16: steps 0-3, a workgroup of 32 residues (one 128-byte segment per lattice point, 32 KB of
+// LDS, 512 threads).  LAT = 32 (round 5): steps 0-4 on a 32 x 32 torus (g = W / 32) whose steps tap +-16 ... 1
+// lattice points, 16 residues per workgroup (64-byte segments, 64 KB of LDS, 1024 threads of 16 rows) -- one
+// more step in LDS instead of a pass over HBM.
+template <int LAT>
+struct CosetGeo {
+  static constexpr int SEG = LAT == 16 ? 32 : 16;    // residues (adjacent texels) per workgroup
+  static constexpr int PLANE = SEG * LAT;             // texels per lattice row of the workgroup
+  static constexpr int NTHR = LAT == 16 ? 512 : 1024;  // LAT 32: two threads per (segment, texel), 16 rows each
+  static constexpr int RT = LAT * PLANE / NTHR;        // lattice rows per thread (16)
+  static constexpr int STEPS = LAT == 16 ? 4 : 5;
+};
+// threads: one per (segment a, texel u) and all (LAT 16) or half (LAT 32) of the lattice rows (the float keys
+// spill a few row coordinates at 128 VGPRs; splitting the rows over two threads to avoid it measured slower at
+// 8192^2: 0.72 vs 0.58 ms)
+template <bool IKEY, int LAT>
+__global__ __launch_bounds__(CosetGeo<LAT>::NTHR) __attribute__((amdgpu_waves_per_eu(4))) void k_jfa_coset(
     const unsigned *__restrict__ mask, int mpitch, unsigned *__restrict__ dst, ScreenDims s, JfaTaps o) {
-  constexpr int RT = kCosetL * kCosetPlane / coset_threads<IKEY>();  // lattice rows per thread
-  __shared__ unsigned img[kCosetL * kCosetPlane];
-  const int g = s.W / kCosetL;  // lattice spacing (host: W == H, g a multiple of kCosetW)
-  const int nx = g / kCosetW;
-  const int x0 = (blockIdx.x % nx) * kCosetW, y0 = blockIdx.x / nx;
-  const int tid = (int)threadIdx.x, col0 = tid & (kCosetPlane - 1), u = tid & (kCosetW - 1), a = col0 >> 5;
-  const int b0 = (tid / kCosetPlane) * RT;  // the thread's first lattice row
+  using G = CosetGeo<LAT>;
+  constexpr int RT = G::RT, SEG = G::SEG, PLANE = G::PLANE;
+  __shared__ unsigned img[LAT * PLANE];
+  const int g = s.W / LAT;  // lattice spacing (host: W == H, g a multiple of SEG)
+  const int nx = g / SEG;
+  const int x0 = (blockIdx.x % nx) * SEG, y0 = blockIdx.x / nx;
+  const int tid = (int)threadIdx.x, col0 = tid & (PLANE - 1), u = tid & (SEG - 1), a = col0 / SEG;
+  const int b0 = __builtin_amdgcn_readfirstlane((tid / PLANE) * RT);  // the thread's first lattice row (per wave)
   const int x = x0 + a * g + u;
   unsigned m[RT];
 #pragma unroll
@@ -411,30 +422,30 @@ __global__ __launch_bounds__(coset_threads<IKEY>()) __attribute__((amdgpu_waves_
 #pragma unroll
   for (int r = 0; r < RT; ++r) {  // ScreenUV seeds (k_jfa_p2<FIRST>)
     const unsigned y = (unsigned)(y0 + (b0 + r) * g);
-    v[r] = ((m[r] >> u) & 1u) ? ((y << 16) | (unsigned)x) : kNoSeed;
-    img[(b0 + r) * kCosetPlane + col0] = v[r];
+    v[r] = ((m[r] >> (x & 31)) & 1u) ? ((y << 16) | (unsigned)x) : kNoSeed;
+    img[(b0 + r) * PLANE + col0] = v[r];
   }
 #pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    const int k = 8 >> st;  // tap offset in lattice points
+  for (int st = 0; st < G::STEPS; ++st) {
+    const int k = (LAT / 2) >> st;  // tap offset in lattice points
     __syncthreads();
     int col[3];
 #pragma unroll
-    for (int dx = 0; dx < 3; ++dx) col[dx] = (((a + (dx - 1) * k) & (kCosetL - 1)) << 5) + u;
+    for (int dx = 0; dx < 3; ++dx) col[dx] = (((a + (dx - 1) * k) & (LAT - 1)) * SEG) + u;
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       unsigned sd[9];
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx) sd[dy * 3 + dx] = img[((b0 + r + (dy - 1) * k) & (kCosetL - 1)) * kCosetPlane + col[dx]];
+        for (int dx = 0; dx < 3; ++dx) sd[dy * 3 + dx] = img[((b0 + r + (dy - 1) * k) & (LAT - 1)) * PLANE + col[dx]];
       float key;
       v[r] = jfa_best9<IKEY>(sd, ((unsigned)(y0 + (b0 + r) * g) << 16) | (unsigned)x, o, &key);
     }
-    if (st < 3) {
+    if (st < G::STEPS - 1) {
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < RT; ++r) img[(b0 + r) * kCosetPlane + col0] = v[r];
+      for (int r = 0; r < RT; ++r) img[(b0 + r) * PLANE + col0] = v[r];
     }
   }
 #pragma unroll
@@ -613,60 +624,85 @@ __global__ __launch_bounds__(NTH) void k_shade_cmin(const unsigned short *__rest
             cl[k] = color[base + (8 * h + k) * rstep];
           }
         }
+        float4 rec[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const bool hit = hm >> (8 * h + k) & 1u;
-          float4 rec = make_float4(e[k].x, e[k].y, e[k].z, 1.0f);
+          rec[k] = make_float4(e[k].x, e[k].y, e[k].z, 1.0f);
           if (!(sqrtf(e[k].x * e[k].x + e[k].y * e[k].y + e[k].z * e[k].z) > 0.0f))
-            rec = make_float4(cl[k].x, cl[k].y, cl[k].z, reflectivity);
-          if (hit) shade[base + (8 * h + k) * rstep] = rec;
-          if (PAL) {
-            // the wave's distinct records of this row, one at a time (usually one: a surface's texels of a
-            // 64-texel run share it): the first remaining lane's record, the lanes holding the same bits,
-            // the entry found or added by lane 0 of the wave
-            unsigned idx = kCellPal;
-            unsigned long long rem = __ballot(hit);
-            while (rem) {
-              const int ld = __ffsll((long long)rem) - 1;
-              const float rx = __shfl(rec.x, ld, 64), ry = __shfl(rec.y, ld, 64), rz = __shfl(rec.z, ld, 64),
-                          rw = __shfl(rec.w, ld, 64);
-              const auto same = [&](float4 v) {
-                return __float_as_uint(v.x) == __float_as_uint(rx) && __float_as_uint(v.y) == __float_as_uint(ry) &&
-                       __float_as_uint(v.z) == __float_as_uint(rz) && __float_as_uint(v.w) == __float_as_uint(rw);
-              };
-              const unsigned long long mine = __ballot(hit && same(rec)) & rem;
-              // the lanes below the palette's fill compare one entry each; lane 0 adds the record if none holds it
-              const unsigned n = min(__builtin_amdgcn_readfirstlane(*(volatile unsigned *)&s_npal), (unsigned)kCellPal);
-              // (an entry counted but not yet written is skipped: at worst the record is added twice)
-              bool hold = false;
-              if ((unsigned)lane < n) {
-                const bool rdy = *(volatile unsigned *)&s_rdy[lane] != 0u;
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-                const volatile float *pe = reinterpret_cast<const volatile float *>(&s_pal[lane]);
-                hold = rdy && same(make_float4(pe[0], pe[1], pe[2], pe[3]));
-              }
-              const unsigned long long found = __ballot(hold);
-              unsigned e_idx;
-              if (found) {
-                e_idx = (unsigned)(__ffsll((long long)found) - 1);
-              } else {
-                unsigned slot = 0;
-                if (lane == 0) {
-                  slot = atomicAdd(&s_npal, 1u);
-                  if (slot < (unsigned)kCellPal) {
-                    s_pal[slot] = make_float4(rx, ry, rz, rw);
-                    gpal[slot] = make_float4(rx, ry, rz, rw);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                    *(volatile unsigned *)&s_rdy[slot] = 1u;
-                  }
-                }
-                e_idx = min((unsigned)__builtin_amdgcn_readfirstlane((int)slot), (unsigned)kCellPal);
-              }
-              if ((mine >> lane) & 1ull) idx = e_idx;
-              rem &= ~mine;
-            }
-            mf[base + (8 * h + k) * rstep] = (unsigned short)(hit ? idx : q[8 * h + k]);
+            rec[k] = make_float4(cl[k].x, cl[k].y, cl[k].z, reflectivity);
+          if (hit) shade[base + (8 * h + k) * rstep] = rec[k];
+        }
+        if (PAL) {
+          // the wave's distinct records of these 8 rows, one at a time (usually one or two: a surface's texels
+          // share it): the first remaining (row, lane)'s record, every (row, lane) holding the same bits, the
+          // entry found or added by lane 0 of the wave -- one round per distinct record, not per row
+          unsigned idx[8];
+          unsigned long long rem[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            idx[k] = kCellPal;
+            rem[k] = __ballot(hm >> (8 * h + k) & 1u);
           }
+          for (;;) {
+            int kk = -1;
+#pragma unroll
+            for (int k = 7; k >= 0; --k) kk = rem[k] ? k : kk;  // (wave-uniform)
+            if (kk < 0) break;
+            unsigned long long rk = rem[0];
+            float4 rv = rec[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k)
+              if (kk == k) {
+                rk = rem[k];
+                rv = rec[k];
+              }
+            const int ld = __ffsll((long long)rk) - 1;
+            const float rx = __shfl(rv.x, ld, 64), ry = __shfl(rv.y, ld, 64), rz = __shfl(rv.z, ld, 64),
+                        rw = __shfl(rv.w, ld, 64);
+            const auto same = [&](float4 v) {
+              return __float_as_uint(v.x) == __float_as_uint(rx) && __float_as_uint(v.y) == __float_as_uint(ry) &&
+                     __float_as_uint(v.z) == __float_as_uint(rz) && __float_as_uint(v.w) == __float_as_uint(rw);
+            };
+            unsigned long long mine[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) mine[k] = __ballot((hm >> (8 * h + k) & 1u) && same(rec[k])) & rem[k];
+            // the lanes below the palette's fill compare one entry each; lane 0 adds the record if none holds it
+            const unsigned n = min(__builtin_amdgcn_readfirstlane(*(volatile unsigned *)&s_npal), (unsigned)kCellPal);
+            // (an entry counted but not yet written is skipped: at worst the record is added twice)
+            bool hold = false;
+            if ((unsigned)lane < n) {
+              const bool rdy = *(volatile unsigned *)&s_rdy[lane] != 0u;
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+              const volatile float *pe = reinterpret_cast<const volatile float *>(&s_pal[lane]);
+              hold = rdy && same(make_float4(pe[0], pe[1], pe[2], pe[3]));
+            }
+            const unsigned long long found = __ballot(hold);
+            unsigned e_idx;
+            if (found) {
+              e_idx = (unsigned)(__ffsll((long long)found) - 1);
+            } else {
+              unsigned slot = 0;
+              if (lane == 0) {
+                slot = atomicAdd(&s_npal, 1u);
+                if (slot < (unsigned)kCellPal) {
+                  s_pal[slot] = make_float4(rx, ry, rz, rw);
+                  gpal[slot] = make_float4(rx, ry, rz, rw);
+                  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                  *(volatile unsigned *)&s_rdy[slot] = 1u;
+                }
+              }
+              e_idx = min((unsigned)__builtin_amdgcn_readfirstlane((int)slot), (unsigned)kCellPal);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              if ((mine[k] >> lane) & 1ull) idx[k] = e_idx;
+              rem[k] &= ~mine[k];
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            mf[base + (8 * h + k) * rstep] = (unsigned short)((hm >> (8 * h + k) & 1u) ? idx[k] : q[8 * h + k]);
         }
       }
     }
@@ -1226,12 +1262,13 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   return hipGetLastError();
 }
 
-int jfa_coset_steps(ScreenDims s, int S) {
-  // steps 0..3 tap +-W/2, W/4, W/8, W/16 on a square power-of-two screen whose lattice spacing W / 16
-  // holds whole 32-texel segments; the four steps must not be the last two (J_{S-2}, J_{S-1} are
-  // visible) nor overlap the fused short steps
-  if (!(s.powW && s.powH) || s.u8 || s.W != s.H || s.W < kCosetL * kCosetW || s.W > 16384 || S < 9) return 0;
-  for (int t = 0; t < 4; ++t) {
+int jfa_coset_steps(ScreenDims s, int S, int lat) {
+  // steps 0 .. log2(lat) - 1 tap +-W/2 ... W/lat on a square power-of-two screen whose lattice spacing W / lat
+  // holds whole segments; the steps must not be the last two (J_{S-2}, J_{S-1} are visible) nor overlap the
+  // fused short steps
+  const int nst = lat == 32 ? 5 : 4, seg = lat == 32 ? CosetGeo<32>::SEG : CosetGeo<16>::SEG;
+  if (!(s.powW && s.powH) || s.u8 || s.W != s.H || s.W < lat * seg || s.W > 16384 || S < nst + 5) return 0;
+  for (int t = 0; t < nst; ++t) {
     float ox[3], oy[3];
     jfa_offsets(s.W, s.H, t, ox, oy);
     JfaTaps tp;
@@ -1239,10 +1276,10 @@ int jfa_coset_steps(ScreenDims s, int S) {
     const int o = s.W >> (t + 1);
     if (tp.dx[0] != -o || tp.dx[2] != o || tp.dy[0] != -o || tp.dy[2] != o) return 0;
   }
-  return 4;
+  return nst;
 }
 
-hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, ScreenDims s, hipStream_t st) {
+hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, ScreenDims s, hipStream_t st, int lat) {
   float ox[3] = {-1.0f, 0.0f, 1.0f}, oy[3] = {-1.0f, 0.0f, 1.0f};
   for (int k = 0; k < 3; ++k) {
     ox[k] /= (float)s.W;
@@ -1250,12 +1287,20 @@ hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, Scr
   }
   JfaTaps tp;
   if (!jfa_p2_taps(s, ox, oy, &tp)) return hipErrorInvalidValue;
-  const int g = s.W / kCosetL;
-  const dim3 grid((g / kCosetW) * g);
-  if (s.W <= 4096)
-    hipLaunchKernelGGL(k_jfa_coset<true>, grid, dim3(coset_threads<true>()), 0, st, mask, mpitch, dst, s, tp);
+#define RC2DGI_COSET(L)                                                                                           \
+  do {                                                                                                            \
+    const int g = s.W / L;                                                                                        \
+    const dim3 grid((g / CosetGeo<L>::SEG) * g);                                                                  \
+    if (s.W <= 4096)                                                                                              \
+      hipLaunchKernelGGL((k_jfa_coset<true, L>), grid, dim3(CosetGeo<L>::NTHR), 0, st, mask, mpitch, dst, s, tp);  \
+    else                                                                                                          \
+      hipLaunchKernelGGL((k_jfa_coset<false, L>), grid, dim3(CosetGeo<L>::NTHR), 0, st, mask, mpitch, dst, s, tp); \
+  } while (0)
+  if (lat == 32)
+    RC2DGI_COSET(32);
   else
-    hipLaunchKernelGGL(k_jfa_coset<false>, grid, dim3(coset_threads<false>()), 0, st, mask, mpitch, dst, s, tp);
+    RC2DGI_COSET(16);
+#undef RC2DGI_COSET
   return hipGetLastError();
 }
 
@@ -1386,7 +1431,7 @@ const char *rc_variant_name(int v) { return (v >= 0 && v < rc_variant_count()) ?
 // the diagnostic counters (one device buffer per process, zeroed when made): [16 levels][16], then (timing
 // builds) kDiagSlots copies of it that rc2dgi_diag_stats sums
 #ifdef RC2DGI_DIAG_TIMING
-constexpr size_t kDiagWords = 256 * (1 + (size_t)kDiagSlots);
+constexpr size_t kDiagWords = kDiagRecBase + ((size_t)8 << 17) * 2;
 #else
 constexpr size_t kDiagWords = 256;
 #endif
@@ -1694,6 +1739,15 @@ hipError_t launch_quantize_u8(float4 *buf, int pitch, int W, int H, hipStream_t 
 }  // namespace rc2dgi
 
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
+#ifdef RC2DGI_DIAG_TIMING
+extern "C" int rc2dgi_diag_raw(unsigned long long *out, long long n) {  // the per-workgroup records (timing builds)
+  hipDeviceSynchronize();
+  unsigned long long *d = rc2dgi::diag_stats_buffer();
+  if (!d) return -3;
+  const size_t m = std::min((size_t)n, rc2dgi::kDiagWords - rc2dgi::kDiagRecBase);
+  return hipMemcpy(out, d + rc2dgi::kDiagRecBase, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+#endif
 extern "C" int rc2dgi_diag_stats(unsigned long long *out, int reset) {  // out: [16][16]
   hipDeviceSynchronize();
   unsigned long long *d = rc2dgi::diag_stats_buffer();
@@ -1702,7 +1756,12 @@ extern "C" int rc2dgi_diag_stats(unsigned long long *out, int reset) {  // out: 
   if (hipMemcpy(h.data(), d, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -3;
   for (int i = 0; i < 256; ++i) {
     unsigned long long s = h[i];
-    for (size_t c = 256 + i; c < h.size(); c += 256) s += h[c];
+#ifdef RC2DGI_DIAG_TIMING
+    const size_t end = rc2dgi::kDiagRecBase;  // (the per-workgroup records follow the table copies)
+#else
+    const size_t end = h.size();
+#endif
+    for (size_t c = 256 + i; c < end; c += 256) s += h[c];
     out[i] = s;
   }
   if (reset && hipMemset(d, 0, h.size() * sizeof(unsigned long long)) != hipSuccess) return -3;

@@ -46,6 +46,7 @@ struct RcParams {
 // counts the wave in stats[level][15] (scripts/rc_timing.py)
 #ifdef RC2DGI_DIAG_TIMING
 constexpr int kDiagSlots = 4096;  // copies of the [16][16] table the waves add into (summed on the host)
+constexpr size_t kDiagRecBase = 256 * (1 + (size_t)kDiagSlots);  // then 2 words per workgroup, 2^17 per level
 #define RC_TSTAMP(i) rc_ts[i] = __builtin_amdgcn_s_memtime()
 #else
 #define RC_TSTAMP(i)
@@ -1076,15 +1077,17 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
 #ifdef RC2DGI_DIAG_TIMING
   RC_TSTAMP(8);
-  if (threadIdx.x == 0 && P.level < 6) {
-    // per XCD (hardware XCC_ID): the last workgroup end and (inverted) the first start on the global 100 MHz
-    // clock, rows 8 + level of the [16][16] table: the spread of the XCDs' finishing times is the imbalance
-    unsigned xcc;
+  if (threadIdx.x == 0 && P.level < 8 && blockIdx.x < (1u << 17)) {
+    // per workgroup (no atomics): XCC_ID, CU id and the start / end on the 100 MHz clock, after the summed
+    // tables (rc2dgi_diag_raw; scripts/rc_timing.py --xcd)
+    unsigned xcc, hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     unsigned long long rt;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt));
-    atomicMax(&P.stats[(8 + P.level) * 16 + (xcc & 7)], rt);
-    atomicMax(&P.stats[(8 + P.level) * 16 + 8 + (xcc & 7)], ~rc_rt0);
+    unsigned long long *rec = P.stats + kDiagRecBase + ((size_t)P.level << 17 | blockIdx.x) * 2;
+    rec[0] = (unsigned long long)(xcc & 15) << 60 | (unsigned long long)(hw & 0xFFFFFu) << 40 | (rc_rt0 & 0xFFFFFFFFFFull);
+    rec[1] = rt;
   }
   if ((threadIdx.x & 63) == 0) {  // spread over kDiagSlots copies (one hot address would serialize the atomics)
     unsigned long long *st = P.stats + 256 + ((size_t)(blockIdx.x * (TX * TY / 64) + (threadIdx.x >> 6)) % kDiagSlots) * 256;

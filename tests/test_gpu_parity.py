@@ -586,15 +586,16 @@ def test_jfa_coset_long_steps_are_bit_identical(RC2DGI, W, H, N, storage):
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
     out = {}
-    for on in (0, 1):
+    for on in (0, 1, 2):  # 2: the first five steps (32 x 32 tori, integer keys; float keys take the 4-step kernel)
         ctx.set_tuning("jfa_coset", on)
         assert ctx.get_tuning("jfa_coset") == on
         ctx.set_tuning("poison", 1)
         ctx.do_rc2dgi()
         ctx.sync()
         out[on] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
-    for k in out[0]:
-        assert np.array_equal(out[0][k], out[1][k]), f"{k}: {np.count_nonzero(out[0][k] != out[1][k])}"
+    for on in (1, 2):
+        for k in out[0]:
+            assert np.array_equal(out[0][k], out[on][k]), f"jfa_coset={on} {k}: {np.count_nonzero(out[0][k] != out[on][k])}"
     ctx.close()
 
 

@@ -24,7 +24,7 @@ def built_variants(storage):
     if storage == "f32":
         return set(range(variant_count()))
     src = open(os.path.join(CSRC, {"f16": "rc2dgi_rc_f16.hip", "rgba8": "rc2dgi_rc_u8.hip"}[storage])).read()
-    return {0} | {int(v) for v in re.findall(r"case (\d+):", src)}
+    return {0, 25} | {int(v) for v in re.findall(r"case (\d+):", src)}  # (25: k_rc_top, every storage)
 
 
 KNOBS = {"rc_pal", "rc_skip", "rc_tail", "rc_wgproof", "jfa_lds", "jfa_coset", "shade_fused", "blur_path"}
@@ -49,7 +49,9 @@ def test_schedule_file_is_well_formed(path):
         for v in e["rc_variant"]:
             assert v in built_variants(storage), f"variant {v} is not built for {storage}"
         for code in e["rc_order"]:
-            px, py, dg, mode = code & 0xFF, (code >> 8) & 0xFF, (code >> 16) & 0xFF, code >> 24
-            assert code == 0 or (px > 0 and py > 0 and dg > 0 and mode in (0, 1, 2)), f"order code {code}"
+            # px | py << 8 | dg << 16 | mode << 24 (0 patches, 1 oriented, 2 bands) | lc << 26 (XCD interleave)
+            px, py, dg, mode, lc = code & 0xFF, (code >> 8) & 0xFF, (code >> 16) & 0xFF, (code >> 24) & 3, code >> 26
+            base = code & ((1 << 26) - 1)
+            assert 0 <= lc <= 31 and (base == 0 or (px > 0 and py > 0 and dg > 0 and mode in (0, 1, 2))), f"order code {code}"
     for k in d.get("knobs", {}):
         assert k in KNOBS or re.match(r"rc_(tail|mp|noproof|order|variant)_L\d+$", k), f"knob {k}"
