@@ -365,6 +365,82 @@ def bench_strips(a, rank, local, world):
         g.close()
 
 
+def strips_launch_check(a, rank, world):
+    """--mode strips --launch-check: the row-strip exchange of one frame rehearsed over the process
+    group without a GPU: every JumpFlood step's transfers of the library's plan (rc2dgi_plan_jfa_exchange) as
+    point-to-point messages carrying the global rows they stand for, checked at the receiver against the plan's
+    window / block layout, and every row the own strip's taps read (JumpFlood.fs, NEAREST + REPEAT) own or
+    delivered; then the distRT strips (all-gather) partition the screen.  Returns a summary dict."""
+    import math
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from radiancecascade2dglobalillumination_amd import rc2dgi as R
+
+    W, H, N = a.size, a.height or a.size, a.cascades
+    (y0, y1), = R.plan_rows(W, H, N, 1.5, rank, world, R.PLAN_MERGE)
+    S = int(math.log(max(W, H)) / math.log(2))  # RC2DGI.cs:290 (double)
+    mx = max(W, H)
+    aspx = np.float32(W) / np.float32(mx)  # peekUV.y = v + y * _Aspect.x * _StepSize (JumpFlood.fs:20)
+    n_xfers = n_rows = 0
+    step = np.float32(0.5)
+    for t in range(1, S):
+        step = np.float32(step * np.float32(0.5))
+        info, xf = R.plan_jfa_exchange(W, H, N, world, t)
+        bufs, row0 = R.plan_jfa_window(W, H, N, rank, world, t)
+
+        def glob(buf, local):  # global row of a local row of this shard's buffer `buf` at step t
+            base = (y0 - info["m"]) if buf == 0 else row0[bufs.index(buf)]
+            return (base + local) % H
+
+        held = set(range(y0, y1))
+        reqs, inbox = [], []
+        for tag, (src, src_row, rows, dst, dst_buf, dst_row) in enumerate(xf):
+            if src == rank:
+                g = [(y0 - info["m"] + src_row + k) % H for k in range(rows)]
+                assert all(y0 <= r < y1 for r in g), f"step {t}: rank {rank} would send rows it does not own"
+                if dst == rank:
+                    assert [glob(dst_buf, dst_row + k) for k in range(rows)] == g, f"step {t}: local copy lands wrong"
+                    held.update(g)
+                else:
+                    reqs.append(dist.isend(torch.tensor(g, dtype=torch.int64), dst, tag=tag))
+                n_xfers += 1
+                n_rows += rows
+            elif dst == rank:
+                buf = torch.empty(rows, dtype=torch.int64)
+                reqs.append(dist.irecv(buf, src, tag=tag))
+                inbox.append((buf, dst_buf, dst_row, rows))
+        for r in reqs:
+            r.wait()
+        for buf, dst_buf, dst_row, rows in inbox:
+            want = [glob(dst_buf, dst_row + k) for k in range(rows)]
+            assert buf.tolist() == want, f"step {t}: rank {rank} received rows {buf.tolist()[:4]} for {want[:4]}"
+            held.update(want)
+        # the rows of J_{t-1} the own strip's taps read (JumpFlood.fs: NEAREST + REPEAT of v + offset)
+        v = (np.arange(y0, y1, dtype=np.float32) + np.float32(0.5)) / np.float32(H)
+        need = set()
+        for k in (-1, 0, 1):
+            x = (v + np.float32(np.float32(np.float32(k) * aspx) * step)).astype(np.float32)
+            if H & (H - 1) == 0:
+                r = np.floor(x * np.float32(H)).astype(np.int64) % H
+            else:
+                f = (x - np.floor(x)).astype(np.float32)
+                r = np.minimum(np.floor(f * np.float32(H)).astype(np.int64), H - 1)
+            need |= set(int(q) for q in r)
+        missing = need - held
+        assert not missing, f"step {t}: rank {rank} taps rows {sorted(missing)[:4]} nobody delivered"
+    strips = [None] * world
+    dist.all_gather_object(strips, (y0, y1))  # the distRT exchange: every shard gets every strip
+    assert sorted(strips)[0][0] == 0 and sorted(strips)[-1][1] == H
+    assert all(p[1] == q[0] for p, q in zip(sorted(strips), sorted(strips)[1:]))
+    tot = torch.tensor([float(n_xfers), float(n_rows)])
+    dist.all_reduce(tot)
+    return {"steps_checked": S - 1, "transfers": int(tot[0]), "rows_exchanged": int(tot[1]),
+            "strips": [list(p) for p in strips]}
+
+
 def spawn_ranks(n):
     """bench.py --gpus N outside torch.distributed.run: run N ranks of this same command line under
     it (one process per GPU, rendezvous on 127.0.0.1) as a child, and return its exit code."""
@@ -450,9 +526,13 @@ def main():
     if a.launch_check:
         rank, local, world = rdist.init(a.backend)
         got = rdist.max_over_ranks([float(rank)], device="cpu" if a.backend == "gloo" else "cuda")
+        extra = {}
+        if a.mode == "strips" and world > 1:
+            extra = {"mode": "strips", "config": f"{a.size}x{a.height or a.size} N={a.cascades}",
+                     **strips_launch_check(a, rank, world)}
         if rank == 0:
             print(json.dumps({"launch_check": True, "n_gpus": world, "pg_world": pg_world(), "backend": a.backend,
-                              "max_rank": int(got[0])}), flush=True)
+                              "max_rank": int(got[0]), **extra}), flush=True)
         finish_pg()
         return 0
 

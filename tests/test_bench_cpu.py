@@ -100,3 +100,17 @@ def test_gpus_n_spawns_n_ranks_over_gloo():
 def test_world_size_mismatch_is_an_error():
     r = _run_bench(["--gpus", "4", "--launch-check", "--backend", "gloo"], {"WORLD_SIZE": "2"}, timeout=60)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_strips_launch_check_world_8_over_gloo():
+    """bench.py --gpus 8 --mode strips --launch-check --backend gloo: eight ranks rehearse the row-strip exchange of a
+    C3 frame (8192^2, N=8) without a GPU -- every JumpFlood step's transfers of the library's plan as point-to-point
+    messages carrying their global rows, checked at the receiver, every tap row of every strip own or delivered,
+    the distRT strips partitioning the screen (bench.strips_launch_check)."""
+    r = _run_bench(["--gpus", "8", "--mode", "strips", "--launch-check", "--backend", "gloo", "--size", "8192",
+                    "--cascades", "8", "--ray-range", "64"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 8 and line["pg_world"] == 8 and line["mode"] == "strips"
+    assert line["steps_checked"] == 12 and line["transfers"] > 0 and line["rows_exchanged"] > 0
+    assert sorted(tuple(p) for p in line["strips"]) == [(1024 * k, 1024 * (k + 1)) for k in range(8)]
