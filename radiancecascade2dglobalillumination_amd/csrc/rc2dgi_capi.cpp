@@ -139,7 +139,7 @@ struct rc2dgi_ctx {
   std::vector<int> rc_noproof;   // per level: no bound table / exit proofs at this level (tuning rc_noproof_L<n>)
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
-  int jfa_coset = 1;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
+  int jfa_coset = 2;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;

@@ -52,6 +52,9 @@ def main():
     ctx.set_timing(True)
     ctx.do_rc2dgi()
     ctx.sync()
+    raw = np.zeros(8 * (1 << 17) * 2, np.uint64)  # the per-workgroup records, before the reset below
+    L.rc2dgi_diag_raw.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+    L.rc2dgi_diag_raw(raw.ctypes.data, raw.size)
     L.rc2dgi_diag_stats(buf.ctypes.data, 1)
     lv_ms = ctx.pass_times(levels=N)["levels"]
     out = {"config": f"{W}x{W} N={N} rr={a.ray_range}", "tune": a.tune, "levels": {}}
@@ -64,9 +67,6 @@ def main():
               file=sys.stderr)
     # per-workgroup records (start / end on the 100 MHz clock, XCC id): per XCD the busy span and the summed
     # workgroup time, each XCD on its own clock
-    L.rc2dgi_diag_raw.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
-    raw = np.zeros(8 * (1 << 17) * 2, np.uint64)
-    L.rc2dgi_diag_raw(raw.ctypes.data, raw.size)
     for lv in range(min(N, 8)):
         rec = raw[(lv << 17) * 2:((lv + 1) << 17) * 2].reshape(-1, 2)
         rec = rec[rec[:, 1] != 0]
