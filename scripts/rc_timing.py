@@ -25,15 +25,17 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--height", type=int, default=0, help="screen height (default: --size)")
     ap.add_argument("--cascades", type=int, default=6)
     ap.add_argument("--ray-range", type=float, default=2.0)
     ap.add_argument("--tune", action="append", default=[])
     a = ap.parse_args()
     W, N = a.size, a.cascades
+    H = a.height or W
     L = load_library()
     L.rc2dgi_diag_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    ctx = RC2DGI(W, W, cascade_count=N, ray_range=a.ray_range)
-    sched = os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning", f"{W}x{W}_N{N}_rr{a.ray_range:g}_f32.json")
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range)
+    sched = os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning", f"{W}x{H}_N{N}_rr{a.ray_range:g}_f32.json")
     if os.path.exists(sched):
         tun = json.load(open(sched))
         for lv in range(N):
@@ -42,7 +44,7 @@ def main():
     for kv in a.tune:
         k, v = kv.split("=")
         ctx.set_tuning(k, int(v))
-    c, e = scenes.demo(W, W)
+    c, e = scenes.demo(W, H)
     ctx.upload("color", c)
     ctx.upload("emissive", e)
     buf = np.zeros((16, 16), np.uint64)
@@ -57,7 +59,7 @@ def main():
     L.rc2dgi_diag_raw(raw.ctypes.data, raw.size)
     L.rc2dgi_diag_stats(buf.ctypes.data, 1)
     lv_ms = ctx.pass_times(levels=N)["levels"]
-    out = {"config": f"{W}x{W} N={N} rr={a.ray_range}", "tune": a.tune, "levels": {}}
+    out = {"config": f"{W}x{H} N={N} rr={a.ray_range}", "tune": a.tune, "levels": {}}
     for lv in range(N):
         waves = int(buf[lv, 15])
         cyc = {s: round(float(buf[lv, i]) / max(waves, 1), 1) for i, s in enumerate(SECTIONS)}
@@ -75,15 +77,28 @@ def main():
         xcc = (rec[:, 0] >> np.uint64(60)).astype(int)
         t0 = (rec[:, 0] & np.uint64(0xFFFFFFFFFF)).astype(np.int64)
         t1 = (rec[:, 1] & np.uint64(0xFFFFFFFFFF)).astype(np.int64)
-        spans, busy = [], []
+        spans, busy, ramp, tail = [], [], [], []
         for x in range(8):
             m = xcc == x
             if m.any():
-                spans.append(round(float(t1[m].max() - t0[m].min()) / 100.0, 1))
-                busy.append(round(float((t1[m] - t0[m]).sum()) / 100.0 / 1000.0, 2))
+                a0, a1 = t0[m], t1[m]
+                spans.append(round(float(a1.max() - a0.min()) / 100.0, 1))
+                busy.append(round(float((a1 - a0).sum()) / 100.0 / 1000.0, 2))
+                # workgroups resident over time (10 ns ticks): the ramp until half the peak, the tail after the
+                # last time it was above half the peak
+                ev = np.concatenate([np.stack([a0, np.ones_like(a0)], 1), np.stack([a1, -np.ones_like(a1)], 1)])
+                ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+                conc = np.cumsum(ev[:, 1])
+                half = conc.max() / 2.0
+                above = np.nonzero(conc >= half)[0]
+                ramp.append(round(float(ev[above[0], 0] - a0.min()) / 100.0, 1))
+                tail.append(round(float(a1.max() - ev[min(above[-1] + 1, len(ev) - 1), 0]) / 100.0, 1))
         out["levels"][f"L{lv}"]["xcd_span_us"] = spans
         out["levels"][f"L{lv}"]["xcd_wg_time_ms"] = busy
-        print(f"L{lv} per XCD: span us {spans}  summed workgroup ms {busy}", file=sys.stderr)
+        out["levels"][f"L{lv}"]["xcd_ramp_us"] = ramp
+        out["levels"][f"L{lv}"]["xcd_tail_us"] = tail
+        print(f"L{lv} per XCD: span us {spans}  summed workgroup ms {busy}  ramp us {ramp}  tail (below half the "
+              f"peak residency) us {tail}", file=sys.stderr)
     print(json.dumps(out), flush=True)
     ctx.close()
 
