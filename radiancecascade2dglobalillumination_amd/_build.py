@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "librc2dgi.so")
 SOURCES = ["rc2dgi_kernels.hip", "rc2dgi_rc_f32a.hip", "rc2dgi_rc_f32b.hip", "rc2dgi_rc_f32c.hip", "rc2dgi_rc_f16.hip",
-           "rc2dgi_rc_u8.hip", "rc2dgi_rc_top.hip", "rc2dgi_capi.cpp", "rc2dgi_shard.cpp", "rc2dgi_paint.hip"]
+           "rc2dgi_rc_u8.hip", "rc2dgi_rc_top.hip", "rc2dgi_rc_chain.hip", "rc2dgi_capi.cpp", "rc2dgi_shard.cpp", "rc2dgi_paint.hip"]
 HEADERS = ["rc2dgi_device.h", "rc2dgi_kernels.h", "rc2dgi_rc.h", "rc2dgi_shard.h", "rc2dgi_paint.h"]
 ARCH = os.environ.get("RC2DGI_OFFLOAD_ARCH", "gfx950")
 

@@ -144,6 +144,9 @@ struct rc2dgi_ctx {
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
   std::vector<float4 *> level_bufs;  // debug copies of G_L
+  int rc_chain = 0;                  // tuning "rc_chain": levels N-2 .. 0 in one launch (1; 2: unrolled march)
+  RcChain *chain = nullptr;          // its argument block and readiness flags (rc2dgi_rc_chain.hip)
+  std::vector<float4 *> chain_bufs;  // per level >= 2: its own G_L (the chain's levels overlap)
   // row-strip sharding
   RcMapCache rc_maps;  // host-built k_rc_level workgroup maps
   PaintBuffers paint_buf;  // rc2dgi_paint primitive setup
@@ -232,8 +235,22 @@ void free_level_bufs(rc2dgi_ctx *c) {
   c->level_bufs.clear();
 }
 
+void free_chain(rc2dgi_ctx *c) {
+  for (float4 *p : c->chain_bufs)
+    if (p) (void)hipFree(p);
+  c->chain_bufs.clear();
+  rc_chain_destroy(c->chain);
+  c->chain = nullptr;
+}
+
+// the cascade chain runs this frame: asked for, f32 cascades, one process (whole levels), >= 3 levels
+bool chain_active(const rc2dgi_ctx *c) {
+  return c->rc_chain && c->storage == RC2DGI_STORAGE_F32 && c->world == 1 && c->N >= 3 && rc_chain_ok(c->N - 1);
+}
+
 void free_buffers(rc2dgi_ctx *c) {
   free_level_bufs(c);
+  free_chain(c);
   c->rc_maps.clear();
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
@@ -348,6 +365,17 @@ int prepare_side_buffers(rc2dgi_ctx *c, bool all = false) {
     HIPCHK(c, alloc(&c->dist_t, (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64 * sizeof(unsigned short)));
   if (packed && p2s && !c->dist_p) HIPCHK(c, alloc(&c->dist_p, dist_packed_bytes(c->W, c->H)));
   if (nib && p2s && !c->dist_n) HIPCHK(c, alloc(&c->dist_n, dist_nib_bytes(c->W, c->H)));
+  if (chain_active(c) && c->chain_bufs.empty()) {  // the chain's own level textures (levels 0 / 1 use giRT1 / 2)
+    c->chain_bufs.assign(c->N, nullptr);
+    for (int L = 2; L < c->N; ++L) {
+      hipError_t e = alloc(&c->chain_bufs[L], (size_t)c->cd.pitch * c->CH * sizeof(float4));
+      if (e != hipSuccess) {
+        free_chain(c);
+        return hip_fail(c, e, "cascade chain textures");
+      }
+    }
+    c->chain = rc_chain_create();
+  }
   const bool pal = c->rc_pal && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch) &&
                    (size_t)c->sd.pitch * c->H <= ((size_t)1 << 26);
   if (pal && (!c->mfield || !c->cell_pal)) {
@@ -867,6 +895,8 @@ int phase1_begin(rc2dgi_ctx *c, const FramePlan &plan) {
     HIPCHK(c, hipMemsetAsync(c->temp, 0xFF, ns * 16, st));
     HIPCHK(c, hipMemsetAsync(c->color_out, 0xFF, ns * 16, st));
     for (float4 *b : {c->gi1, c->gi2, c->gi_spare}) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * gi_bytes(c), st));
+    for (float4 *b : c->chain_bufs)
+      if (b) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * 16, st));
     HIPCHK(c, hipMemsetAsync(c->blur, 0xFF, nc * 16, st));
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[0], st));
@@ -984,16 +1014,29 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   }
   if (mps) HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
   bool gi1final = false;
+  // The cascade chain (tuning rc_chain, rc2dgi_rc_chain.hip): the top level as usual, then levels N-2 .. 0 in one
+  // launch of 16x16x1 tiles, each level into a texture of its own -- level 0 into giRT1 / giRT2 as the loop below
+  // leaves it (N odd: giRT1), level 1 into the other, levels >= 2 into chain_bufs.
+  const bool chain = chain_active(c) && c->chain && (int)c->chain_bufs.size() == c->N;
+  std::vector<RcLevelArgs> chain_args;
+  float4 *const g0 = (c->N % 2) ? c->gi1 : c->gi2, *const g1 = (c->N % 2) ? c->gi2 : c->gi1;
+  auto chain_out = [&](int L) { return L == 0 ? g0 : (L == 1 ? g1 : c->chain_bufs[L]); };
   for (int L = c->N - 1; L >= 0; --L) {
     float4 *srcGI = gi1final ? c->gi1 : c->gi2;
     float4 *dstGI = gi1final ? c->gi2 : c->gi1;
-    if (LT && L + 1 < c->N) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
+    if (chain) {
+      srcGI = L + 1 < c->N ? chain_out(L + 1) : nullptr;
+      dstGI = chain_out(L);
+    }
+    if (LT && L + 1 < c->N && !(chain && L + 2 < c->N)) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
     RcLevelArgs a;
     a.upper = (L == c->N - 1) ? nullptr : srcGI;
     a.out = dstGI;
-    // (palettes: the one-probe tiles of the plain field, rc2dgi_rc.h PALC; level 0 shares its first sample)
-    const bool plain = !rc_variant_tiled(c->rc_variant[L]) && !rc_variant_packed(c->rc_variant[L]) &&
-                       !rc_variant_nib(c->rc_variant[L]) && rc_variant_one_probe(c->rc_variant[L]) && L > 0;
+    // (palettes: the one-probe tiles of the plain field, rc2dgi_rc.h PALC; level 0 shares its first sample; the
+    // chain's levels are 16x16x1 tiles of the plain field)
+    const int var = (chain && L < c->N - 1) ? 0 : c->rc_variant[L];
+    const bool plain = !rc_variant_tiled(var) && !rc_variant_packed(var) && !rc_variant_nib(var) &&
+                       rc_variant_one_probe(var) && L > 0;
     a.dist = (pal && plain) ? c->mfield : c->dist;  // the march field: same samples, hits carry a palette entry
     a.cell_pal = (pal && plain) ? c->cell_pal : nullptr;
     a.shade = c->shade;
@@ -1017,15 +1060,29 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
 
-    for (auto &r : plan.level[L].iv) {
-      a.p0 = r.first;
-      a.p1 = r.second;
-      HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
+    if (chain && L < c->N - 1) {
+      chain_args.push_back(a);  // (whole levels: one process)
+    } else {
+      for (auto &r : plan.level[L].iv) {
+        a.p0 = r.first;
+        a.p1 = r.second;
+        HIPCHK(c, launch_rc_level(a, c->sd, c->cd, st));
+      }
     }
-    if (c->keep_levels)
+    if (c->keep_levels && !chain)
       HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], dstGI, (size_t)c->cd.pitch * c->CH * gi_bytes(c),
                                hipMemcpyDeviceToDevice, st));
     gi1final = !gi1final;
+  }
+  if (chain) {
+    HIPCHK(c, launch_rc_chain(c->chain, chain_args.data(), (int)chain_args.size(), c->sd, c->cd, c->rc_chain == 2 ? 32 : 1, st));
+    // (per-level events: the whole chain counts as level N-2, the levels below it as 0)
+    if (LT)
+      for (int L = c->N - 2; L >= 1; --L) HIPCHK(c, hipEventRecord(c->ev_level[L], st));
+    if (c->keep_levels)
+      for (int L = 0; L < c->N; ++L)
+        HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], chain_out(L), (size_t)c->cd.pitch * c->CH * gi_bytes(c),
+                                 hipMemcpyDeviceToDevice, st));
   }
   if (LT) HIPCHK(c, hipEventRecord(c->ev_level[0], st));
   if (T) HIPCHK(c, hipEventRecord(c->ev[3], st));
@@ -1698,6 +1755,14 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_pal = value != 0;
     return prepare_side_buffers(c);
   }
+  if (k == "rc_chain") {
+    if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "rc_chain is 0 (off), 1 (chain), 2 (chain, unrolled march)");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->rc_chain = value;
+    if (!value) free_chain(c);
+    return prepare_side_buffers(c);
+  }
   if (k.rfind("rc_noproof_L", 0) == 0) {
     const int L = std::atoi(k.c_str() + 12);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
@@ -1769,6 +1834,14 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "rc_pal") {
     *value = c->rc_pal;
+    return RC2DGI_OK;
+  }
+  if (k == "rc_chain") {
+    *value = c->rc_chain;
+    return RC2DGI_OK;
+  }
+  if (k == "rc_chain_timeouts") {  // workgroups of the chain that stopped waiting (synchronises; 0 in a correct run)
+    *value = chain_active(c) && c->chain ? rc_chain_timeouts(c->chain, c->stream) : 0;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_noproof_L", 0) == 0) {

@@ -124,6 +124,19 @@ struct RcLevelArgs {
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
 };
 
+// The cascade chain (rc2dgi_rc_chain.hip, tuning rc_chain): the levels a[0 .. n) (consecutive, from the level
+// below the top down; the top level already written to a[0].upper) in one launch of 16x16x1 tiles (unr: the march
+// unrolled 32 as variant 13, else rolled as variant 0), f32 cascades, whole levels.  Each level's `out` must be a
+// buffer of its own (no level reads what another writes in the same launch).  rc_chain_timeouts: workgroups that
+// stopped waiting for their upper tiles (synchronises the stream; 0 in a correct run).
+struct RcChain;
+RcChain *rc_chain_create();
+void rc_chain_destroy(RcChain *ch);
+bool rc_chain_ok(int nlev);
+hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDims s, CascadeDims c, int unr,
+                           hipStream_t st);
+int rc_chain_timeouts(RcChain *ch, hipStream_t st);
+
 int dist_cmin_shift(int W, int H);
 // hitc (optional): per cell 1 when a texel the march may sample there passes the hit test (the REPEAT wrap of
 // u = 1 / v = 1 onto column / row 0 included in the last cell column / row), else 0

@@ -738,6 +738,22 @@ __global__ __launch_bounds__(NTH) void k_shade_cmin(const unsigned short *__rest
 // A wave per (bin, row of cells), one lane per step: the step's row OR and box, then per cell of the row one
 // ballot of the steps that meet a hit cell: kDirBins x 16 workgroups of 4 rows; the flag grid as one 64-bit
 // word per row in LDS.
+// Transpose of the wave's 64 x 64 bit matrix (row = lane, column = bit): returns to lane c the bits
+// [r] = bit c of lane r's x.  Round k swaps the off-diagonal j x j blocks (j = 32 ... 1) with lane ^ j.
+__device__ __forceinline__ unsigned long long bit_transpose64(unsigned long long x, int lane) {
+  constexpr unsigned long long kLow[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                                          0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int j = 32 >> r;
+    const unsigned long long mlo = kLow[r];
+    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)x, j, 64), hi = (unsigned)__shfl_xor((int)(unsigned)(x >> 32), j, 64);
+    const unsigned long long p = (unsigned long long)hi << 32 | lo;
+    x = (lane & j) ? (x & ~mlo) | ((p & ~mlo) >> j) : (x & mlo) | ((p & mlo) << j);
+  }
+  return x;
+}
+
 __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restrict__ hitc,
                                                    const int4 *__restrict__ boxes,
                                                    unsigned char *__restrict__ dclr) {
@@ -791,13 +807,12 @@ __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restri
     om = ~on;
   }
   hm &= ~om;
-  int clear = 255;
-  for (int cx = 0; cx < D; ++cx) {
-    const unsigned long long hb = __ballot((hm >> cx) & 1ull), ob = __ballot((om >> cx) & 1ull);
-    const int first_hit = hb ? (int)__builtin_ctzll(hb) : NS;
-    const int first_off = min(nsteps, ob ? (int)__builtin_ctzll(ob) : NS);
-    if (lane == cx) clear = first_hit < first_off ? first_hit : 255;
-  }
+  // lane cx: the steps (bits) whose box meets a hit cell / lies off the grid for cell cx -- the 64 x 64 bit
+  // matrices transposed in six shuffle rounds (round 5; was one pair of ballots per cell, 64 rounds)
+  const unsigned long long hb = bit_transpose64(hm, lane), ob = bit_transpose64(om, lane);
+  const int first_hit = hb ? (int)__builtin_ctzll(hb) : NS;
+  const int first_off = min(nsteps, ob ? (int)__builtin_ctzll(ob) : NS);
+  const int clear = first_hit < first_off ? first_hit : 255;
   dclr[(size_t)j * D * D + c] = (unsigned char)clear;
 }
 
@@ -1443,7 +1458,8 @@ unsigned long long *diag_stats_buffer() {
 }
 #endif
 
-hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
+// the level's parameters that do not depend on the tile shape (rc_tile_params adds those)
+RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c) {
   RcParams P;
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   P.stats = diag_stats_buffer();
@@ -1471,6 +1487,11 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
   P.t0 = ((float)start / (float)maxValue) * a.ray_range;
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
+  return P;
+}
+
+hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
+  const RcParams P = rc_level_params(a, s, c);
   hipError_t e;
   if (a.variant == 25)
     e = launch_rc_top(a, P, st);  // the barrier-free top level (any storage; elsewhere variant 13)

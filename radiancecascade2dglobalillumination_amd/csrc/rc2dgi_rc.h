@@ -3,6 +3,8 @@
 // parallel) and by rc2dgi_kernels.hip (decode_dist, the workgroup-order maps).
 #pragma once
 
+#include <type_traits>
+
 #include "rc2dgi_device.h"
 #include "rc2dgi_kernels.h"
 
@@ -40,6 +42,49 @@ struct RcParams {
   unsigned long long *stats;  // diagnostic builds: [16 levels][16] counters (rc2dgi_diag_stats)
 #endif
 };
+
+// the level's parameters that do not depend on the tile shape (rc2dgi_kernels.hip; rc_tile_params adds those)
+RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c);
+
+// The cascade chain (k_rc_level<..., CH = true>, launched by rc2dgi_rc_chain.hip): the levels below the top in
+// one launch, each level's workgroups in a consecutive range of it, upper levels first.
+constexpr int kChainMax = 15;
+constexpr unsigned kChainSpin = 1u << 20;  // polls (s_sleep 2 each) before a workgroup gives up waiting
+struct RcChainLevel {
+  RcParams P;
+  const float4 *upper;
+  float4 *out;
+  const unsigned short *dist;
+  const float4 *shade;
+  const float2 *dirs;
+  unsigned wg0, nwg;        // the level's workgroups in the launch: [wg0, wg0 + nwg)
+  unsigned *flags;          // its readiness flags: slot group * tiles_per_block + tile (nullptr: nobody waits)
+  const unsigned *uflags;   // the upper level's (nullptr: the upper level ran before the launch)
+  int utx, utpb;            // upper level: tiles per block row, tiles per block
+  int pad[2];
+};
+struct RcChainArgs {
+  RcChainLevel lv[kChainMax];
+  unsigned *err;  // workgroups that stopped waiting (rc_chain_timeouts)
+  int n;
+  int pad;
+};
+
+// (block, tile) segments of the upper texture's columns (or rows) [lo, hi) (global, REPEAT-wrapped): up to 6,
+// -1 when there are more
+__device__ __forceinline__ int chain_segments(int lo, int hi, int n, int ub, int T, int *blk, int *tile) {
+  int cnt = 0;
+  int x = lo;
+  while (x < hi && cnt < 6) {
+    const int xw = ((x % n) + n) % n;
+    const int B = xw / ub, lx = xw - B * ub, t = lx / T;
+    blk[cnt] = B;
+    tile[cnt] = t;
+    ++cnt;
+    x += min(min(T - lx % T, ub - lx), n - xw);
+  }
+  return x < hi ? -1 : cnt;
+}
 
 // Diagnostic build (-DRC2DGI_DIAG_TIMING, python _build.py timing): wave-lifetime split of k_rc_level by
 // section, s_memtime stamps; lane 0 of every wave adds the cycles of section i to stats[level][i] and
@@ -320,10 +365,31 @@ __device__ __forceinline__ unsigned fetch_q(const unsigned short *dist, const ui
 #define RC_SECTION(n)
 #endif
 
+// the chain's hand-off forms: 16-byte sc1 buffer loads and stores (offsets in texels, < 2^28)
+typedef int rc_v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rc_rsrc(const void *p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ float4 ld_sc1(const float4 *base, unsigned off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rc_rsrc(base), off << 4, 0, 16));  // aux 16: sc1
+}
+__device__ __forceinline__ void st_sc1(float4 *base, unsigned off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i_t, v), rc_rsrc(base), off << 4, 0, 16);
+}
+
 // DL: distance-field layout the march reads: 0 pitch-linear uint16, 1 8x8-tiled (TILED), 2 packed
 // 14-texel row packets (`dpk`, see kPackTexels; power-of-two screens <= 16384).
 // Z0: level 0 on a power-of-two screen (t0 = 0): the first march iteration is shared by a probe's rays
-template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false>
+// CH: a level of the cascade chain (rc2dgi_rc_chain.hip).  `dpk` then carries the chain's argument block
+// (RcChainArgs) and `sky` the frame's epoch; the workgroup finds its level there (P, the textures), waits until
+// the upper tiles under its staged footprint are written, and publishes its own tile when done.  Hand-off across
+// the XCDs, whose L2s are not coherent (MI355X_MICROARCH, inter-workgroup visibility): every store of a level's
+// output is an sc1 (write-through) store, every storing wave drains (s_waitcnt vmcnt(0)), the barrier, one lane
+// stores the readiness flag (sc1, the epoch); the consumer polls with sc1 loads, the barrier, and every load of
+// the upper level is an sc1 load.  The footprint is widened to whole 128-byte lines, so no line a consumer reads
+// holds texels of a tile it did not wait for.  A poll gives up after kChainSpin tries (counted in the error word):
+// a broken assumption shows as wrong results, never as a hung GPU.
+template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false, bool CH = false>
 __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
@@ -331,6 +397,69 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                      const float2 *__restrict__ dirs,
                                                      const float4 *__restrict__ sky,
                                                      const uint4 *__restrict__ dpk) {
+  static_assert(!CH || (std::is_same<GI, GiF32>::value && !Z0 && !TOP && DL == 0 && PY == 1 && PD == 1),
+                "the chain: f32 one-probe tiles of the plain field below the top level");
+  unsigned wgid = blockIdx.x;
+  unsigned *ch_flag = nullptr;  // (CH) this workgroup's readiness flag
+  unsigned ch_epoch = 0;
+  if constexpr (CH) {
+    const RcChainArgs *C = reinterpret_cast<const RcChainArgs *>(dpk);
+    ch_epoch = (unsigned)reinterpret_cast<unsigned long long>(sky);
+    const int n = ld_uniform(&C->n);
+    int k = 0;
+    for (int q = 1; q < n; ++q) k = blockIdx.x >= ld_uniform(&C->lv[q].wg0) ? q : k;
+    const RcChainLevel *lv = &C->lv[k];
+    P = ld_uniform(&lv->P);
+    wgid = blockIdx.x - ld_uniform(&lv->wg0);
+    upper = ld_uniform(&lv->upper);
+    out = ld_uniform(&lv->out);
+    dist = ld_uniform(&lv->dist);
+    shade = ld_uniform(&lv->shade);
+    dirs = ld_uniform(&lv->dirs);
+    dpk = nullptr;
+    const uint2 m = ld_uniform(P.wg_map + wgid);
+    const int tx = (int)(m.x & 0xFFFFu), ty = (int)(m.x >> 16), dgi = (int)m.y;
+    unsigned *fl = ld_uniform(&lv->flags);
+    if (fl) ch_flag = fl + (unsigned)(dgi * P.tiles_per_block + ty * P.tiles_x + tx);
+    const unsigned *uf = ld_uniform(&lv->uflags);
+    if (uf) {
+      if (threadIdx.x < 64) {
+        // lane j: upper direction r = j / 16, column segment j % 4 and row segment (j / 4) % 4 of that direction's
+        // staged footprint [bx, bx + RW) x [by, by + RH) (below), one texel of margin for the GL path's rounding,
+        // the columns widened to whole 8-texel lines
+        const int lane = (int)threadIdx.x;
+        const int utx = ld_uniform(&lv->utx), utpb = ld_uniform(&lv->utpb);
+        const int ubx = P.bdx >> 1, uby = P.bdy >> 1, umask = 2 * P.bsc - 1, ushift = P.level + 1;
+        const int r = lane >> 4, sx = lane & 3, sy = (lane >> 2) & 3;
+        const int a = dgi * 4 + r;
+        const int bx = (a & umask) * ubx + ((tx * TX) >> 1) - 1, by = (a >> ushift) * uby + ((ty * TY) >> 1) - 1;
+        constexpr int RW = TX / 2 + 2, RH = TY / 2 + 2;
+        int bxs[6], txs[6], bys[6], tys[6];
+        const int ncx = chain_segments((bx - 1) & ~7, (bx + RW + 1 + 7) & ~7, P.c.CW, ubx, TX, bxs, txs);
+        const int ncy = chain_segments(by - 1, by + RH + 1, P.c.CH, uby, TY, bys, tys);
+        const bool all = __any(ncx < 0 || ncy < 0 || ncx > 4 || ncy > 4);  // (other shapes: every upper tile)
+        unsigned timeouts = 0;
+        auto wait_slot = [&](unsigned slot) {
+          unsigned it = 0;
+          while (__hip_atomic_load(uf + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ch_epoch) {
+            if (++it >= kChainSpin) {
+              ++timeouts;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        };
+        if (!all) {
+          if (sx < ncx && sy < ncy) wait_slot((unsigned)((bxs[sx] + bys[sy] * 2 * P.bsc) * utpb + tys[sy] * utx + txs[sx]));
+        } else {
+          const unsigned nup = (unsigned)(4 * P.bsc * P.bsc) * (unsigned)utpb;
+          for (unsigned q = (unsigned)lane; q < nup; q += 64) wait_slot(q);
+        }
+        if (timeouts) atomicAdd(ld_uniform(&C->err), timeouts);
+      }
+      __syncthreads();
+    }
+  }
   RC_SECTION("setup");
 #ifdef RC2DGI_DIAG_TIMING
   unsigned long long rc_ts[9];
@@ -396,11 +525,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   const int ngrp = (P.bsc * P.bsc) / PD;  // direction-block groups
   // one scalar load: XCD remap + workgroup order (rc_order_map), precomputed on the host
 #if RC2DGI_DIAG_ABL & 8
-  const uint2 wgm = make_uint2(((blockIdx.x / (unsigned)P.bsc / (unsigned)P.bsc) % (unsigned)P.tiles_x) |
-                                   (((blockIdx.x / (unsigned)P.bsc / (unsigned)P.bsc) / (unsigned)P.tiles_x) << 16),
-                               blockIdx.x % (unsigned)(P.bsc * P.bsc / PD));
+  const uint2 wgm = make_uint2(((wgid / (unsigned)P.bsc / (unsigned)P.bsc) % (unsigned)P.tiles_x) |
+                                   (((wgid / (unsigned)P.bsc / (unsigned)P.bsc) / (unsigned)P.tiles_x) << 16),
+                               wgid % (unsigned)(P.bsc * P.bsc / PD));
 #else
-  const uint2 wgm = ld_uniform(P.wg_map + blockIdx.x);
+  const uint2 wgm = ld_uniform(P.wg_map + wgid);
 #endif
   const int tx = (int)(wgm.x & 0xFFFFu), ty = (int)(wgm.x >> 16), dgi = (int)wgm.y;
 #ifdef RC2DGI_DIAG_TIMING
@@ -487,7 +616,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
             gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
           }
           const unsigned off = __umul24((unsigned)gy, (unsigned)P.c.pitch) + (unsigned)gx;
-          const typename GI::T v = upper[off];  // issued now, consumed after the march
+          typename GI::T v;  // issued now, consumed after the march
+          if constexpr (CH)
+            v = ld_sc1(upper, off);
+          else
+            v = upper[off];
           const int t = j * QPD + q;
           if constexpr (NWD == 1) {
             stx[t] = v;
@@ -1042,10 +1175,17 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
               } else {
                 // rounding stepped outside the staged footprint: read HBM.  Non-temporal loads
                 // keep the compiler from fusing this path with the LDS path into flat loads.
-                t00 = GI::ld_stage_nt(&upper[(size_t)y0 * P.c.pitch + x0]);
-                t10 = GI::ld_stage_nt(&upper[(size_t)y0 * P.c.pitch + x1]);
-                t01 = GI::ld_stage_nt(&upper[(size_t)y1 * P.c.pitch + x0]);
-                t11 = GI::ld_stage_nt(&upper[(size_t)y1 * P.c.pitch + x1]);
+                if constexpr (CH) {  // (every load of a handed-off level sc1)
+                  t00 = ld_sc1(upper, (unsigned)(y0 * P.c.pitch + x0));
+                  t10 = ld_sc1(upper, (unsigned)(y0 * P.c.pitch + x1));
+                  t01 = ld_sc1(upper, (unsigned)(y1 * P.c.pitch + x0));
+                  t11 = ld_sc1(upper, (unsigned)(y1 * P.c.pitch + x1));
+                } else {
+                  t00 = GI::ld_stage_nt(&upper[(size_t)y0 * P.c.pitch + x0]);
+                  t10 = GI::ld_stage_nt(&upper[(size_t)y0 * P.c.pitch + x1]);
+                  t01 = GI::ld_stage_nt(&upper[(size_t)y1 * P.c.pitch + x0]);
+                  t11 = GI::ld_stage_nt(&upper[(size_t)y1 * P.c.pitch + x1]);
+                }
               }
             }
             const float4 up = GI::bilerp(t00, t10, t01, t11, ux, uy);
@@ -1072,12 +1212,22 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       }
       const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
       const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
-      GI::st(&out[(size_t)j * P.c.pitch + i], GI::blend_black(acc));
+      if constexpr (CH)
+        st_sc1(out, (unsigned)(j * P.c.pitch + i), GI::blend_black(acc));
+      else
+        GI::st(&out[(size_t)j * P.c.pitch + i], GI::blend_black(acc));
+    }
+  }
+  if constexpr (CH) {
+    if (ch_flag) {  // publish: every wave's write-through stores drained, the barrier, one flag
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(ch_flag, ch_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 #ifdef RC2DGI_DIAG_TIMING
   RC_TSTAMP(8);
-  if (threadIdx.x == 0 && P.level < 8 && blockIdx.x < (1u << 17)) {
+  if (threadIdx.x == 0 && P.level < 8 && wgid < (1u << 17)) {
     // per workgroup (no atomics): XCC_ID, CU id and the start / end on the 100 MHz clock, after the summed
     // tables (rc2dgi_diag_raw; scripts/rc_timing.py --xcd)
     unsigned xcc, hw;
@@ -1085,25 +1235,24 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     unsigned long long rt;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt));
-    unsigned long long *rec = P.stats + kDiagRecBase + ((size_t)P.level << 17 | blockIdx.x) * 2;
+    unsigned long long *rec = P.stats + kDiagRecBase + ((size_t)P.level << 17 | wgid) * 2;
     rec[0] = (unsigned long long)(xcc & 15) << 60 | (unsigned long long)(hw & 0xFFFFFu) << 40 | (rc_rt0 & 0xFFFFFFFFFFull);
     rec[1] = rt;
   }
   if ((threadIdx.x & 63) == 0) {  // spread over kDiagSlots copies (one hot address would serialize the atomics)
-    unsigned long long *st = P.stats + 256 + ((size_t)(blockIdx.x * (TX * TY / 64) + (threadIdx.x >> 6)) % kDiagSlots) * 256;
+    unsigned long long *st = P.stats + 256 + ((size_t)(wgid * (TX * TY / 64) + (threadIdx.x >> 6)) % kDiagSlots) * 256;
     for (int i = 0; i < 8; ++i) atomicAdd(&st[P.level * 16 + i], rc_ts[i + 1] - rc_ts[i]);
     atomicAdd(&st[P.level * 16 + 15], 1ull);
   }
 #endif
 }
 
-template <int TX, int TY, int PY, int PD = 1, int UNR = 1, int DL = 0, class GI = GiF32>
-static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
+// The launch geometry and side-table parameters of one level for a TX x (TY * PY) tile of PD direction blocks
+// (launch_rc_tiles, the chain's levels): fills the P fields launch_rc_level leaves, returns the workgroup count
+// (0: no map; DL 1 without its copy: -1).
+template <int TX, int TY, int PY, int PD, int DL>
+static inline int rc_tile_params(const RcLevelArgs &a, RcParams &P) {
   const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
-  if constexpr (DL == 2 || DL == 3) {  // packed field: power-of-two screens up to 16384 wide; same bits either way
-    if (!p2s || P.s.W > 16384) return launch_rc_tiles<TX, TY, PY, PD, UNR, 0, GI>(a, P, st);
-    if (!(DL == 2 ? a.dist_packed : a.dist_nib)) return hipErrorInvalidValue;
-  }
   P.tiles_x = ceil_div(P.bdx, TX);
   const int tiles_y = ceil_div(P.p1 - P.p0, TY * PY);
   P.tiles_per_block = P.tiles_x * tiles_y;
@@ -1112,9 +1261,9 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   // 16-bit fields (<= 32768 probes per axis)
   const int ngrp = P.bsc * P.bsc / PD;
   P.wg_map = rc_wg_map(a.map_cache, nwg, P.tiles_x, tiles_y, ngrp, a.order_code, TX, TY * PY);
-  if (!P.wg_map) return hipErrorOutOfMemory;
+  if (!P.wg_map) return 0;
   P.tpr = DL == 2 ? pack_per_row(P.s.W) : (DL == 3 ? nib_per_row(P.s.W) : (P.s.W + 7) / 8);
-  if (DL == 1 && !a.dist_tiled) return hipErrorInvalidValue;
+  if (DL == 1 && !a.dist_tiled) return -1;
   P.sWf = (float)P.s.W;
   P.sHf = (float)P.s.H;
   P.cmin = reinterpret_cast<const float4 *>(a.cmin);
@@ -1126,7 +1275,7 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   // texels per unit t: the position moves (dir * asp) per unit t, asp = (H, W) / max(W, H), i.e.
   // W H / max(W, H) texels on either axis
   P.kclr = (float)(1 << P.csh) * (float)std::max(P.s.W, P.s.H) / ((float)P.s.W * (float)P.s.H);
-  if (P.cmin && P.cscr && !P.dexit) return hipErrorInvalidValue;
+  if (P.cmin && P.cscr && !P.dexit) return -1;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
   // palettes: the plain field's march (DL 0) on power-of-two screens whose byte offsets fit 27 bits
@@ -1134,6 +1283,19 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   P.lgw = 0;
   while ((1 << P.lgw) < P.s.pitch) ++P.lgw;
   if (P.cpal && (1 << P.lgw) != P.s.pitch) P.cpal = nullptr;
+  return nwg;
+}
+
+template <int TX, int TY, int PY, int PD = 1, int UNR = 1, int DL = 0, class GI = GiF32>
+static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipStream_t st) {
+  const bool p2s = P.s.powW && P.s.powH && P.c.powW && P.c.powH;
+  if constexpr (DL == 2 || DL == 3) {  // packed field: power-of-two screens up to 16384 wide; same bits either way
+    if (!p2s || P.s.W > 16384) return launch_rc_tiles<TX, TY, PY, PD, UNR, 0, GI>(a, P, st);
+    if (!(DL == 2 ? a.dist_packed : a.dist_nib)) return hipErrorInvalidValue;
+  }
+  const int nwg = rc_tile_params<TX, TY, PY, PD, DL>(a, P);
+  if (nwg == 0) return hipErrorOutOfMemory;
+  if (nwg < 0) return hipErrorInvalidValue;
 #define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \
   hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL >= 2 ? 0 : DL)), GI, Z0V>), \
                      dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),   \

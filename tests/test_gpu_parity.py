@@ -599,6 +599,38 @@ def test_jfa_coset_long_steps_are_bit_identical(RC2DGI, W, H, N, storage):
     ctx.close()
 
 
+@pytest.mark.parametrize("W,H,N,rr,scene", [(1200, 900, 6, 2.0, "demo"), (1024, 1024, 6, 2.0, "demo"),
+                                             (333, 200, 4, 8.0, "rand:44"), (4096, 4096, 6, 2.0, "demo")])
+def test_cascade_chain_is_bit_identical(RC2DGI, W, H, N, rr, scene):
+    """The cascade chain (tuning rc_chain, rc2dgi_rc_chain.hip: levels N-2 .. 0 in one launch, a workgroup
+    waiting on the readiness flags of the upper tiles under its footprint, sc1 hand-off) leaves every level G_L,
+    giRT1 / giRT2 and the frame as the level-by-level launches, over two consecutive frames (the flags carry
+    the frame's epoch), rolled and unrolled march, with no workgroup timing out."""
+    color, emis = make_scene(scene, W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
+    ctx.set_keep_levels(True)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for on in (0, 1, 2):
+        ctx.set_tuning("rc_chain", on)
+        assert ctx.get_tuning("rc_chain") == on
+        ctx.set_tuning("poison", 1)
+        for frame in range(2):
+            ctx.do_rc2dgi()
+            ctx.sync()
+            assert ctx.get_tuning("rc_chain_timeouts") == 0
+            out[on, frame] = {k: ctx.download(k) for k in ("gi1", "gi2", "color")}
+            out[on, frame].update({f"G{L}": ctx.download_level(L) for L in range(N)})
+    for on in (1, 2):
+        for frame in range(2):
+            for k in out[0, frame]:
+                a, b = out[0, frame][k], out[on, frame][k]
+                assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), \
+                    f"rc_chain={on} frame {frame} {k}: {np.count_nonzero(a != b)}"
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,N", [(4096, 4096, 6), (8192, 8192, 8)])
 def test_shade_cmin_fused_is_bit_identical(RC2DGI, W, H, N):
     """k_shade_cmin (surface records + the proofs' bound table and hit flags in one pass over distRT,
