@@ -245,7 +245,7 @@ void free_chain(rc2dgi_ctx *c) {
 
 // the cascade chain runs this frame: asked for, f32 cascades, one process (whole levels), >= 3 levels
 bool chain_active(const rc2dgi_ctx *c) {
-  return c->rc_chain && c->storage == RC2DGI_STORAGE_F32 && c->world == 1 && c->N >= 3 && rc_chain_ok(c->N - 1);
+  return c->rc_chain && c->storage == RC2DGI_STORAGE_F32 && c->world == 1 && c->N >= 3 && rc_chain_ok(c->N);
 }
 
 void free_buffers(rc2dgi_ctx *c) {
@@ -1028,13 +1028,13 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
       srcGI = L + 1 < c->N ? chain_out(L + 1) : nullptr;
       dstGI = chain_out(L);
     }
-    if (LT && L + 1 < c->N && !(chain && L + 2 < c->N)) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
+    if (LT && L + 1 < c->N && !(chain && (L + 2 < c->N || c->rc_chain == 4))) HIPCHK(c, hipEventRecord(c->ev_level[L + 1], st));
     RcLevelArgs a;
     a.upper = (L == c->N - 1) ? nullptr : srcGI;
     a.out = dstGI;
     // (palettes: the one-probe tiles of the plain field, rc2dgi_rc.h PALC; level 0 shares its first sample; the
     // chain's levels are 16x16x1 tiles of the plain field)
-    const int var = (chain && L < c->N - 1) ? 0 : c->rc_variant[L];
+    const int var = (chain && (L < c->N - 1 || c->rc_chain == 4)) ? 0 : c->rc_variant[L];
     const bool plain = !rc_variant_tiled(var) && !rc_variant_packed(var) && !rc_variant_nib(var) &&
                        rc_variant_one_probe(var) && L > 0;
     a.dist = (pal && plain) ? c->mfield : c->dist;  // the march field: same samples, hits carry a palette entry
@@ -1060,8 +1060,8 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
 
-    if (chain && L < c->N - 1) {
-      chain_args.push_back(a);  // (whole levels: one process)
+    if (chain && (L < c->N - 1 || c->rc_chain == 4)) {
+      chain_args.push_back(a);  // (whole levels: one process; rc_chain 4: the top level in the launch too)
     } else {
       for (auto &r : plan.level[L].iv) {
         a.p0 = r.first;
@@ -1075,10 +1075,11 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     gi1final = !gi1final;
   }
   if (chain) {
-    HIPCHK(c, launch_rc_chain(c->chain, chain_args.data(), (int)chain_args.size(), c->sd, c->cd, c->rc_chain == 2 ? 32 : 1, st));
-    // (per-level events: the whole chain counts as level N-2, the levels below it as 0)
+    HIPCHK(c, launch_rc_chain(c->chain, chain_args.data(), (int)chain_args.size(), c->sd, c->cd,
+                              c->rc_chain == 2 ? 32 : 1, st, c->rc_chain == 3));
+    // (per-level events: the whole chain counts as its first level, the levels below it as 0)
     if (LT)
-      for (int L = c->N - 2; L >= 1; --L) HIPCHK(c, hipEventRecord(c->ev_level[L], st));
+      for (int L = c->N - (c->rc_chain == 4 ? 1 : 2); L >= 1; --L) HIPCHK(c, hipEventRecord(c->ev_level[L], st));
     if (c->keep_levels)
       for (int L = 0; L < c->N; ++L)
         HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], chain_out(L), (size_t)c->cd.pitch * c->CH * gi_bytes(c),
@@ -1756,7 +1757,8 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     return prepare_side_buffers(c);
   }
   if (k == "rc_chain") {
-    if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "rc_chain is 0 (off), 1 (chain), 2 (chain, unrolled march)");
+    if (value < 0 || value > 4)
+      return fail(c, RC2DGI_E_ARG, "rc_chain is 0 (off), 1 (chain), 2 (unrolled march), 3 (timing experiment), 4 (with the top level)");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->rc_chain = value;

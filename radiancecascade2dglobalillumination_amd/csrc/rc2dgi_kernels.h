@@ -134,7 +134,7 @@ RcChain *rc_chain_create();
 void rc_chain_destroy(RcChain *ch);
 bool rc_chain_ok(int nlev);
 hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDims s, CascadeDims c, int unr,
-                           hipStream_t st);
+                           hipStream_t st, bool tight = false);
 int rc_chain_timeouts(RcChain *ch, hipStream_t st);
 
 int dist_cmin_shift(int W, int H);

@@ -61,7 +61,9 @@ struct RcChainLevel {
   unsigned *flags;          // its readiness flags: slot group * tiles_per_block + tile (nullptr: nobody waits)
   const unsigned *uflags;   // the upper level's (nullptr: the upper level ran before the launch)
   int utx, utpb;            // upper level: tiles per block row, tiles per block
-  int pad[2];
+  int tight;                // experiment (rc_chain 3): wait only for the footprint inside the upper blocks
+  int top;                  // the top level (no upper level: the sky), first in the launch
+  const float4 *sky;        // (the top level's sky terms)
 };
 struct RcChainArgs {
   RcChainLevel lv[kChainMax];
@@ -398,10 +400,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                      const float4 *__restrict__ sky,
                                                      const uint4 *__restrict__ dpk) {
   static_assert(!CH || (std::is_same<GI, GiF32>::value && !Z0 && !TOP && DL == 0 && PY == 1 && PD == 1),
-                "the chain: f32 one-probe tiles of the plain field below the top level");
+                "the chain: f32 one-probe tiles of the plain field (its top level a runtime case)");
   unsigned wgid = blockIdx.x;
   unsigned *ch_flag = nullptr;  // (CH) this workgroup's readiness flag
   unsigned ch_epoch = 0;
+  bool ch_top = false;          // (CH) this workgroup is of the top level: no staging, the sky merge
   if constexpr (CH) {
     const RcChainArgs *C = reinterpret_cast<const RcChainArgs *>(dpk);
     ch_epoch = (unsigned)reinterpret_cast<unsigned long long>(sky);
@@ -416,6 +419,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
     dist = ld_uniform(&lv->dist);
     shade = ld_uniform(&lv->shade);
     dirs = ld_uniform(&lv->dirs);
+    sky = ld_uniform(&lv->sky);
+    ch_top = ld_uniform(&lv->top) != 0;
     dpk = nullptr;
     const uint2 m = ld_uniform(P.wg_map + wgid);
     const int tx = (int)(m.x & 0xFFFFu), ty = (int)(m.x >> 16), dgi = (int)m.y;
@@ -435,8 +440,16 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         const int bx = (a & umask) * ubx + ((tx * TX) >> 1) - 1, by = (a >> ushift) * uby + ((ty * TY) >> 1) - 1;
         constexpr int RW = TX / 2 + 2, RH = TY / 2 + 2;
         int bxs[6], txs[6], bys[6], tys[6];
-        const int ncx = chain_segments((bx - 1) & ~7, (bx + RW + 1 + 7) & ~7, P.c.CW, ubx, TX, bxs, txs);
-        const int ncy = chain_segments(by - 1, by + RH + 1, P.c.CH, uby, TY, bys, tys);
+        int wx0 = (bx - 1) & ~7, wx1 = (bx + RW + 1 + 7) & ~7, wy0 = by - 1, wy1 = by + RH + 1;
+        if (ld_uniform(&lv->tight)) {  // (timing experiment: not a valid hand-off for every shape, see rc2dgi_rc_chain.hip)
+          const int x0b = (a & umask) * ubx, y0b = (a >> ushift) * uby;
+          wx0 = max(bx, x0b);
+          wx1 = min(bx + RW, x0b + ubx);
+          wy0 = max(by, y0b);
+          wy1 = min(by + RH, y0b + uby);
+        }
+        const int ncx = chain_segments(wx0, wx1, P.c.CW, ubx, TX, bxs, txs);
+        const int ncy = chain_segments(wy0, wy1, P.c.CH, uby, TY, bys, tys);
         const bool all = __any(ncx < 0 || ncy < 0 || ncx > 4 || ncy > 4);  // (other shapes: every upper tile)
         unsigned timeouts = 0;
         auto wait_slot = [&](unsigned slot) {
@@ -492,6 +505,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #else
   constexpr bool STG = !TOP;  // stage and merge the level-(L+1) cascade
 #endif
+  const bool stg = STG && !ch_top;
   __shared__ typename GI::S s_up[STG ? NSTAGE : 1];
   // Exit proofs.  The march's last sample of a ray that misses only decides that the ray ends: it
   // is not a hit and t + d leaves the interval or (further along the ray) the screen.  A coarse
@@ -587,7 +601,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // Level 0 issues its shared first distance sample before them (vmcnt retires in order, so
   // the march then waits for that sample only).
   auto stage_loads = [&]() {
-    if (STG) {
+    if (stg) {
   #pragma unroll
       for (int j = 0; j < DPW; ++j) {
         const int r = wdir + j * NW;  // direction (of the 4*PD) this wave stages
@@ -640,7 +654,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   if constexpr (!Z0) stage_loads();
   // the staged footprint to LDS, after the march
   auto stage_write = [&]() {
-    if (STG) {
+    if (stg) {
 #pragma unroll
       for (int j = 0; j < DPW; ++j) {
 #pragma unroll
@@ -1088,7 +1102,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   RC_TSTAMP(6);
   RC_SECTION("stage_write");
   stage_write();
-  if (STG || tl) __syncthreads();
+  if (stg || tl) __syncthreads();
   if (tl) {  // hit texels of this lane's rays that finished in the tail
 #pragma unroll
     for (int k = 0; k < NR; ++k)
@@ -1140,8 +1154,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         const int r = dblk * 4 + r4;  // index into the 4*PD directions
         float4 rad = hr[p * ND + r];
         const int ai = bi * 4 + r4;  // angleIndex
-        if (rad.w != 0.0f && (STG || TOP)) {
-          if (!TOP) {
+        if (rad.w != 0.0f && (stg || TOP || ch_top)) {
+          if (!TOP && !ch_top) {
             typename GI::S t00, t10, t01, t11;
             float ux = wx, uy = wy;
             if (pow2c) {

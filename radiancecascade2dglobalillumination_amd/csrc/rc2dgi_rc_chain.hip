@@ -50,7 +50,7 @@ int rc_chain_timeouts(RcChain *ch, hipStream_t st) {
 bool rc_chain_ok(int nlev) { return nlev >= 1 && nlev <= kChainMax; }
 
 hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDims s, CascadeDims c, int unr,
-                           hipStream_t st) {
+                           hipStream_t st, bool tight) {
   if (!ch || !rc_chain_ok(nlev) || c.gi_f16 || c.gi_u8) return hipErrorInvalidValue;
   RcChainArgs h{};
   h.n = nlev;
@@ -66,7 +66,11 @@ hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDi
     if (nwg == 0) return hipErrorOutOfMemory;
     if (nwg < 0) return hipErrorInvalidValue;
     if (i > 0 && a[i].level != a[i - 1].level - 1) return hipErrorInvalidValue;
-    if (a[i].level == a[i].N - 1 || !a[i].upper) return hipErrorInvalidValue;  // (the top level runs before)
+    // (the top level, if in the launch, is its first level; every other level reads the one before it)
+    const bool top = a[i].level == a[i].N - 1;
+    if (top ? (i != 0 || a[i].upper) : !a[i].upper) return hipErrorInvalidValue;
+    l.top = top ? 1 : 0;
+    l.sky = a[i].sky;
     l.upper = a[i].upper;
     l.out = a[i].out;
     l.dist = a[i].dist;
@@ -100,6 +104,7 @@ hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDi
     h.lv[i].uflags = i > 0 ? ch->flags + foff[i - 1] : nullptr;
     h.lv[i].utx = i > 0 ? h.lv[i - 1].P.tiles_x : 0;
     h.lv[i].utpb = i > 0 ? h.lv[i - 1].P.tiles_per_block : 0;
+    h.lv[i].tight = tight ? 1 : 0;
   }
   if (!ch->uploaded || std::memcmp(&h, &ch->host, sizeof(h)) != 0) {
     if (ch->uploaded) {  // (a copy still queued reads ch->host)

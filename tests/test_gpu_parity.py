@@ -605,14 +605,15 @@ def test_cascade_chain_is_bit_identical(RC2DGI, W, H, N, rr, scene):
     """The cascade chain (tuning rc_chain, rc2dgi_rc_chain.hip: levels N-2 .. 0 in one launch, a workgroup
     waiting on the readiness flags of the upper tiles under its footprint, sc1 hand-off) leaves every level G_L,
     giRT1 / giRT2 and the frame as the level-by-level launches, over two consecutive frames (the flags carry
-    the frame's epoch), rolled and unrolled march, with no workgroup timing out."""
+    the frame's epoch), rolled and unrolled march, the top level in the launch or before it, with no workgroup
+    timing out."""
     color, emis = make_scene(scene, W, H)
     ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
     ctx.set_keep_levels(True)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
     out = {}
-    for on in (0, 1, 2):
+    for on in (0, 1, 2, 4):  # 4: the top level in the launch too
         ctx.set_tuning("rc_chain", on)
         assert ctx.get_tuning("rc_chain") == on
         ctx.set_tuning("poison", 1)
@@ -622,7 +623,7 @@ def test_cascade_chain_is_bit_identical(RC2DGI, W, H, N, rr, scene):
             assert ctx.get_tuning("rc_chain_timeouts") == 0
             out[on, frame] = {k: ctx.download(k) for k in ("gi1", "gi2", "color")}
             out[on, frame].update({f"G{L}": ctx.download_level(L) for L in range(N)})
-    for on in (1, 2):
+    for on in (1, 2, 4):
         for frame in range(2):
             for k in out[0, frame]:
                 a, b = out[0, frame][k], out[on, frame][k]
