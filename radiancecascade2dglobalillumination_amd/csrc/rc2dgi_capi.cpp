@@ -1757,8 +1757,12 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     return prepare_side_buffers(c);
   }
   if (k == "rc_chain") {
-    if (value < 0 || value > 4)
-      return fail(c, RC2DGI_E_ARG, "rc_chain is 0 (off), 1 (chain), 2 (unrolled march), 3 (timing experiment), 4 (with the top level)");
+#ifdef RC2DGI_DIAG_CHAIN_TIGHT
+    const bool ok = value >= 0 && value <= 4;  // (3: the timing-only in-block window)
+#else
+    const bool ok = value >= 0 && value <= 4 && value != 3;
+#endif
+    if (!ok) return fail(c, RC2DGI_E_ARG, "rc_chain is 0 (off), 1 (chain), 2 (unrolled march), 4 (with the top level)");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->rc_chain = value;

@@ -61,7 +61,7 @@ struct RcChainLevel {
   unsigned *flags;          // its readiness flags: slot group * tiles_per_block + tile (nullptr: nobody waits)
   const unsigned *uflags;   // the upper level's (nullptr: the upper level ran before the launch)
   int utx, utpb;            // upper level: tiles per block row, tiles per block
-  int tight;                // experiment (rc_chain 3): wait only for the footprint inside the upper blocks
+  int tight;                // timing-only builds (RC2DGI_DIAG_CHAIN_TIGHT, rc_chain 3): the in-block footprint only
   int top;                  // the top level (no upper level: the sky), first in the launch
   const float4 *sky;        // (the top level's sky terms)
 };
@@ -441,13 +441,17 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         constexpr int RW = TX / 2 + 2, RH = TY / 2 + 2;
         int bxs[6], txs[6], bys[6], tys[6];
         int wx0 = (bx - 1) & ~7, wx1 = (bx + RW + 1 + 7) & ~7, wy0 = by - 1, wy1 = by + RH + 1;
-        if (ld_uniform(&lv->tight)) {  // (timing experiment: not a valid hand-off for every shape, see rc2dgi_rc_chain.hip)
+#ifdef RC2DGI_DIAG_CHAIN_TIGHT
+        // timing-only build (rc_chain 3): the footprint inside the upper blocks only -- changes results at C1
+        // (DESIGN §5.11), never built into the product
+        if (ld_uniform(&lv->tight)) {
           const int x0b = (a & umask) * ubx, y0b = (a >> ushift) * uby;
           wx0 = max(bx, x0b);
           wx1 = min(bx + RW, x0b + ubx);
           wy0 = max(by, y0b);
           wy1 = min(by + RH, y0b + uby);
         }
+#endif
         const int ncx = chain_segments(wx0, wx1, P.c.CW, ubx, TX, bxs, txs);
         const int ncy = chain_segments(wy0, wy1, P.c.CH, uby, TY, bys, tys);
         const bool all = __any(ncx < 0 || ncy < 0 || ncx > 4 || ncy > 4);  // (other shapes: every upper tile)

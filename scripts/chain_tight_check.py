@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""rc_chain 3 (timing experiment: waits only for the footprint inside the upper blocks) against the level-by-level
+"""rc_chain 3 (timing-only build: RC2DGI_LIB=build/ab/librc2dgi_tight.so from `_build.py exp tight
+-DRC2DGI_DIAG_CHAIN_TIGHT`; waits only for the footprint inside the upper blocks) against the level-by-level
 launches on one frame pair: does it still reproduce every level (C1 by default)?  Prints differing texel counts."""
 import os
 import sys
