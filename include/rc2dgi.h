@@ -178,8 +178,9 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *   "rc_chain"        0 (default); 1 / 2: the levels below the top in ONE launch of 16x16x1 tiles, a tile
  *                     starting when the upper tiles under its footprint are written (2: unrolled march);
  *                     4: the top level in that launch too; f32 cascades, one process
- * rc2dgi_get_tuning also answers "rc_variant_count" and "rc_chain_timeouts" (workgroups of the last
- * chained frames that stopped waiting for their upper tiles: 0 in a correct run; synchronises). */
+ * rc2dgi_get_tuning also answers "rc_variant_count" and "rc_chain_timeouts" (workgroups of the chained
+ * frames since the chain was set up that stopped waiting for their upper tiles: 0 in a correct run;
+ * synchronises). */
 int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
 /* time `frames` frames per candidate workgroup order x march variant ("rc_variant" 0 / 13 / 14 / 15) on
  * the uploaded scene and keep the fastest per level (like a convolution library's benchmark mode; results are identical for every

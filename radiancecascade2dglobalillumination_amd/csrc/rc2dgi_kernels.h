@@ -124,11 +124,12 @@ struct RcLevelArgs {
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
 };
 
-// The cascade chain (rc2dgi_rc_chain.hip, tuning rc_chain): the levels a[0 .. n) (consecutive, from the level
-// below the top down; the top level already written to a[0].upper) in one launch of 16x16x1 tiles (unr: the march
-// unrolled 32 as variant 13, else rolled as variant 0), f32 cascades, whole levels.  Each level's `out` must be a
-// buffer of its own (no level reads what another writes in the same launch).  rc_chain_timeouts: workgroups that
-// stopped waiting for their upper tiles (synchronises the stream; 0 in a correct run).
+// The cascade chain (rc2dgi_rc_chain.hip, tuning rc_chain): the levels a[0 .. n) (consecutive, downwards; a[0]
+// is the top level, or the level below it with the top already written to a[0].upper) in one launch of 16x16x1
+// tiles (unr: the march unrolled 32 as variant 13, else rolled as variant 0), f32 cascades, whole levels.  Each
+// level's `out` must be a buffer of its own (no level reads what another writes in the same launch).
+// rc_chain_timeouts: workgroups that stopped waiting for their upper tiles since the chain's buffers were made
+// (synchronises the stream; 0 in a correct run).
 struct RcChain;
 RcChain *rc_chain_create();
 void rc_chain_destroy(RcChain *ch);
