@@ -175,6 +175,8 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     per lane in a compacted queue (0 off; default 10)
  *   "shade_fused"     1 (default): surface records and the proofs' bound table in one pass over
  *                     distRT where its cells are >= 64 texels (square power-of-two screens >= 4096)
+ *   "jfa_rt"          rows per lane of the JumpFlood steps on small non-power-of-two screens: 1 (default),
+ *                     2, 4
  *   "rc_chain"        0 (default); 1 / 2: the levels below the top in ONE launch of 16x16x1 tiles, a tile
  *                     starting when the upper tiles under its footprint are written (2: unrolled march);
  *                     4: the top level in that launch too; f32 cascades, one process

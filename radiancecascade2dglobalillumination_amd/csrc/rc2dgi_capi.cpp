@@ -139,6 +139,7 @@ struct rc2dgi_ctx {
   std::vector<int> rc_noproof;   // per level: no bound table / exit proofs at this level (tuning rc_noproof_L<n>)
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
+  int jfa_rt = 1;                // tuning "jfa_rt": rows per lane of the float-path steps on small screens (1, 2, 4)
   int jfa_coset = 2;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
@@ -857,7 +858,7 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
     const unsigned *src = t == 0 ? c->occ : jfa_out(c, t - 1);
     for (auto &r : plan.jfa[t].iv)
       HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, out, dist, c->sd, ox, oy, st,
-                                r.first, r.second, nullptr, 0, c->jfa_lds));
+                                r.first, r.second, nullptr, 0, c->jfa_lds, c->jfa_rt));
     return RC2DGI_OK;
   }
   // row-strip shard: the own strip, into its window (global row y0 - m = local row 0)
@@ -1730,6 +1731,11 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->jfa_lds = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "jfa_rt") {
+    if (value != 1 && value != 2 && value != 4) return fail(c, RC2DGI_E_ARG, "jfa_rt is 1, 2 or 4");
+    c->jfa_rt = value;
+    return RC2DGI_OK;
+  }
   if (k == "rc_mp" || k.rfind("rc_mp_L", 0) == 0) {
     if (k == "rc_mp") {
       for (int &v : c->rc_mp) v = value != 0;
@@ -1816,6 +1822,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "jfa_lds") {
     *value = c->jfa_lds;
+    return RC2DGI_OK;
+  }
+  if (k == "jfa_rt") {
+    *value = c->jfa_rt;
     return RC2DGI_OK;
   }
   if (k == "jfa_coset") {

@@ -59,7 +59,8 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0 = 0,
                            int row1 = -1,  // output rows [row0, row1) (-1 = H)
                            const JfaSrc *window = nullptr, int dst_row0 = 0,
-                           int lds = 0);  // LDS-staged taps for short power-of-two steps (tuning jfa_lds)
+                           int lds = 0,   // LDS-staged taps for short power-of-two steps (tuning jfa_lds)
+                           int small_rt = 1);  // rows per lane of the float-path steps on small screens (tuning jfa_rt)
 // integer taps of the power-of-two JFA kernel (false: the float path runs); also used by the
 // row-strip planner
 bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp);

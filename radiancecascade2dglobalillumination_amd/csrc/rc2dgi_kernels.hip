@@ -1199,7 +1199,7 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
 
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0,
-                           int row1, const JfaSrc *window, int dst_row0, int lds) {
+                           int row1, const JfaSrc *window, int dst_row0, int lds, int small_rt) {
   JfaSrc win{};
   if (window && !first) win = *window;
   if (row1 < 0 || row1 > s.H) row1 = s.H;
@@ -1212,8 +1212,9 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   }
   const dim3 grid(ceil_div(s.W, 64), ceil_div(row1 - row0, 4 * JT));
   // float-path steps on small screens: one row per lane (k_jfa_step RT)
-  const bool small = (size_t)s.W * (size_t)(row1 - row0) <= ((size_t)1 << 21);
-  const dim3 grid1(ceil_div(s.W, 64), ceil_div(row1 - row0, 4));
+  const bool small = (size_t)s.W * (size_t)(row1 - row0) <= ((size_t)1 << 21) && small_rt != JT;
+  const bool rt2 = small_rt == 2;  // two rows per lane (8-row workgroups)
+  const dim3 grid1(ceil_div(s.W, 64), ceil_div(row1 - row0, rt2 ? 8 : 4));
   JfaTaps tp;
   const bool p2 = jfa_p2_taps(s, off_x, off_y, &tp);
   // lattice order (k_jfa_p2) for whole-frame launches whose steps span several tiles (not the
@@ -1230,7 +1231,13 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
       hipLaunchKernelGGL((k_jfa_p2<false, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp,
                          row0, row1, lattice, win, dst_row0);
   } else if (s.u8) {  // RGBA8 jumpRT: quantized seed uv, the float path
-    if (small) {
+    if (small && rt2) {
+      if (first)
+        hipLaunchKernelGGL((k_jfa_step<true, true, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
+      else
+        hipLaunchKernelGGL((k_jfa_step<false, true, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
+                           row1, win, dst_row0);
+    } else if (small) {
       if (first)
         hipLaunchKernelGGL((k_jfa_step<true, true, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
       else
@@ -1262,6 +1269,12 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
       if (ikey) RC2DGI_JFA(false, true); else RC2DGI_JFA(false, false);
     }
 #undef RC2DGI_JFA
+  } else if (small && rt2) {
+    if (first)
+      hipLaunchKernelGGL((k_jfa_step<true, false, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
+    else
+      hipLaunchKernelGGL((k_jfa_step<false, false, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
+                         row1, win, dst_row0);
   } else if (small) {
     if (first)
       hipLaunchKernelGGL((k_jfa_step<true, false, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);

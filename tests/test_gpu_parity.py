@@ -599,6 +599,28 @@ def test_jfa_coset_long_steps_are_bit_identical(RC2DGI, W, H, N, storage):
     ctx.close()
 
 
+@pytest.mark.parametrize("W,H,N,storage", [(1200, 900, 6, "f32"), (333, 200, 4, "f32"), (640, 360, 5, "rgba8")])
+def test_jfa_rows_per_lane_are_bit_identical(RC2DGI, W, H, N, storage):
+    """The float-path JumpFlood steps of small screens with 1, 2 or 4 rows per lane (tuning jfa_rt) leave the
+    same jumpRT1 / jumpRT2, distance field and frame."""
+    color, emis = make_scene("demo", W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for rt in (1, 2, 4):
+        ctx.set_tuning("jfa_rt", rt)
+        assert ctx.get_tuning("jfa_rt") == rt
+        ctx.set_tuning("poison", 1)
+        ctx.do_rc2dgi()
+        ctx.sync()
+        out[rt] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
+    for rt in (2, 4):
+        for k in out[1]:
+            assert np.array_equal(out[1][k], out[rt][k]), f"jfa_rt={rt} {k}: {np.count_nonzero(out[1][k] != out[rt][k])}"
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,N,rr,scene", [(1200, 900, 6, 2.0, "demo"), (1024, 1024, 6, 2.0, "demo"),
                                              (333, 200, 4, 8.0, "rand:44"), (4096, 4096, 6, 2.0, "demo")])
 def test_cascade_chain_is_bit_identical(RC2DGI, W, H, N, rr, scene):
