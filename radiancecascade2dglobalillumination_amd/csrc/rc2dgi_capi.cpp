@@ -75,6 +75,8 @@ const Rccl &rccl() {
 struct rc2dgi_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
+  hipStream_t side_stream = nullptr;  // the directional table beside the split records pass (fork / join events)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipStream_t stream = nullptr;
   // knobs (RC2DGI.cs:28-41, 66-68)
   int W = 0, H = 0, N = 0;
@@ -104,6 +106,10 @@ struct rc2dgi_ctx {
   uint4 *dist_n = nullptr;           // nibble-predicted copy for the "n" RC variants (k_dist_nib)
   unsigned short *mfield = nullptr;  // march field of the surface palettes (tuning rc_pal, launch_shade_cmin)
   float4 *cell_pal = nullptr;        // kCminDim^2 cells x kCellPalStride palette entries
+  unsigned *shade_list = nullptr;    // the split records pass's cell list (launch_shade_cmin, tuning shade_split)
+  int shade_split = 1;               // tuning "shade_split": the records / palette pass split at the cells with hits
+  int side_overlap = 0;              // tuning "side_overlap": k_dir_clear on the side stream beside k_shade_cells (measured slower)
+  unsigned split_frames = 0;         // split records passes enqueued (their list counters alternate by this parity)
   // which side tables the last frame built (rc2dgi_download_table answers RC2DGI_E_STATE for the others)
   bool built_hitc = false, built_cmin = false, built_dclr = false, built_pal = false;
   int rc_pal = 1;                    // surface palettes on (where they apply: 4096^2 .. 8192^2 square screens)
@@ -256,7 +262,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
-                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes, c->mfield, c->cell_pal};
+                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes, c->mfield, c->cell_pal, c->shade_list};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -274,6 +280,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->hitc = c->dclr = nullptr;
   c->mfield = nullptr;
   c->cell_pal = nullptr;
+  c->shade_list = nullptr;
   c->built_hitc = c->built_cmin = c->built_dclr = c->built_pal = false;
   c->dboxes = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
@@ -389,6 +396,16 @@ int prepare_side_buffers(rc2dgi_ctx *c, bool all = false) {
       c->mfield = nullptr;
       c->cell_pal = nullptr;
       return hip_fail(c, e, "surface palette tables");
+    }
+  }
+  if (pal && !c->shade_list) {
+    const size_t n = (2 + (size_t)kCminDim * kCminDim) * sizeof(unsigned);
+    hipError_t e = alloc(&c->shade_list, n);
+    if (e == hipSuccess) e = hipMemset(c->shade_list, 0, n);
+    if (e != hipSuccess) {
+      if (c->shade_list) (void)hipFree(c->shade_list);
+      c->shade_list = nullptr;
+      return hip_fail(c, e, "records pass cell list");
     }
   }
   return RC2DGI_OK;
@@ -627,6 +644,9 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
   int rc = RC2DGI_OK;
   hipError_t e = hipSetDevice(c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
   if (e != hipSuccess) {
     fprintf(stderr, "rc2dgi_create: %s\n", hipGetErrorString(e));
     delete c;
@@ -662,6 +682,10 @@ int rc2dgi_destroy(rc2dgi_ctx *c) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : c->ev_level)
     if (ev) (void)hipEventDestroy(ev);
+  if (c->side_stream) (void)hipStreamSynchronize(c->side_stream);
+  for (hipEvent_t ev : {c->ev_fork, c->ev_join})
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return RC2DGI_OK;
@@ -1006,14 +1030,30 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   c->built_cmin = proofs;
   c->built_dclr = mps;
   c->built_pal = pal;
+  bool side = false;  // (k_dir_clear on the side stream)
   if (fused) {
+    // (the split pass's parity advances only with the split passes themselves: k_shade_cells clears the other
+    // parity's counter for the next one)
+    const bool split = pal && c->shade_split && shade_split_ok(c->W, c->H);
+    // split pass with directional proofs: k_dir_clear needs only the scan's hit flags, so it runs on the side
+    // stream beside k_shade_cells (the few hundred workgroups of the hit cells leave most CUs idle)
+    side = split && mps && c->side_stream && c->side_overlap;
     HIPCHK(c, launch_shade_cmin(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, c->cmin,
-                                mps ? c->hitc : nullptr, st, pal ? c->mfield : nullptr, pal ? c->cell_pal : nullptr));
+                                mps ? c->hitc : nullptr, st, pal ? c->mfield : nullptr, pal ? c->cell_pal : nullptr,
+                                split ? c->shade_list : nullptr, split ? (int)(c->split_frames++ & 1u) : 0,
+                                side ? c->ev_fork : nullptr));
   } else {
     HIPCHK(c, launch_shade(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, st));
     if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
   }
-  if (mps) HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
+  if (mps && side) {
+    HIPCHK(c, hipStreamWaitEvent(c->side_stream, c->ev_fork, 0));
+    HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, c->side_stream));
+    HIPCHK(c, hipEventRecord(c->ev_join, c->side_stream));
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_join, 0));
+  } else if (mps) {
+    HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
+  }
   bool gi1final = false;
   // The cascade chain (tuning rc_chain, rc2dgi_rc_chain.hip): the top level as usual, then levels N-2 .. 0 in one
   // launch of 16x16x1 tiles, each level into a texture of its own -- level 0 into giRT1 / giRT2 as the loop below
@@ -1727,6 +1767,14 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->shade_fused = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "shade_split") {
+    c->shade_split = value != 0;
+    return RC2DGI_OK;
+  }
+  if (k == "side_overlap") {
+    c->side_overlap = value != 0;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_lds") {
     c->jfa_lds = value != 0;
     return RC2DGI_OK;
@@ -1834,6 +1882,14 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "shade_fused") {
     *value = c->shade_fused;
+    return RC2DGI_OK;
+  }
+  if (k == "shade_split") {
+    *value = c->shade_split;
+    return RC2DGI_OK;
+  }
+  if (k == "side_overlap") {
+    *value = c->side_overlap;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_tail_L", 0) == 0) {

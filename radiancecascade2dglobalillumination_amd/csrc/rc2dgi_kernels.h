@@ -151,9 +151,14 @@ bool shade_cmin_fused_ok(int W, int H, int pitch);
 // A march reading mf takes the same samples (a hit is still a value <= 65, other texels keep q) and finds a
 // hit's record in a 1 MB table shared by all the rays that end on one surface of the cell.
 constexpr int kCellPal = 15, kCellPalStride = 16;  // entries per cell (index 15 marks "no entry"), slots per cell
+// list (optional, with mf / cpal; shade_split_ok sizes): 2 + kCminDim^2 words, zeroed once; the pass then runs
+// split (k_shade_scan over every cell, k_shade_cells over the cells holding a hittable texel).  `parity` must
+// alternate from one split pass to the next (k_shade_cells clears the other parity's counter).
+bool shade_split_ok(int W, int H);
 hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
                              ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st,
-                             unsigned short *mf = nullptr, float4 *cpal = nullptr);
+                             unsigned short *mf = nullptr, float4 *cpal = nullptr, unsigned *list = nullptr,
+                             int parity = 0, hipEvent_t after_scan = nullptr);  // (split: recorded after the scan)
 hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st,
                             unsigned char *hitc = nullptr);
 // Directional clear distances of the march proofs (k_rc_level, one-probe tiles): kDirBins angular bins x

@@ -570,15 +570,16 @@ __global__ __launch_bounds__(256) void k_dist_cmin(const unsigned short *__restr
 // cell's hittable texels in cpal[cell * kCellPalStride + i] (deduplicated in LDS; two waves inserting one record
 // at once may both add it -- a wasted entry, never a wrong one), and mf = distRT with every hittable texel's
 // q replaced by its palette entry i (kCellPal: no entry left, the march reads its record from shade).
-template <bool PAL, int NTH = 256>
-__global__ __launch_bounds__(NTH) void k_shade_cmin(const unsigned short *__restrict__ dist,
-                                                    const float4 *__restrict__ color, const float4 *__restrict__ emis,
-                                                    float4 *__restrict__ shade, ScreenDims s, float reflectivity,
-                                                    int csh, CminT *__restrict__ cmin, unsigned char *__restrict__ hitc,
-                                                    unsigned short *__restrict__ mf, float4 *__restrict__ cpal) {
+// (one cell (bx, by); TAB: also its bound-table entry and hit flag)
+template <bool PAL, int NTH, bool TAB>
+__device__ __forceinline__ void shade_cell(const unsigned short *__restrict__ dist, const float4 *__restrict__ color,
+                                           const float4 *__restrict__ emis, float4 *__restrict__ shade, ScreenDims s,
+                                           float reflectivity, int csh, CminT *__restrict__ cmin,
+                                           unsigned char *__restrict__ hitc, unsigned short *__restrict__ mf,
+                                           float4 *__restrict__ cpal, const int bx, const int by) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cw = 1 << csh;
-  const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
+  const int x0 = bx << csh, y0 = by << csh;
   __shared__ float4 s_pal[PAL ? kCellPal : 1];
   __shared__ unsigned s_rdy[PAL ? kCellPal : 1];  // entry i holds its record (set after the record is written)
   __shared__ unsigned s_npal;
@@ -587,7 +588,7 @@ __global__ __launch_bounds__(NTH) void k_shade_cmin(const unsigned short *__rest
     if (threadIdx.x < kCellPal) s_rdy[threadIdx.x] = 0u;
     __syncthreads();
   }
-  float4 *const gpal = PAL ? cpal + (size_t)(blockIdx.y * kCminDim + blockIdx.x) * kCellPalStride : nullptr;
+  float4 *const gpal = PAL ? cpal + (size_t)(by * kCminDim + bx) * kCellPalStride : nullptr;
   unsigned m = 0xFFFFu;
   constexpr int NW = NTH / 64, RPW = 64 / NW;  // waves; a wave's rows of a 64-row block (NW apart)
   const size_t rstep = (size_t)NW * s.pitch;
@@ -707,23 +708,117 @@ __global__ __launch_bounds__(NTH) void k_shade_cmin(const unsigned short *__rest
       }
     }
   }
+  if constexpr (TAB) {
+    // REPEAT wrap (k_dist_cmin): samples at u = 1 / v = 1 read column 0 / row 0
+    if (x0 + cw == s.W)
+      for (int e = (int)threadIdx.x; e < cw; e += NTH) m = min(m, (unsigned)dist[(size_t)(y0 + e) * s.pitch]);
+    if (y0 + cw == s.H)
+      for (int e = (int)threadIdx.x; e < cw; e += NTH) m = min(m, (unsigned)dist[x0 + e]);
+    if (x0 + cw == s.W && y0 + cw == s.H && threadIdx.x == 0) m = min(m, (unsigned)dist[0]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, o, 64));
+    __shared__ unsigned s_m[NW];
+    if (lane == 0) s_m[w] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int i = 1; i < NW; ++i) m = min(m, s_m[i]);
+      const float d = decode_dist(m);
+      if (hitc) hitc[by * kCminDim + bx] = d < 0.001f ? 1 : 0;
+      cmin[by * kCminDim + bx] = d >= 0.001f ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
+    }
+  } else {
+    (void)m;
+    __syncthreads();  // (the next cell of this workgroup reuses the palette's LDS)
+  }
+}
+
+template <bool PAL, int NTH = 256>
+__global__ __launch_bounds__(NTH) void k_shade_cmin(const unsigned short *__restrict__ dist,
+                                                    const float4 *__restrict__ color, const float4 *__restrict__ emis,
+                                                    float4 *__restrict__ shade, ScreenDims s, float reflectivity,
+                                                    int csh, CminT *__restrict__ cmin, unsigned char *__restrict__ hitc,
+                                                    unsigned short *__restrict__ mf, float4 *__restrict__ cpal) {
+  shade_cell<PAL, NTH, true>(dist, color, emis, shade, s, reflectivity, csh, cmin, hitc, mf, cpal, (int)blockIdx.x,
+                             (int)blockIdx.y);
+}
+
+// The same pass split in two (tuning shade_split; round 5).  Most cells hold no hittable texel (demo frame:
+// 262 of 4096), yet every cell ran in the 114-VGPR kernel above (2 workgroups per CU, 8 rounds).
+// k_shade_scan: one light workgroup per cell -- 16-byte distance loads, the bound table and hit flag, the march
+// field copied where the cell holds no hit, and the cells that do appended to `list` (count in list[p], cells
+// from list[2]; p = the frame's parity).  k_shade_cells: the records, palette and march field of the listed cells,
+// shade_cell's code; it clears the other parity's count for the next frame.  Same outputs bit for bit.
+template <int NR>  // runs per lane: 2 (64-texel cells)
+__global__ __launch_bounds__(256) void k_shade_scan(const unsigned short *__restrict__ dist, ScreenDims s, int csh,
+                                                    CminT *__restrict__ cmin, unsigned char *__restrict__ hitc,
+                                                    unsigned short *__restrict__ mf, unsigned *__restrict__ list,
+                                                    int p) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cw = 1 << csh, sh = csh - 3;  // 2^sh runs of 8 texels per cell row
+  const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
+  constexpr int nr = NR;
+  uint4 v[NR];
+  size_t base[NR];
+  unsigned m = 0xFFFFu;
+  bool hit = false;
+#pragma unroll
+  for (int g = 0; g < NR; ++g) {
+    {
+      const int e = g * 256 + (int)threadIdx.x;
+      base[g] = (size_t)(y0 + (e >> sh)) * s.pitch + x0 + ((e & ((1 << sh) - 1)) << 3);
+      v[g] = *reinterpret_cast<const uint4 *>(dist + base[g]);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < NR; ++g) {
+    {
+      const unsigned wd[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const unsigned q = (wd[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        m = min(m, q);
+        hit |= decode_dist(q) < 0.001f;
+      }
+    }
+  }
+  const bool cell_hit = __syncthreads_or(hit);
+  if (!cell_hit) {
+#pragma unroll
+    for (int g = 0; g < NR; ++g) *reinterpret_cast<uint4 *>(mf + base[g]) = v[g];
+  } else if (threadIdx.x == 0) {
+    list[2 + atomicAdd(&list[p], 1u)] = blockIdx.y * kCminDim + blockIdx.x;
+  }
   // REPEAT wrap (k_dist_cmin): samples at u = 1 / v = 1 read column 0 / row 0
   if (x0 + cw == s.W)
-    for (int e = (int)threadIdx.x; e < cw; e += NTH) m = min(m, (unsigned)dist[(size_t)(y0 + e) * s.pitch]);
+    for (int e = (int)threadIdx.x; e < cw; e += 256) m = min(m, (unsigned)dist[(size_t)(y0 + e) * s.pitch]);
   if (y0 + cw == s.H)
-    for (int e = (int)threadIdx.x; e < cw; e += NTH) m = min(m, (unsigned)dist[x0 + e]);
+    for (int e = (int)threadIdx.x; e < cw; e += 256) m = min(m, (unsigned)dist[x0 + e]);
   if (x0 + cw == s.W && y0 + cw == s.H && threadIdx.x == 0) m = min(m, (unsigned)dist[0]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, o, 64));
-  __shared__ unsigned s_m[NW];
+  __shared__ unsigned s_m[4];
   if (lane == 0) s_m[w] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 1; i < NW; ++i) m = min(m, s_m[i]);
+    m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
     const float d = decode_dist(m);
     if (hitc) hitc[blockIdx.y * kCminDim + blockIdx.x] = d < 0.001f ? 1 : 0;
     cmin[blockIdx.y * kCminDim + blockIdx.x] = d >= 0.001f ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
+  }
+}
+
+__global__ __launch_bounds__(512) void k_shade_cells(const unsigned short *__restrict__ dist,
+                                                     const float4 *__restrict__ color, const float4 *__restrict__ emis,
+                                                     float4 *__restrict__ shade, ScreenDims s, float reflectivity,
+                                                     int csh, unsigned short *__restrict__ mf, float4 *__restrict__ cpal,
+                                                     unsigned *__restrict__ list, int p) {
+  const unsigned n = *(volatile unsigned *)&list[p];
+  if (blockIdx.x == 0 && threadIdx.x == 0) list[p ^ 1] = 0u;  // (the next frame's count)
+  for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
+    const unsigned cell = list[2 + i];
+    shade_cell<true, 512, false>(dist, color, emis, shade, s, reflectivity, csh, nullptr, nullptr, mf, cpal,
+                                 (int)(cell % kCminDim), (int)(cell / kCminDim));
   }
 }
 
@@ -1733,6 +1828,9 @@ hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, 
   return hipGetLastError();
 }
 
+// the split pass: 64-texel cells (4096^2; at 8192^2 the scan would hold 8 runs per lane, 130 VGPRs)
+bool shade_split_ok(int W, int H) { return dist_cmin_shift(W, H) == 6; }
+
 bool shade_cmin_fused_ok(int W, int H, int pitch) {
   const int csh = dist_cmin_shift(W, H);
   return csh >= 6 && W == H && W == (kCminDim << csh) && pitch % 64 == 0;
@@ -1740,8 +1838,21 @@ bool shade_cmin_fused_ok(int W, int H, int pitch) {
 
 hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
                              ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st,
-                             unsigned short *mf, float4 *cpal) {
+                             unsigned short *mf, float4 *cpal, unsigned *list, int parity, hipEvent_t after_scan) {
   if (!shade_cmin_fused_ok(s.W, s.H, s.pitch)) return hipErrorInvalidValue;
+  const int csh = dist_cmin_shift(s.W, s.H);
+  if (mf && cpal && list) {
+    if (!shade_split_ok(s.W, s.H)) return hipErrorInvalidValue;
+    const int p = parity & 1;
+    hipLaunchKernelGGL(k_shade_scan<2>, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, s, csh, cmin, hitc, mf, list, p);
+    if (after_scan) {  // (the bound table and hit flags are final here)
+      const hipError_t e = hipEventRecord(after_scan, st);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_shade_cells, dim3(512), dim3(512), 0, st, dist, color, emis, shade, s, reflectivity, csh, mf,
+                       cpal, list, p);
+    return hipGetLastError();
+  }
   if (mf && cpal)
     hipLaunchKernelGGL((k_shade_cmin<true, 512>), dim3(kCminDim, kCminDim), dim3(512), 0, st, dist, color, emis, shade, s,
                        reflectivity, dist_cmin_shift(s.W, s.H), cmin, hitc, mf, cpal);

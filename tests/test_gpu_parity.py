@@ -654,6 +654,37 @@ def test_cascade_chain_is_bit_identical(RC2DGI, W, H, N, rr, scene):
     ctx.close()
 
 
+@pytest.mark.parametrize("scene", ["demo", "speckled", "rand:45"])
+def test_shade_split_is_bit_identical(RC2DGI, scene):
+    """The records / palette pass split at the cells holding a hittable texel (tuning shade_split: k_shade_scan
+    over every cell, k_shade_cells over the listed ones, the list counters alternating frame to frame) gives
+    the frames, every level, the bound table and hit flags of the one-kernel pass, over three frames."""
+    W = H = 4096
+    color, emis = speckled_scene(W, H) if scene == "speckled" else make_scene(scene, W, H)
+    ctx = RC2DGI(W, H, cascade_count=6, ray_range=2.0)
+    ctx.set_keep_levels(True)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for split in (0, 1, 2):  # 2: split, k_dir_clear on the side stream
+        ctx.set_tuning("shade_split", min(split, 1))
+        ctx.set_tuning("side_overlap", int(split == 2))
+        assert ctx.get_tuning("shade_split") == min(split, 1)
+        for frame in range(3):
+            ctx.do_rc2dgi()
+            ctx.sync()
+            out[split, frame] = {"color": ctx.download("color"), "hitc": ctx.download_table("hitc"),
+                                 "cmin": ctx.download_table("cmin")}
+            out[split, frame].update({f"G{L}": ctx.download_level(L) for L in range(6)})
+    for split in (1, 2):
+        for frame in range(3):
+            for k in out[0, frame]:
+                a, b = out[0, frame][k], out[split, frame][k]
+                assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), \
+                    f"split {split} frame {frame} {k}: {np.count_nonzero(a != b)}"
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,N", [(4096, 4096, 6), (8192, 8192, 8)])
 def test_shade_cmin_fused_is_bit_identical(RC2DGI, W, H, N):
     """k_shade_cmin (surface records + the proofs' bound table and hit flags in one pass over distRT,

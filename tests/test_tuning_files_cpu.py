@@ -27,7 +27,7 @@ def built_variants(storage):
     return {0, 25} | {int(v) for v in re.findall(r"case (\d+):", src)}  # (25: k_rc_top, every storage)
 
 
-KNOBS = {"rc_pal", "rc_skip", "rc_tail", "rc_wgproof", "jfa_lds", "jfa_coset", "shade_fused", "blur_path", "rc_chain", "jfa_rt"}
+KNOBS = {"rc_pal", "rc_skip", "rc_tail", "rc_wgproof", "jfa_lds", "jfa_coset", "shade_fused", "blur_path", "rc_chain", "jfa_rt", "shade_split", "side_overlap"}
 
 FILES = sorted(glob.glob(os.path.join(TUNING, "*.json")))
 
