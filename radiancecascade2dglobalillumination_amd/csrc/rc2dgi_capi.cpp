@@ -644,9 +644,6 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
   int rc = RC2DGI_OK;
   hipError_t e = hipSetDevice(c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
   if (e != hipSuccess) {
     fprintf(stderr, "rc2dgi_create: %s\n", hipGetErrorString(e));
     delete c;
@@ -1772,6 +1769,14 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     return RC2DGI_OK;
   }
   if (k == "side_overlap") {
+    // (the side stream is made on first use only: every extra stream takes a share of the process's hardware
+    // queues, and the 8 in-process shards of the strips rehearsal ran 0.8 ms slower with one per context)
+    if (value && !c->side_stream) {
+      HIPCHK(c, hipSetDevice(c->device));
+      HIPCHK(c, hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
     c->side_overlap = value != 0;
     return RC2DGI_OK;
   }
