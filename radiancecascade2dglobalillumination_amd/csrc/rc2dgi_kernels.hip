@@ -591,6 +591,8 @@ __device__ __forceinline__ void shade_cell(const unsigned short *__restrict__ di
   float4 *const gpal = PAL ? cpal + (size_t)(by * kCminDim + bx) * kCellPalStride : nullptr;
   unsigned m = 0xFFFFu;
   constexpr int NW = NTH / 64, RPW = 64 / NW;  // waves; a wave's rows of a 64-row block (NW apart)
+  constexpr int GR = RPW < 8 ? RPW : 8;         // rows per record group (8; 4 with 1024 lanes)
+  constexpr unsigned GM = (1u << GR) - 1u;
   const size_t rstep = (size_t)NW * s.pitch;
   for (int c = lane; c < cw; c += 64) {
     for (int rb = 0; rb < cw; rb += 64) {
@@ -607,53 +609,53 @@ __device__ __forceinline__ void shade_cell(const unsigned short *__restrict__ di
         hm |= decode_dist(q[t]) < 0.001f ? 1u << t : 0u;
       }
 #pragma unroll
-      for (int h = 0; h < RPW / 8; ++h) {
+      for (int h = 0; h < RPW / GR; ++h) {
         // (with palettes the skip is wave-uniform: the palette code below needs every lane of the wave)
-        if (PAL ? __ballot((hm >> (8 * h) & 0xFFu) != 0u) == 0ull : !(hm >> (8 * h) & 0xFFu)) {
+        if (PAL ? __ballot((hm >> (GR * h) & GM) != 0u) == 0ull : !(hm >> (GR * h) & GM)) {
           if (PAL) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) mf[base + (8 * h + k) * rstep] = (unsigned short)q[8 * h + k];
+            for (int k = 0; k < GR; ++k) mf[base + (GR * h + k) * rstep] = (unsigned short)q[GR * h + k];
           }
           continue;
         }
-        float4 e[8], cl[8];
+        float4 e[GR], cl[GR];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < GR; ++k) {
           e[k] = cl[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          if (hm >> (8 * h + k) & 1u) {
-            e[k] = emis[base + (8 * h + k) * rstep];
-            cl[k] = color[base + (8 * h + k) * rstep];
+          if (hm >> (GR * h + k) & 1u) {
+            e[k] = emis[base + (GR * h + k) * rstep];
+            cl[k] = color[base + (GR * h + k) * rstep];
           }
         }
-        float4 rec[8];
+        float4 rec[GR];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const bool hit = hm >> (8 * h + k) & 1u;
+        for (int k = 0; k < GR; ++k) {
+          const bool hit = hm >> (GR * h + k) & 1u;
           rec[k] = make_float4(e[k].x, e[k].y, e[k].z, 1.0f);
           if (!(sqrtf(e[k].x * e[k].x + e[k].y * e[k].y + e[k].z * e[k].z) > 0.0f))
             rec[k] = make_float4(cl[k].x, cl[k].y, cl[k].z, reflectivity);
-          if (hit) shade[base + (8 * h + k) * rstep] = rec[k];
+          if (hit) shade[base + (GR * h + k) * rstep] = rec[k];
         }
         if (PAL) {
           // the wave's distinct records of these 8 rows, one at a time (usually one or two: a surface's texels
           // share it): the first remaining (row, lane)'s record, every (row, lane) holding the same bits, the
           // entry found or added by lane 0 of the wave -- one round per distinct record, not per row
-          unsigned idx[8];
-          unsigned long long rem[8];
+          unsigned idx[GR];
+          unsigned long long rem[GR];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
+          for (int k = 0; k < GR; ++k) {
             idx[k] = kCellPal;
-            rem[k] = __ballot(hm >> (8 * h + k) & 1u);
+            rem[k] = __ballot(hm >> (GR * h + k) & 1u);
           }
           for (;;) {
             int kk = -1;
 #pragma unroll
-            for (int k = 7; k >= 0; --k) kk = rem[k] ? k : kk;  // (wave-uniform)
+            for (int k = GR - 1; k >= 0; --k) kk = rem[k] ? k : kk;  // (wave-uniform)
             if (kk < 0) break;
             unsigned long long rk = rem[0];
             float4 rv = rec[0];
 #pragma unroll
-            for (int k = 1; k < 8; ++k)
+            for (int k = 1; k < GR; ++k)
               if (kk == k) {
                 rk = rem[k];
                 rv = rec[k];
@@ -665,9 +667,9 @@ __device__ __forceinline__ void shade_cell(const unsigned short *__restrict__ di
               return __float_as_uint(v.x) == __float_as_uint(rx) && __float_as_uint(v.y) == __float_as_uint(ry) &&
                      __float_as_uint(v.z) == __float_as_uint(rz) && __float_as_uint(v.w) == __float_as_uint(rw);
             };
-            unsigned long long mine[8];
+            unsigned long long mine[GR];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) mine[k] = __ballot((hm >> (8 * h + k) & 1u) && same(rec[k])) & rem[k];
+            for (int k = 0; k < GR; ++k) mine[k] = __ballot((hm >> (GR * h + k) & 1u) && same(rec[k])) & rem[k];
             // the lanes below the palette's fill compare one entry each; lane 0 adds the record if none holds it
             const unsigned n = min(__builtin_amdgcn_readfirstlane(*(volatile unsigned *)&s_npal), (unsigned)kCellPal);
             // (an entry counted but not yet written is skipped: at worst the record is added twice)
@@ -696,14 +698,14 @@ __device__ __forceinline__ void shade_cell(const unsigned short *__restrict__ di
               e_idx = min((unsigned)__builtin_amdgcn_readfirstlane((int)slot), (unsigned)kCellPal);
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < GR; ++k) {
               if ((mine[k] >> lane) & 1ull) idx[k] = e_idx;
               rem[k] &= ~mine[k];
             }
           }
 #pragma unroll
-          for (int k = 0; k < 8; ++k)
-            mf[base + (8 * h + k) * rstep] = (unsigned short)((hm >> (8 * h + k) & 1u) ? idx[k] : q[8 * h + k]);
+          for (int k = 0; k < GR; ++k)
+            mf[base + (GR * h + k) * rstep] = (unsigned short)((hm >> (GR * h + k) & 1u) ? idx[k] : q[GR * h + k]);
         }
       }
     }
@@ -808,7 +810,10 @@ __global__ __launch_bounds__(256) void k_shade_scan(const unsigned short *__rest
   }
 }
 
-__global__ __launch_bounds__(512) void k_shade_cells(const unsigned short *__restrict__ dist,
+#ifndef RC2DGI_SHADE_CELLS_NTH
+#define RC2DGI_SHADE_CELLS_NTH 512  // (A/B builds: 1024 lanes, record groups of 4 rows)
+#endif
+__global__ __launch_bounds__(RC2DGI_SHADE_CELLS_NTH) void k_shade_cells(const unsigned short *__restrict__ dist,
                                                      const float4 *__restrict__ color, const float4 *__restrict__ emis,
                                                      float4 *__restrict__ shade, ScreenDims s, float reflectivity,
                                                      int csh, unsigned short *__restrict__ mf, float4 *__restrict__ cpal,
@@ -817,7 +822,7 @@ __global__ __launch_bounds__(512) void k_shade_cells(const unsigned short *__res
   if (blockIdx.x == 0 && threadIdx.x == 0) list[p ^ 1] = 0u;  // (the next frame's count)
   for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
     const unsigned cell = list[2 + i];
-    shade_cell<true, 512, false>(dist, color, emis, shade, s, reflectivity, csh, nullptr, nullptr, mf, cpal,
+    shade_cell<true, RC2DGI_SHADE_CELLS_NTH, false>(dist, color, emis, shade, s, reflectivity, csh, nullptr, nullptr, mf, cpal,
                                  (int)(cell % kCminDim), (int)(cell / kCminDim));
   }
 }
@@ -1849,7 +1854,7 @@ hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, co
       const hipError_t e = hipEventRecord(after_scan, st);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_shade_cells, dim3(512), dim3(512), 0, st, dist, color, emis, shade, s, reflectivity, csh, mf,
+    hipLaunchKernelGGL(k_shade_cells, dim3(512), dim3(RC2DGI_SHADE_CELLS_NTH), 0, st, dist, color, emis, shade, s, reflectivity, csh, mf,
                        cpal, list, p);
     return hipGetLastError();
   }
