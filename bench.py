@@ -321,6 +321,7 @@ def bench_strips(a, rank, local, world):
         g.set_shard(k, nsh)
         return g
 
+    free0 = torch.cuda.mem_get_info(local)[0]  # (device bytes the shard contexts hold, measured after the warmup)
     if virtual:
         ctxs = [make(k) for k in range(nsh)]
         run = lambda: R.do_group(ctxs)  # noqa: E731
@@ -339,6 +340,7 @@ def bench_strips(a, rank, local, world):
         run()
     for g in ctxs:
         g.sync()
+    shard_bytes = (free0 - torch.cuda.mem_get_info(local)[0]) // len(ctxs)
     rdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -360,6 +362,7 @@ def bench_strips(a, rank, local, world):
             "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}, row strips",
                        "shards": nsh, "parallelism": f"strips{nsh}" + ("-in-process" if virtual else "-rccl"),
                        "rc_variant": [ctxs[0].get_tuning(f"rc_variant_L{L}") for L in range(N)]},
+            "device_bytes_per_shard": int(shard_bytes),
             "frames_per_s": round(a.steps / wall, 2)}), flush=True)
     for g in ctxs:
         g.close()
