@@ -1149,16 +1149,20 @@ __global__ __launch_bounds__(256) void k_blur_fused(const typename GI::T *__rest
 // finite values (fma(0, b - a, a) = a) and are skipped.  With MERGE (screen == cascade size) the
 // merge's LINEAR sample of finalGI lands exactly on the texel as well (same argument), so
 // merge.fs runs on the blended GI value held in registers.
+#ifndef RC2DGI_BLUR_RPT
+#define RC2DGI_BLUR_RPT 8  // output rows per thread (tiles of 4 x this many rows; A/B builds: 4)
+#endif
 template <int F, bool MERGE, class GI>
 __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restrict__ gi_in,
                                                    float4 *__restrict__ blur_out, typename GI::T *__restrict__ gi_out,
                                                    CascadeDims c, BlurTaps bt,
                                                    const float4 *__restrict__ color_in, float4 *__restrict__ temp,
                                                    float4 *__restrict__ color_out, int spitch, int tile0) {
-  constexpr int HALO = F + 1, TW = 64 + 2 * HALO, TH = 32 + 2 * HALO, NR = 8 + 2 * HALO;
+  constexpr int RPT = RC2DGI_BLUR_RPT, TR = 4 * RPT;  // rows per thread, rows per tile
+  constexpr int HALO = F + 1, TW = 64 + 2 * HALO, TH = TR + 2 * HALO, NR = RPT + 2 * HALO;
   __shared__ float4 tile[TH * TW];
-  const int by = (int)blockIdx.y + tile0;  // 32-row tile
-  const int x0 = blockIdx.x * 64 - HALO, y0 = by * 32 - HALO;
+  const int by = (int)blockIdx.y + tile0;  // TR-row tile
+  const int x0 = blockIdx.x * 64 - HALO, y0 = by * TR - HALO;
   for (int k = threadIdx.x; k < TW * TH; k += 256) {
     const int ty = k / TW, tx = k - ty * TW;
     const int gx = (x0 + tx) & (c.CW - 1), gy = (y0 + ty) & (c.CH - 1);
@@ -1166,7 +1170,7 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
   }
   __syncthreads();
   const int lx = (threadIdx.x & 63) + HALO;  // tile column of this thread's texel
-  const int r0 = (threadIdx.x >> 6) * 8;     // first input row (tile-local) = first output row - HALO
+  const int r0 = (threadIdx.x >> 6) * RPT;   // first input row (tile-local) = first output row - HALO
   const bool lo = bt.a0 == -F - 1;           // a0 is -F-1 (fractional radius) or -F (integral radius)
   const float w0 = bt.w0, w2 = bt.w2;
   // h[k][q]: input row r0 + k lerped horizontally at column offset q (0: a0, 1: 0, 2: F)
@@ -1181,7 +1185,7 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
   }
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
+  for (int t = 0; t < RPT; ++t) {
     const int m = t + HALO;  // this output's own row in h
     // row pairs of the y offsets: -1 -> (m + a0, m + a0 + 1) w0; 0 -> m (weight 0); +1 -> (m + F, m + F + 1) w2
     float4 s[3][3];  // s[qy][qx]
@@ -1209,7 +1213,7 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
     }
     const float4 b = blend_over_black(res);  // cascadeBlurRT cleared to (0,0,0,1)
     const float4 g = GI::round(blend(b, h[m][1]));  // copy-back onto finalGI, blended (as stored)
-    const int j = by * 32 + r0 + t;
+    const int j = by * TR + r0 + t;
     const size_t o = (size_t)j * c.pitch + i;
     blur_out[o] = b;
     GI::st(&gi_out[o], g);
@@ -1693,7 +1697,8 @@ bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Cas
   if (merge && !(s.W == c.CW && s.H == c.CH)) return false;
   clamp_rows(c.CH, row0, row1);
   if (row0 >= row1) return true;
-  const int t0 = row0 / 32, t1 = ceil_div(row1, 32);  // whole 32-row tiles
+  constexpr int TR = 4 * RC2DGI_BLUR_RPT;
+  const int t0 = row0 / TR, t1 = ceil_div(row1, TR);  // whole tiles
   const dim3 grid(c.CW / 64, t1 - t0);
 #define RC2DGI_BLUR_ROWS(FV, MV)                                                                               \
   do {                                                                                                         \
