@@ -1034,7 +1034,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     const bool split = pal && c->shade_split && shade_split_ok(c->W, c->H);
     // split pass with directional proofs: k_dir_clear needs only the scan's hit flags, so it runs on the side
     // stream beside k_shade_cells (the few hundred workgroups of the hit cells leave most CUs idle)
-    side = split && mps && c->side_stream && c->side_overlap;
+    side = split && mps && c->side_overlap && c->side_stream && c->ev_fork && c->ev_join;
     HIPCHK(c, launch_shade_cmin(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, c->cmin,
                                 mps ? c->hitc : nullptr, st, pal ? c->mfield : nullptr, pal ? c->cell_pal : nullptr,
                                 split ? c->shade_list : nullptr, split ? (int)(c->split_frames++ & 1u) : 0,
@@ -1771,11 +1771,11 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
   if (k == "side_overlap") {
     // (the side stream is made on first use only: every extra stream takes a share of the process's hardware
     // queues, and the 8 in-process shards of the strips rehearsal ran 0.8 ms slower with one per context)
-    if (value && !c->side_stream) {
+    if (value && !(c->side_stream && c->ev_fork && c->ev_join)) {
       HIPCHK(c, hipSetDevice(c->device));
-      HIPCHK(c, hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+      if (!c->side_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+      if (!c->ev_fork) HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+      if (!c->ev_join) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     }
     c->side_overlap = value != 0;
     return RC2DGI_OK;
