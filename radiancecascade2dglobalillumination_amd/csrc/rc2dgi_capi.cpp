@@ -383,6 +383,15 @@ int prepare_side_buffers(rc2dgi_ctx *c, bool all = false) {
       }
     }
     c->chain = rc_chain_create();
+    // one flag per 16x16 tile of every level, bounded by (CW/16 + 2^L)(CH/16 + 2^L) per level
+    size_t nflags = 0;
+    for (int L = 0; L < c->N; ++L)
+      nflags += (size_t)(c->CW / 16 + (1 << L) + 1) * (size_t)(c->CH / 16 + (1 << L) + 1);
+    const hipError_t e = rc_chain_reserve(c->chain, nflags);
+    if (e != hipSuccess) {
+      free_chain(c);
+      return hip_fail(c, e, "cascade chain flags");
+    }
   }
   const bool pal = c->rc_pal && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch) &&
                    (size_t)c->sd.pitch * c->H <= ((size_t)1 << 26);

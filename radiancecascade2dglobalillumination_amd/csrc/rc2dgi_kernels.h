@@ -138,6 +138,8 @@ bool rc_chain_ok(int nlev);
 hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDims s, CascadeDims c, int unr,
                            hipStream_t st, bool tight = false);
 int rc_chain_timeouts(RcChain *ch, hipStream_t st);
+// the argument block, error word and `nflags` readiness flags (zeroed), made at configuration time
+hipError_t rc_chain_reserve(RcChain *ch, size_t nflags);
 
 int dist_cmin_shift(int W, int H);
 // hitc (optional): per cell 1 when a texel the march may sample there passes the hit test (the REPEAT wrap of

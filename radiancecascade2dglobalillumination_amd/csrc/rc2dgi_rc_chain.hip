@@ -40,6 +40,28 @@ void rc_chain_destroy(RcChain *ch) {
   delete ch;
 }
 
+hipError_t rc_chain_reserve(RcChain *ch, size_t nflags) {
+  if (!ch) return hipErrorInvalidValue;
+  if (!ch->dev) {
+    hipError_t e = hipMalloc(&ch->dev, sizeof(RcChainArgs));
+    if (e == hipSuccess) e = hipMalloc(&ch->err, 4);
+    if (e == hipSuccess) e = hipMemset(ch->err, 0, 4);
+    if (e != hipSuccess) return e;
+  }
+  if (nflags > ch->nflags) {
+    if (ch->flags) (void)hipFree(ch->flags);
+    ch->flags = nullptr;
+    ch->nflags = 0;
+    hipError_t e = hipMalloc(&ch->flags, nflags * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(ch->flags, 0, nflags * sizeof(unsigned));
+    if (e != hipSuccess) return e;
+    ch->nflags = nflags;
+    ch->epoch = 0;
+    ch->uploaded = false;
+  }
+  return hipSuccess;
+}
+
 int rc_chain_timeouts(RcChain *ch, hipStream_t st) {
   if (!ch || !ch->err) return 0;
   unsigned v = 0;
@@ -82,22 +104,8 @@ hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDi
     foff[i] = nflags;
     nflags += (size_t)nwg;
   }
-  if (!ch->dev) {
-    hipError_t e = hipMalloc(&ch->dev, sizeof(RcChainArgs));
-    if (e == hipSuccess) e = hipMalloc(&ch->err, 4);
-    if (e == hipSuccess) e = hipMemsetAsync(ch->err, 0, 4, st);
-    if (e != hipSuccess) return e;
-  }
-  if (nflags > ch->nflags) {
-    if (ch->flags) (void)hipFree(ch->flags);
-    ch->flags = nullptr;
-    ch->nflags = 0;
-    hipError_t e = hipMalloc(&ch->flags, nflags * sizeof(unsigned));
-    if (e == hipSuccess) e = hipMemsetAsync(ch->flags, 0, nflags * sizeof(unsigned), st);
-    if (e != hipSuccess) return e;
-    ch->nflags = nflags;
-    ch->epoch = 0;
-  }
+  // (the buffers were reserved when the chain was set up, rc_chain_reserve: a frame never allocates)
+  if (!ch->dev || nflags > ch->nflags) return hipErrorInvalidValue;
   h.err = ch->err;
   for (int i = 0; i < nlev; ++i) {
     h.lv[i].flags = i + 1 < nlev ? ch->flags + foff[i] : nullptr;  // (nobody waits for level 0)
