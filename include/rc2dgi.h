@@ -177,8 +177,9 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     distRT where its cells are >= 64 texels (square power-of-two screens >= 4096)
  *   "shade_split"     1 (default): that pass split in two, a light scan of every cell and the records and
  *                     surface palettes of the cells holding a hittable texel
- *   "side_overlap"    0 (default); 1: with the split pass, the directional clear table on a second stream
- *                     beside the records of the hit cells (the fork / join costs more than it overlaps)
+ *   "side_overlap"    with the split pass, the directional clear table beside the records of the hit cells:
+ *                     2 (default): its workgroups appended to the records launch; 1: on a second stream (the
+ *                     fork / join costs more than it overlaps); 0: after the records, one launch of its own
  *   "jfa_rt"          rows per lane of the JumpFlood steps on small non-power-of-two screens: 1 (default),
  *                     2, 4
  *   "rc_chain"        0 (default); 1 / 2: the levels below the top in ONE launch of 16x16x1 tiles, a tile

@@ -108,7 +108,8 @@ struct rc2dgi_ctx {
   float4 *cell_pal = nullptr;        // kCminDim^2 cells x kCellPalStride palette entries
   unsigned *shade_list = nullptr;    // the split records pass's cell list (launch_shade_cmin, tuning shade_split)
   int shade_split = 1;               // tuning "shade_split": the records / palette pass split at the cells with hits
-  int side_overlap = 0;              // tuning "side_overlap": k_dir_clear on the side stream beside k_shade_cells (measured slower)
+  int side_overlap = 2;              // tuning "side_overlap": k_dir_clear beside k_shade_cells -- 1: on the side stream
+                                     // (measured slower), 2: in its launch (default; 7 us less than 0)
   unsigned split_frames = 0;         // split records passes enqueued (their list counters alternate by this parity)
   // which side tables the last frame built (rc2dgi_download_table answers RC2DGI_E_STATE for the others)
   bool built_hitc = false, built_cmin = false, built_dclr = false, built_pal = false;
@@ -1036,18 +1037,20 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   c->built_cmin = proofs;
   c->built_dclr = mps;
   c->built_pal = pal;
-  bool side = false;  // (k_dir_clear on the side stream)
+  bool side = false, dc_merged = false;  // (k_dir_clear on the side stream / in k_shade_cells' launch)
   if (fused) {
     // (the split pass's parity advances only with the split passes themselves: k_shade_cells clears the other
     // parity's counter for the next one)
     const bool split = pal && c->shade_split && shade_split_ok(c->W, c->H);
     // split pass with directional proofs: k_dir_clear needs only the scan's hit flags, so it runs on the side
     // stream beside k_shade_cells (the few hundred workgroups of the hit cells leave most CUs idle)
-    side = split && mps && c->side_overlap && c->side_stream && c->ev_fork && c->ev_join;
+    side = split && mps && c->side_overlap == 1 && c->side_stream && c->ev_fork && c->ev_join;
+    // side_overlap 2: k_dir_clear's workgroups appended to k_shade_cells' grid instead (one launch, one stream)
+    dc_merged = split && mps && c->side_overlap == 2;
     HIPCHK(c, launch_shade_cmin(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, c->cmin,
                                 mps ? c->hitc : nullptr, st, pal ? c->mfield : nullptr, pal ? c->cell_pal : nullptr,
                                 split ? c->shade_list : nullptr, split ? (int)(c->split_frames++ & 1u) : 0,
-                                side ? c->ev_fork : nullptr));
+                                side ? c->ev_fork : nullptr, dc_merged ? c->dboxes : nullptr, dc_merged ? c->dclr : nullptr));
   } else {
     HIPCHK(c, launch_shade(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, st));
     if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
@@ -1057,7 +1060,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, c->side_stream));
     HIPCHK(c, hipEventRecord(c->ev_join, c->side_stream));
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_join, 0));
-  } else if (mps) {
+  } else if (mps && !dc_merged) {
     HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
   }
   bool gi1final = false;
@@ -1780,13 +1783,15 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
   if (k == "side_overlap") {
     // (the side stream is made on first use only: every extra stream takes a share of the process's hardware
     // queues, and the 8 in-process shards of the strips rehearsal ran 0.8 ms slower with one per context)
-    if (value && !(c->side_stream && c->ev_fork && c->ev_join)) {
+    if (value < 0 || value > 2)
+      return fail(c, RC2DGI_E_ARG, "side_overlap is 0 (off), 1 (side stream), 2 (merged into k_shade_cells)");
+    if (value == 1 && !(c->side_stream && c->ev_fork && c->ev_join)) {
       HIPCHK(c, hipSetDevice(c->device));
       if (!c->side_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
       if (!c->ev_fork) HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
       if (!c->ev_join) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     }
-    c->side_overlap = value != 0;
+    c->side_overlap = value;
     return RC2DGI_OK;
   }
   if (k == "jfa_lds") {

@@ -160,7 +160,8 @@ bool shade_split_ok(int W, int H);
 hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
                              ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st,
                              unsigned short *mf = nullptr, float4 *cpal = nullptr, unsigned *list = nullptr,
-                             int parity = 0, hipEvent_t after_scan = nullptr);  // (split: recorded after the scan)
+                             int parity = 0, hipEvent_t after_scan = nullptr,  // (split: recorded after the scan)
+                             const int4 *boxes = nullptr, unsigned char *dclr = nullptr);  // (split: k_dir_clear merged)
 hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st,
                             unsigned char *hitc = nullptr);
 // Directional clear distances of the march proofs (k_rc_level, one-probe tiles): kDirBins angular bins x

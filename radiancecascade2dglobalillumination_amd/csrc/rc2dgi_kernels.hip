@@ -813,14 +813,37 @@ __global__ __launch_bounds__(256) void k_shade_scan(const unsigned short *__rest
 #ifndef RC2DGI_SHADE_CELLS_NTH
 #define RC2DGI_SHADE_CELLS_NTH 512  // (A/B builds: 1024 lanes, record groups of 4 rows)
 #endif
+constexpr int kShadeCellsWG = 512;
+// k_dir_clear's LDS (dir_clear_block below)
+struct DirClearLds {
+  unsigned short part[kCminDim * 4];  // 16-cell pieces of the rows
+  unsigned long long rows[kCminDim];
+  int4 box[kCminDim];                 // per step: cell offsets x0, x1, y0, y1 relative to the start cell
+};
+__device__ __forceinline__ void dir_clear_block(const unsigned char *__restrict__, const int4 *__restrict__,
+                                                unsigned char *__restrict__, int, int, DirClearLds &);
+// DC (side_overlap 2): k_dir_clear's workgroups appended to the grid, two per workgroup (lanes 0-255 / 256-511),
+// beside the hit cells on the CUs they leave idle -- no second stream, no events
+template <bool DC>
 __global__ __launch_bounds__(RC2DGI_SHADE_CELLS_NTH) void k_shade_cells(const unsigned short *__restrict__ dist,
                                                      const float4 *__restrict__ color, const float4 *__restrict__ emis,
                                                      float4 *__restrict__ shade, ScreenDims s, float reflectivity,
                                                      int csh, unsigned short *__restrict__ mf, float4 *__restrict__ cpal,
-                                                     unsigned *__restrict__ list, int p) {
+                                                     unsigned *__restrict__ list, int p, const unsigned char *__restrict__ hitc,
+                                                     const int4 *__restrict__ boxes, unsigned char *__restrict__ dclr) {
+  if constexpr (DC) {
+    static_assert(RC2DGI_SHADE_CELLS_NTH == 512, "two k_dir_clear workgroups per workgroup");
+    if (blockIdx.x >= (unsigned)kShadeCellsWG) {
+      extern __shared__ unsigned char dc_lds[];
+      DirClearLds *const L = reinterpret_cast<DirClearLds *>(dc_lds);
+      const int h = (int)threadIdx.x >> 8;
+      dir_clear_block(hitc, boxes, dclr, 2 * ((int)blockIdx.x - kShadeCellsWG) + h, (int)threadIdx.x & 255, L[h]);
+      return;
+    }
+  }
   const unsigned n = *(volatile unsigned *)&list[p];
   if (blockIdx.x == 0 && threadIdx.x == 0) list[p ^ 1] = 0u;  // (the next frame's count)
-  for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
+  for (unsigned i = blockIdx.x; i < n; i += kShadeCellsWG) {
     const unsigned cell = list[2 + i];
     shade_cell<true, RC2DGI_SHADE_CELLS_NTH, false>(dist, color, emis, shade, s, reflectivity, csh, nullptr, nullptr, mf, cpal,
                                  (int)(cell % kCminDim), (int)(cell / kCminDim));
@@ -854,32 +877,32 @@ __device__ __forceinline__ unsigned long long bit_transpose64(unsigned long long
   return x;
 }
 
-__global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restrict__ hitc,
-                                                   const int4 *__restrict__ boxes,
-                                                   unsigned char *__restrict__ dclr) {
+// One workgroup's work (bin vb / 16, rows 4 (vb % 16) .. + 3) by 256 threads t; the LDS arrays passed in (the
+// merged launch below runs two per 512-lane workgroup, barriers shared)
+__device__ __forceinline__ void dir_clear_block(const unsigned char *__restrict__ hitc, const int4 *__restrict__ boxes,
+                                                unsigned char *__restrict__ dclr, int vb, int t, DirClearLds &L) {
   constexpr int D = kCminDim, NS = kCminDim;
   static_assert(D == 64, "one 64-bit word per row, a wave per row");
-  __shared__ unsigned short part[D * 4];  // 16-cell pieces of the rows
-  __shared__ unsigned long long rows[D];
-  __shared__ int4 box[NS];                // per step: cell offsets x0, x1, y0, y1 relative to the start cell
-  const int j = blockIdx.x >> 4, c = (int)((blockIdx.x & 15) * 256 + threadIdx.x);
+  unsigned short *const part = L.part;
+  unsigned long long *const rows = L.rows;
+  int4 *const box = L.box;
+  const int j = vb >> 4, c = (vb & 15) * 256 + t;
   {  // thread t packs cells 16 t .. 16 t + 15 (row t / 4, piece t % 4)
-    const uint4 v = reinterpret_cast<const uint4 *>(hitc)[threadIdx.x];
+    const uint4 v = reinterpret_cast<const uint4 *>(hitc)[t];
     unsigned m = 0;
     const unsigned w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int q = 0; q < 16; ++q) m |= ((w[q >> 2] >> (8 * (q & 3))) & 0xFFu) ? 1u << q : 0u;
-    part[threadIdx.x] = (unsigned short)m;
+    part[t] = (unsigned short)m;
   }
-  if (threadIdx.x < NS) box[threadIdx.x] = boxes[j * NS + threadIdx.x];  // host-built (dir_clear_boxes)
+  if (t < NS) box[t] = boxes[j * NS + t];  // host-built (dir_clear_boxes)
   __syncthreads();
-  if (threadIdx.x < D)
-    rows[threadIdx.x] = (unsigned long long)part[4 * threadIdx.x] | (unsigned long long)part[4 * threadIdx.x + 1] << 16 |
-                        (unsigned long long)part[4 * threadIdx.x + 2] << 32 |
-                        (unsigned long long)part[4 * threadIdx.x + 3] << 48;
+  if (t < D)
+    rows[t] = (unsigned long long)part[4 * t] | (unsigned long long)part[4 * t + 1] << 16 |
+              (unsigned long long)part[4 * t + 2] << 32 | (unsigned long long)part[4 * t + 3] << 48;
   __syncthreads();
   const int cy = __builtin_amdgcn_readfirstlane(c / D);
-  const int lane = (int)threadIdx.x & 63;
+  const int lane = t & 63;
   // lane s holds step s of this wave's row: the OR of the grid rows its box covers (the rows do not
   // depend on the cell's column) and the box's column offsets
   const int4 bl = box[lane];
@@ -914,6 +937,13 @@ __global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restri
   const int first_off = min(nsteps, ob ? (int)__builtin_ctzll(ob) : NS);
   const int clear = first_hit < first_off ? first_hit : 255;
   dclr[(size_t)j * D * D + c] = (unsigned char)clear;
+}
+
+__global__ __launch_bounds__(256) void k_dir_clear(const unsigned char *__restrict__ hitc,
+                                                   const int4 *__restrict__ boxes,
+                                                   unsigned char *__restrict__ dclr) {
+  __shared__ DirClearLds L;
+  dir_clear_block(hitc, boxes, dclr, (int)blockIdx.x, (int)threadIdx.x, L);
 }
 
 // ---------------------------------------------------------------- tiled distance field
@@ -1848,7 +1878,8 @@ bool shade_cmin_fused_ok(int W, int H, int pitch) {
 
 hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
                              ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st,
-                             unsigned short *mf, float4 *cpal, unsigned *list, int parity, hipEvent_t after_scan) {
+                             unsigned short *mf, float4 *cpal, unsigned *list, int parity, hipEvent_t after_scan,
+                             const int4 *boxes, unsigned char *dclr) {
   if (!shade_cmin_fused_ok(s.W, s.H, s.pitch)) return hipErrorInvalidValue;
   const int csh = dist_cmin_shift(s.W, s.H);
   if (mf && cpal && list) {
@@ -1859,8 +1890,13 @@ hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, co
       const hipError_t e = hipEventRecord(after_scan, st);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_shade_cells, dim3(512), dim3(RC2DGI_SHADE_CELLS_NTH), 0, st, dist, color, emis, shade, s, reflectivity, csh, mf,
-                       cpal, list, p);
+    if (dclr)
+      hipLaunchKernelGGL(k_shade_cells<true>, dim3(kShadeCellsWG + kDirBins * 16 / 2), dim3(RC2DGI_SHADE_CELLS_NTH),
+                         2 * sizeof(DirClearLds), st, dist, color, emis, shade, s, reflectivity, csh, mf, cpal, list, p,
+                         hitc, boxes, dclr);
+    else
+      hipLaunchKernelGGL(k_shade_cells<false>, dim3(kShadeCellsWG), dim3(RC2DGI_SHADE_CELLS_NTH), 0, st, dist, color, emis,
+                         shade, s, reflectivity, csh, mf, cpal, list, p, nullptr, nullptr, nullptr);
     return hipGetLastError();
   }
   if (mf && cpal)

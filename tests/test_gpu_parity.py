@@ -666,17 +666,19 @@ def test_shade_split_is_bit_identical(RC2DGI, scene):
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
     out = {}
-    for split in (0, 1, 2):  # 2: split, k_dir_clear on the side stream
+    # 2: split, k_dir_clear on the side stream; 3: split, k_dir_clear's workgroups in k_shade_cells' launch
+    for split in (0, 1, 2, 3):
         ctx.set_tuning("shade_split", min(split, 1))
-        ctx.set_tuning("side_overlap", int(split == 2))
+        ctx.set_tuning("side_overlap", max(split - 1, 0))
         assert ctx.get_tuning("shade_split") == min(split, 1)
+        assert ctx.get_tuning("side_overlap") == max(split - 1, 0)
         for frame in range(3):
             ctx.do_rc2dgi()
             ctx.sync()
             out[split, frame] = {"color": ctx.download("color"), "hitc": ctx.download_table("hitc"),
-                                 "cmin": ctx.download_table("cmin")}
+                                 "cmin": ctx.download_table("cmin"), "dclr": ctx.download_table("dclr")}
             out[split, frame].update({f"G{L}": ctx.download_level(L) for L in range(6)})
-    for split in (1, 2):
+    for split in (1, 2, 3):
         for frame in range(3):
             for k in out[0, frame]:
                 a, b = out[0, frame][k], out[split, frame][k]
