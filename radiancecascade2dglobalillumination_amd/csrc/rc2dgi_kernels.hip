@@ -833,6 +833,7 @@ __global__ __launch_bounds__(RC2DGI_SHADE_CELLS_NTH) void k_shade_cells(const un
                                                      const int4 *__restrict__ boxes, unsigned char *__restrict__ dclr) {
   if constexpr (DC) {
     static_assert(RC2DGI_SHADE_CELLS_NTH == 512, "two k_dir_clear workgroups per workgroup");
+    // (after the records' workgroups: with them first, L5 + side kernels took 2.5 us more, ab/ab_dclr_merged.txt)
     if (blockIdx.x >= (unsigned)kShadeCellsWG) {
       extern __shared__ unsigned char dc_lds[];
       DirClearLds *const L = reinterpret_cast<DirClearLds *>(dc_lds);
