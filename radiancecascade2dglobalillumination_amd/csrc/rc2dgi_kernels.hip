@@ -1891,13 +1891,19 @@ hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, co
       const hipError_t e = hipEventRecord(after_scan, st);
       if (e != hipSuccess) return e;
     }
-    if (dclr)
-      hipLaunchKernelGGL(k_shade_cells<true>, dim3(kShadeCellsWG + kDirBins * 16 / 2), dim3(RC2DGI_SHADE_CELLS_NTH),
-                         2 * sizeof(DirClearLds), st, dist, color, emis, shade, s, reflectivity, csh, mf, cpal, list, p,
-                         hitc, boxes, dclr);
-    else
-      hipLaunchKernelGGL(k_shade_cells<false>, dim3(kShadeCellsWG), dim3(RC2DGI_SHADE_CELLS_NTH), 0, st, dist, color, emis,
-                         shade, s, reflectivity, csh, mf, cpal, list, p, nullptr, nullptr, nullptr);
+    if (dclr && (!hitc || !boxes)) return hipErrorInvalidValue;
+    constexpr bool kMerge = RC2DGI_SHADE_CELLS_NTH == 512;  // (two k_dir_clear workgroups per workgroup)
+    if constexpr (kMerge) {
+      if (dclr) {
+        hipLaunchKernelGGL(k_shade_cells<kMerge>, dim3(kShadeCellsWG + kDirBins * 16 / 2), dim3(RC2DGI_SHADE_CELLS_NTH),
+                           2 * sizeof(DirClearLds), st, dist, color, emis, shade, s, reflectivity, csh, mf, cpal, list, p,
+                           hitc, boxes, dclr);
+        return hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL(k_shade_cells<false>, dim3(kShadeCellsWG), dim3(RC2DGI_SHADE_CELLS_NTH), 0, st, dist, color, emis,
+                       shade, s, reflectivity, csh, mf, cpal, list, p, nullptr, nullptr, nullptr);
+    if (dclr) hipLaunchKernelGGL(k_dir_clear, dim3(kDirBins * 16), dim3(256), 0, st, hitc, boxes, dclr);
     return hipGetLastError();
   }
   if (mf && cpal)
