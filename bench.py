@@ -90,6 +90,27 @@ def cpu_baseline(W, H, N, rr, budget_s=12.0):
 GATHER_L2_GLINES, GATHER_MALL_GLINES = 260.0, 73.0
 
 
+def pmc_key(W, H, N, ray_range, storage, scene, orders, variants, knobs=None):
+    """What a committed PMC record was measured on: counters describe one configuration, scene and schedule
+    (the march's line requests and instructions follow the scene's occluders and the workgroup orders), so a
+    bench line carries them only when all of these match (profiles/rc_level_pmc.json, scripts/pmc_summary.py)."""
+    return {"config": f"{W}x{H}_N{N}", "ray_range": float(ray_range), "storage": storage, "scene": scene,
+            "rc_order": [int(x) for x in orders] if orders else "default",
+            "rc_variant": [int(x) for x in variants], "knobs": dict(sorted((knobs or {}).items()))}
+
+
+def find_pmc_record(path, key):
+    """The record of profiles/rc_level_pmc.json measured on exactly `key` (pmc_key), or None."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        doc = json.load(f)
+    for rec in doc.get("records", []):
+        if rec.get("key") == key:
+            return rec
+    return None
+
+
 def gather_roofline(rec, N, level_ms):
     """The march-bound levels' L1->L2 line-request rate (PMC l2_requests from the committed profile
     over this run's level times) against the random-gather ceiling blended by their L2 hit rate
@@ -631,16 +652,20 @@ def main():
     avg_launch_s = (t_rc / 1e3) / (a.steps * N)
     achieved = bytes_launch / avg_launch_s / 1e9
     traffic, gather, valu = None, None, None
-    pmc = os.path.join(ROOT, "profiles", "rc_level_pmc.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            rec = json.load(f)
-        if rec.get("config") == f"{W}x{H}_N{N}" and a.storage == "f32":
-            traffic = rec.get("hbm_bytes_per_launch")
-            gather = gather_roofline(rec, N, lvl_ms / a.steps)
-            mixp = os.path.join(ROOT, "profiles", "rc_isa_mix.json")
-            mix = json.load(open(mixp)) if os.path.exists(mixp) else None
-            valu = valu_roofline(rec, N, lvl_ms / a.steps, mix)
+    knobs = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.tune}
+    if a.load_tuning:
+        knobs = {**tun.get("knobs", {}), **knobs}
+    key = pmc_key(W, H, N, a.ray_range, a.storage, a.scene, orders, variants, knobs)
+    rec = find_pmc_record(os.path.join(ROOT, "profiles", "rc_level_pmc.json"), key)
+    chain = ctx.get_tuning("rc_chain") != 0
+    if rec is not None and not chain:
+        traffic = rec.get("hbm_bytes_per_launch")
+        gather = gather_roofline(rec, N, lvl_ms / a.steps)
+        mixp = os.path.join(ROOT, "profiles", "rc_isa_mix.json")
+        mix = json.load(open(mixp)) if os.path.exists(mixp) else None
+        if mix is not None and mix.get("key") != {k: key[k] for k in ("config", "rc_variant")}:
+            mix = None  # (another schedule's instruction mix: price every instruction at 2 cycles instead)
+        valu = valu_roofline(rec, N, lvl_ms / a.steps, mix)
     line = {
         "metric": (f"Mpixel*cascades/s (RC pass) at {W}^2, cascadeCount={N}" if W == H else
                    f"Mpixel*cascades/s (RC pass) at {W}x{H}, cascadeCount={N}"),
@@ -665,13 +690,20 @@ def main():
                    "rc_skip": ctx.get_tuning("rc_skip"),
                    "rc_schedule": (os.path.relpath(a.load_tuning, ROOT) if a.load_tuning else
                                    ("default" if a.no_autotune else "autotune in setup"))},
+        "pmc_key": key,
         "rc_ms_per_frame": round(t_rc / a.steps, 4),
         "rc_level_ms": [round(x / a.steps, 4) for x in lvl_ms.tolist()],
-        "rc_level_timing": f"{lvl_steps} further frames with an event around every level (timing mode 1)",
+        "rc_level_timing": (f"{lvl_steps} further frames with an event around every level (timing mode 1)" +
+                            ("; cascade chain on: levels N-2..0 run in ONE launch, booked on level N-2 (the lower "
+                             "levels' entries are event gaps, not level times)" if chain else "")),
         "full_pipeline_ms": round(t_tot / a.steps, 4),
         "full_pipeline_fps": round(1e3 * a.steps / t_tot, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": ("profiles/rc_level_pmc.json record of this config, scene and schedule"
+                                        if traffic is not None else
+                                        "null: no PMC record of this (config, scene, schedule)" +
+                                        (" (cascade chain on: no per-level launches)" if chain else "")),
                      "kernel": "k_rc_level", "bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(avg_launch_s * 1e3, 5)},
     }

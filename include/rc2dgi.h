@@ -44,8 +44,8 @@
 extern "C" {
 #endif
 
-#define RC2DGI_ABI_VERSION 4  /* 2: row-strip sharding entry points; 3: JumpFlood exchange planner;
-                                 4: rc2dgi_config.flags (Linux merge fallback) */
+#define RC2DGI_ABI_VERSION 5  /* 2: row-strip sharding entry points; 3: JumpFlood exchange planner;
+                                 4: rc2dgi_config.flags (Linux merge fallback); 5: RC2DGI_E_DEVICE */
 
 typedef struct rc2dgi_ctx rc2dgi_ctx;
 
@@ -56,7 +56,9 @@ typedef enum rc2dgi_status {
   RC2DGI_E_HIP = -3,          /* HIP runtime error (message in rc2dgi_last_error) */
   RC2DGI_E_OOM = -4,          /* device allocation failed */
   RC2DGI_E_UNSUPPORTED = -5,  /* valid request this build does not implement */
-  RC2DGI_E_STATE = -6         /* call not valid in the current state */
+  RC2DGI_E_STATE = -6,        /* call not valid in the current state */
+  RC2DGI_E_DEVICE = -7        /* a device-side check failed: an enqueued frame's results are wrong (the cascade
+                                 chain's wait timed out; reported by the next rc2dgi_sync / _download / _do) */
 } rc2dgi_status;
 
 typedef enum rc2dgi_storage {
@@ -184,7 +186,10 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     2, 4
  *   "rc_chain"        0 (default); 1 / 2: the levels below the top in ONE launch of 16x16x1 tiles, a tile
  *                     starting when the upper tiles under its footprint are written (2: unrolled march);
- *                     4: the top level in that launch too; f32 cascades, one process
+ *                     4: the top level in that launch too; f32 cascades, one process.  A wait that times out
+ *                     makes the next rc2dgi_sync / rc2dgi_download / rc2dgi_do return RC2DGI_E_DEVICE and turns
+ *                     the chain off for the context (never a silent wrong frame)
+ *   "rc_chain_spin"   diagnostic: polls per chain wait (0: the default bound; -1: every wait times out at once)
  * rc2dgi_get_tuning also answers "rc_variant_count" and "rc_chain_timeouts" (workgroups of the chained
  * frames since the chain was set up that stopped waiting for their upper tiles: 0 in a correct run;
  * synchronises). */

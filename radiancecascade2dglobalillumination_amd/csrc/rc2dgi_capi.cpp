@@ -154,6 +154,7 @@ struct rc2dgi_ctx {
   std::vector<float4 *> level_bufs;  // debug copies of G_L
   int rc_chain = 0;                  // tuning "rc_chain": levels N-2 .. 0 in one launch (1; 2: unrolled march)
   RcChain *chain = nullptr;          // its argument block and readiness flags (rc2dgi_rc_chain.hip)
+  int rc_chain_spin = 0;             // tuning "rc_chain_spin": polls per wait (0 default; -1 diagnostic: all time out)
   std::vector<float4 *> chain_bufs;  // per level >= 2: its own G_L (the chain's levels overlap)
   // row-strip sharding
   RcMapCache rc_maps;  // host-built k_rc_level workgroup maps
@@ -254,6 +255,17 @@ void free_chain(rc2dgi_ctx *c) {
 // the cascade chain runs this frame: asked for, f32 cascades, one process (whole levels), >= 3 levels
 bool chain_active(const rc2dgi_ctx *c) {
   return c->rc_chain && c->storage == RC2DGI_STORAGE_F32 && c->world == 1 && c->N >= 3 && rc_chain_ok(c->N);
+}
+
+// A chained frame whose workgroup stopped waiting for its upper tiles merged texels that were not written: no
+// silent wrong frame.  The kernel sets a host-mapped word; the next rc2dgi_sync / rc2dgi_download /
+// rc2dgi_do returns RC2DGI_E_DEVICE and the context falls back to one launch per level from then on.
+int check_chain(rc2dgi_ctx *c) {
+  if (!c->chain || !rc_chain_take_error(c->chain)) return RC2DGI_OK;
+  c->rc_chain = 0;
+  return fail(c, RC2DGI_E_DEVICE,
+              "cascade chain: a workgroup stopped waiting for its upper tiles, so a frame's cascades are wrong "
+              "(rc_chain_timeouts counts them); the chain is off for this context from now on");
 }
 
 void free_buffers(rc2dgi_ctx *c) {
@@ -1126,7 +1138,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   }
   if (chain) {
     HIPCHK(c, launch_rc_chain(c->chain, chain_args.data(), (int)chain_args.size(), c->sd, c->cd,
-                              c->rc_chain == 2 ? 32 : 1, st, c->rc_chain == 3));
+                              c->rc_chain == 2 ? 32 : 1, st, c->rc_chain == 3, c->rc_chain_spin));
     // (per-level events: the whole chain counts as its first level, the levels below it as 0)
     if (LT)
       for (int L = c->N - (c->rc_chain == 4 ? 1 : 2); L >= 1; --L) HIPCHK(c, hipEventRecord(c->ev_level[L], st));
@@ -1201,6 +1213,7 @@ void dist_strip(const rc2dgi_ctx *c, int q, unsigned short **p, size_t *bytes) {
 int rc2dgi_do(rc2dgi_ctx *c) {
   if (!c) return RC2DGI_E_ARG;
   RC2DGI_USABLE(c);
+  if (int rc = check_chain(c)) return rc;  // (an earlier chained frame that has completed)
   if (c->world > 1 && !c->comm)
     return fail(c, RC2DGI_E_STATE, "sharded context: use rc2dgi_shard_connect, rc2dgi_do_group or rc2dgi_do_phase");
   const FramePlan plan = make_plan(c);
@@ -1242,6 +1255,18 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   if (int rc = prepare_side_buffers(c, true)) return rc;  // every copy a candidate variant reads
   const int timing = c->timing;
   c->timing = 1;
+  // the chain books its levels on its first level's event and ignores rc_variant below the top: the per-level
+  // picks are made on separate launches, and the chain setting comes back afterwards
+  const int chain = c->rc_chain;
+  c->rc_chain = 0;
+  struct Restore {
+    rc2dgi_ctx *c;
+    int timing, chain;
+    ~Restore() {
+      c->timing = timing;
+      c->rc_chain = chain;
+    }
+  } restore{c, timing, chain};
   const int nc = (int)(sizeof(kOrderCandidates) / sizeof(kOrderCandidates[0]));
   // march rolled / unrolled x linear / 8x8-tiled / packed / nibble-predicted distance field; 32x8 tiles
   // (x2 probes per lane); one probe per lane in 512- and 1024-lane workgroups
@@ -1664,7 +1689,7 @@ int rc2dgi_sync(rc2dgi_ctx *c) {
   if (!c) return RC2DGI_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  return RC2DGI_OK;
+  return check_chain(c);
 }
 
 int rc2dgi_set_stream(rc2dgi_ctx *c, void *s) {
@@ -1842,6 +1867,11 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     if (!value) free_chain(c);
     return prepare_side_buffers(c);
   }
+  if (k == "rc_chain_spin") {  // diagnostic: polls per wait of the chain (0 default; -1: every wait times out)
+    if (value < -1) return fail(c, RC2DGI_E_ARG, "rc_chain_spin is -1, 0 or a poll count");
+    c->rc_chain_spin = value;
+    return RC2DGI_OK;
+  }
   if (k.rfind("rc_noproof_L", 0) == 0) {
     const int L = std::atoi(k.c_str() + 12);
     if (L < 0 || L >= c->N) return fail(c, RC2DGI_E_ARG, "level out of range");
@@ -1932,7 +1962,7 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
     return RC2DGI_OK;
   }
   if (k == "rc_chain_timeouts") {  // workgroups of the chain that stopped waiting (synchronises; 0 in a correct run)
-    *value = chain_active(c) && c->chain ? rc_chain_timeouts(c->chain, c->stream) : 0;
+    *value = c->chain ? rc_chain_timeouts(c->chain, c->stream) : 0;
     return RC2DGI_OK;
   }
   if (k.rfind("rc_noproof_L", 0) == 0) {
@@ -2001,6 +2031,7 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
   if (pitch_bytes < row) return fail(c, RC2DGI_E_ARG, "pitch smaller than a row");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (int rc = check_chain(c)) return rc;
   std::vector<float4> img((size_t)w * h);
   auto fetch4 = [&](const float4 *src) -> int {
     HIPCHK(c, hipMemcpy2D(img.data(), (size_t)w * 16, src, (size_t)pitch * 16, (size_t)w * 16, h,

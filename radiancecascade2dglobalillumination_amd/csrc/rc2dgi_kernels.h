@@ -135,9 +135,13 @@ struct RcChain;
 RcChain *rc_chain_create();
 void rc_chain_destroy(RcChain *ch);
 bool rc_chain_ok(int nlev);
+// spin: polls per wait before a workgroup gives up (0: the default bound; < 0 diagnostic: every wait times out)
 hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDims s, CascadeDims c, int unr,
-                           hipStream_t st, bool tight = false);
+                           hipStream_t st, bool tight = false, int spin = 0);
 int rc_chain_timeouts(RcChain *ch, hipStream_t st);
+// a chained frame that completed since the last call had a workgroup stop waiting (its results are wrong): reads
+// and clears the host-mapped error word the kernel sets; no synchronisation (frames still running report later)
+bool rc_chain_take_error(RcChain *ch);
 // the argument block, error word and `nflags` readiness flags (zeroed), made at configuration time
 hipError_t rc_chain_reserve(RcChain *ch, size_t nflags);
 

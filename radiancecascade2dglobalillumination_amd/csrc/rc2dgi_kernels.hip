@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 namespace rc2dgi {
@@ -835,7 +836,7 @@ __global__ __launch_bounds__(RC2DGI_SHADE_CELLS_NTH) void k_shade_cells(const un
     static_assert(RC2DGI_SHADE_CELLS_NTH == 512, "two k_dir_clear workgroups per workgroup");
     // (after the records' workgroups: with them first, L5 + side kernels took 2.5 us more, ab/ab_dclr_merged.txt)
     if (blockIdx.x >= (unsigned)kShadeCellsWG) {
-      extern __shared__ unsigned char dc_lds[];
+      extern __shared__ __attribute__((aligned(16))) unsigned char dc_lds[];  // (DirClearLds holds int4 / u64)
       DirClearLds *const L = reinterpret_cast<DirClearLds *>(dc_lds);
       const int h = (int)threadIdx.x >> 8;
       dir_clear_block(hitc, boxes, dclr, 2 * ((int)blockIdx.x - kShadeCellsWG) + h, (int)threadIdx.x & 255, L[h]);
@@ -1609,6 +1610,7 @@ unsigned long long *diag_stats_buffer() {
 // the level's parameters that do not depend on the tile shape (rc_tile_params adds those)
 RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c) {
   RcParams P;
+  std::memset(&P, 0, sizeof(P));  // (padding too: the chain compares whole argument blocks, rc2dgi_rc_chain.hip)
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   P.stats = diag_stats_buffer();
 #endif
@@ -1884,14 +1886,15 @@ hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, co
   if (!shade_cmin_fused_ok(s.W, s.H, s.pitch)) return hipErrorInvalidValue;
   const int csh = dist_cmin_shift(s.W, s.H);
   if (mf && cpal && list) {
+    // every argument check before the first launch: an error leaves nothing enqueued
     if (!shade_split_ok(s.W, s.H)) return hipErrorInvalidValue;
+    if (dclr && (!hitc || !boxes)) return hipErrorInvalidValue;
     const int p = parity & 1;
     hipLaunchKernelGGL(k_shade_scan<2>, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, s, csh, cmin, hitc, mf, list, p);
     if (after_scan) {  // (the bound table and hit flags are final here)
       const hipError_t e = hipEventRecord(after_scan, st);
       if (e != hipSuccess) return e;
     }
-    if (dclr && (!hitc || !boxes)) return hipErrorInvalidValue;
     constexpr bool kMerge = RC2DGI_SHADE_CELLS_NTH == 512;  // (two k_dir_clear workgroups per workgroup)
     if constexpr (kMerge) {
       if (dclr) {

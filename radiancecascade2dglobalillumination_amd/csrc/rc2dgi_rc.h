@@ -67,9 +67,11 @@ struct RcChainLevel {
 };
 struct RcChainArgs {
   RcChainLevel lv[kChainMax];
-  unsigned *err;  // workgroups that stopped waiting (rc_chain_timeouts)
+  unsigned *err;   // workgroups that stopped waiting (rc_chain_timeouts; device word)
+  unsigned *herr;  // host-mapped word set to 1 by such a workgroup: rc2dgi_sync / rc2dgi_do report it
   int n;
-  int pad;
+  int spin;        // polls before giving up: 0 kChainSpin; < 0 (diagnostic knob rc_chain_spin -1): every wait
+                   // counts as timed out at once, so the error path can be tested deterministically
 };
 
 // (block, tile) segments of the upper texture's columns (or rows) [lo, hi) (global, REPEAT-wrapped): up to 6,
@@ -456,10 +458,16 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         const int ncy = chain_segments(wy0, wy1, P.c.CH, uby, TY, bys, tys);
         const bool all = __any(ncx < 0 || ncy < 0 || ncx > 4 || ncy > 4);  // (other shapes: every upper tile)
         unsigned timeouts = 0;
+        const int spin_k = ld_uniform(&C->spin);
+        const unsigned spin = spin_k > 0 ? (unsigned)spin_k : kChainSpin;
         auto wait_slot = [&](unsigned slot) {
+          if (spin_k < 0) {  // (diagnostic: forced timeout)
+            ++timeouts;
+            return;
+          }
           unsigned it = 0;
           while (__hip_atomic_load(uf + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ch_epoch) {
-            if (++it >= kChainSpin) {
+            if (++it >= spin) {
               ++timeouts;
               break;
             }
@@ -472,7 +480,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
           const unsigned nup = (unsigned)(4 * P.bsc * P.bsc) * (unsigned)utpb;
           for (unsigned q = (unsigned)lane; q < nup; q += 64) wait_slot(q);
         }
-        if (timeouts) atomicAdd(ld_uniform(&C->err), timeouts);
+        if (timeouts) {
+          // the count on the device, and the host-mapped error word the next rc2dgi_sync / rc2dgi_do reads: this
+          // frame merged upper tiles that were not written, so it must not come back with status 0 (vector
+          // stores from the lanes that timed out)
+          atomicAdd(ld_uniform(&C->err), timeouts);
+          __hip_atomic_store(ld_uniform(&C->herr), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
       }
       __syncthreads();
     }
@@ -534,7 +548,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // miss proof goes to the queue at once (no lockstep iterations).
   __shared__ uint2 s_q[TLC ? NT * NR : 1];
   __shared__ unsigned s_qn;
-  const bool tl = TLC && P.tailk != 0;
 #ifdef RC2DGI_DIAG_LDS_PAD  // diagnostic build: one workgroup per CU (LDS-limited residency)
   __shared__ unsigned s_pad[RC2DGI_DIAG_LDS_PAD];
   if (P.level == 99) s_pad[threadIdx.x] = 0u;
@@ -567,8 +580,38 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // than s cells (kclr = cell texels / texels per unit t).  The test of a ray's first sample proves most
   // misses before any gather (at L4 on the demo scene 72 % of the rays; samples per ray 2.10 -> 1.24 with
   // the per-sample test, scripts/dirproof_model.py).
-  const bool dp = TLC && P.dclr != nullptr && !(RC2DGI_DIAG_ABL & 4);
-  const bool cm = CMS && P.cmin != nullptr && !dp && !(RC2DGI_DIAG_ABL & 4);
+  const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
+  // Far intervals, whole workgroup (t0 >= 1/4: the top levels).  A ray whose first position is off screen takes no
+  // sample (RadianceCascades.fs:65-69) and returns (0,0,0,1).  The first positions o + (t0 dir) asp of the tile's
+  // probes are monotone in the probe index on each axis (every step of the march's own expression is a correctly
+  // rounded monotone operation), so the tile's extreme probes bound all of them exactly.  When, for each of the
+  // four directions, that range lies off screen on one axis, no ray of the workgroup samples: it skips the proof
+  // table's load and barrier, the march and the tail queue, and goes straight to the merge (the top level: the sky
+  // terms; below it: the staged upper cascade).  Same arithmetic for every texel it stores.  At 4096^2 N=6 this is
+  // 47 % of the top level's workgroups; at rayRange 64 every workgroup of the two top levels.
+  bool wg_off = false;
+  if constexpr (TLC && !CH) {
+    if (P.t0 >= 0.25f && !(P.t0 > P.t1)) {
+      const int cxl = min(cx0 + TX, P.bdx) - 1, cyl = min(cy0 + THY, P.p1) - 1;
+      const bool pw = P2S || P.c.powW, ph = P2S || P.c.powH;
+      const float oxl = div_res(((float)cx0 + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, pw);
+      const float oxh = div_res(((float)cxl + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, pw);
+      const float oyl = div_res(((float)cy0 + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, ph);
+      const float oyh = div_res(((float)cyl + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, ph);
+      bool off = cxl >= cx0 && cyl >= cy0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float2 d = ld_uniform(dirs + bi0 * 4 + r);
+        const float sx = (P.t0 * d.x) * P.aspy, sy = (P.t0 * d.y) * P.aspx;
+        // (-0 or NaN never count as off: the test only claims what every lane's own test concludes)
+        off = off && ((oxh + sx) < 0.0f || (oxl + sx) > 1.0f || (oyh + sy) < 0.0f || (oyl + sy) > 1.0f);
+      }
+      wg_off = off;
+    }
+  }
+  const bool tl = TLC && P.tailk != 0 && !wg_off;
+  const bool dp = TLC && P.dclr != nullptr && !(RC2DGI_DIAG_ABL & 4) && !wg_off;
+  const bool cm = CMS && P.cmin != nullptr && !dp && !(RC2DGI_DIAG_ABL & 4) && !wg_off;
   // (one bin per workgroup: bi0 * kDirBins / 4^L, exact for 4^L >= kDirBins; as a shift, since the product
   // overflows 32 bits from level 13 on)
   static_assert(kDirBins == 64, "the bin shift below assumes 64 = 4^3 bins");
@@ -582,7 +625,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       if (CM4 % NT == 0 || (int)threadIdx.x + j * NT < CM4) cmv[j] = ctab[threadIdx.x + j * NT];
   }
 
-  const int cx0 = tx * TX, cy0 = P.p0 + ty * THY;
 
   const int cx = cx0 + (int)(threadIdx.x % TX);
   const int cyb = cy0 + (int)(threadIdx.x / TX);
@@ -716,7 +758,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr float kDone = __builtin_inff();
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
-    t[k] = pok[k / ND] && !(P.t0 > P.t1) ? P.t0 : kDone;
+    t[k] = pok[k / ND] && !(P.t0 > P.t1) && !wg_off ? P.t0 : kDone;
     hit_idx[k] = -1;
   }
   // Far intervals (t0 >= 1/4: the top levels, where most rays start beyond the screen edge): a ray
@@ -724,7 +766,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // ends here -- and a wave whose rays all start off screen skips the march.  The position is the
   // march's own expression.
   if constexpr (TLC) {
-    if (P.t0 >= 0.25f) {
+    if (P.t0 >= 0.25f && !wg_off) {
 #pragma unroll
       for (int k = 0; k < NR; ++k) {
         const f2v_t pxy =

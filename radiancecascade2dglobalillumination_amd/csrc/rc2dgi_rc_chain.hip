@@ -10,7 +10,8 @@
 // Launch order: the levels' workgroups in consecutive ranges, upper levels first; a workgroup only waits for
 // workgroups of lower launch index, so with in-order dispatch the oldest unfinished workgroup never waits.  The
 // wait is bounded anyway (kChainSpin polls): a timeout sets the error word (rc_chain_timeouts) and the workgroup
-// goes on, so a broken assumption shows as wrong results, never as a hung GPU.
+// goes on, so a broken assumption never hangs the GPU; it sets a host-mapped error word, and the next
+// rc2dgi_sync / rc2dgi_do / rc2dgi_download returns RC2DGI_E_DEVICE for that frame and turns the chain off.
 //
 // The kernel is k_rc_level<16, 16, 1, 1, ..., CH = true> (rc2dgi_rc.h: the wait, the sc1 hand-off, the flags);
 // this file builds its argument block and launches it.
@@ -28,6 +29,8 @@ struct RcChain {
   unsigned *flags = nullptr;   // readiness flags of every level
   size_t nflags = 0;
   unsigned *err = nullptr;     // timeouts (device word)
+  unsigned *herr = nullptr;    // host-mapped error word (set by a workgroup that timed out)
+  unsigned *herr_dev = nullptr;  // (its device address)
   unsigned epoch = 0;
 };
 
@@ -37,6 +40,7 @@ void rc_chain_destroy(RcChain *ch) {
   if (!ch) return;
   for (void *p : {(void *)ch->dev, (void *)ch->flags, (void *)ch->err})
     if (p) (void)hipFree(p);
+  if (ch->herr) (void)hipHostFree(ch->herr);
   delete ch;
 }
 
@@ -46,7 +50,10 @@ hipError_t rc_chain_reserve(RcChain *ch, size_t nflags) {
     hipError_t e = hipMalloc(&ch->dev, sizeof(RcChainArgs));
     if (e == hipSuccess) e = hipMalloc(&ch->err, 4);
     if (e == hipSuccess) e = hipMemset(ch->err, 0, 4);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&ch->herr), 4, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&ch->herr_dev), ch->herr, 0);
     if (e != hipSuccess) return e;
+    *reinterpret_cast<volatile unsigned *>(ch->herr) = 0u;
   }
   if (nflags > ch->nflags) {
     if (ch->flags) (void)hipFree(ch->flags);
@@ -69,12 +76,21 @@ int rc_chain_timeouts(RcChain *ch, hipStream_t st) {
   return (int)v;
 }
 
+bool rc_chain_take_error(RcChain *ch) {
+  if (!ch || !ch->herr) return false;
+  volatile unsigned *w = ch->herr;
+  if (*w == 0u) return false;
+  *w = 0u;
+  return true;
+}
+
 bool rc_chain_ok(int nlev) { return nlev >= 1 && nlev <= kChainMax; }
 
 hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDims s, CascadeDims c, int unr,
-                           hipStream_t st, bool tight) {
+                           hipStream_t st, bool tight, int spin) {
   if (!ch || !rc_chain_ok(nlev) || c.gi_f16 || c.gi_u8) return hipErrorInvalidValue;
-  RcChainArgs h{};
+  RcChainArgs h;
+  std::memset(&h, 0, sizeof(h));  // (padding too: the block is compared bytewise below)
   h.n = nlev;
   h.err = nullptr;  // (set below, once allocated)
   unsigned wg0 = 0;
@@ -82,7 +98,8 @@ hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDi
   std::vector<size_t> foff(nlev);
   for (int i = 0; i < nlev; ++i) {
     RcChainLevel &l = h.lv[i];
-    l.P = rc_level_params(a[i], s, c);
+    const RcParams lp = rc_level_params(a[i], s, c);
+    std::memcpy(&l.P, &lp, sizeof(lp));  // (bytewise, padding included)
     if (l.P.p0 != 0 || l.P.p1 != l.P.bdy) return hipErrorInvalidValue;  // whole levels (no row strips)
     const int nwg = rc_tile_params<16, 16, 1, 1, 0>(a[i], l.P);
     if (nwg == 0) return hipErrorOutOfMemory;
@@ -107,6 +124,8 @@ hipError_t launch_rc_chain(RcChain *ch, const RcLevelArgs *a, int nlev, ScreenDi
   // (the buffers were reserved when the chain was set up, rc_chain_reserve: a frame never allocates)
   if (!ch->dev || nflags > ch->nflags) return hipErrorInvalidValue;
   h.err = ch->err;
+  h.herr = ch->herr_dev;
+  h.spin = spin;
   for (int i = 0; i < nlev; ++i) {
     h.lv[i].flags = i + 1 < nlev ? ch->flags + foff[i] : nullptr;  // (nobody waits for level 0)
     h.lv[i].uflags = i > 0 ? ch->flags + foff[i - 1] : nullptr;

@@ -31,7 +31,7 @@ RT = {"color": 0, "emissive": 1, "jump1": 2, "jump2": 3, "dist": 4, "gi1": 5, "g
       "final_gi": 9}
 SCREEN_RTS = ("color", "emissive", "jump1", "jump2", "dist", "temp")
 FMT_RGBA8, FMT_RGBA32F = 0, 1
-STATUS = {0: "OK", -1: "E_ARG", -2: "E_UNIFORM", -3: "E_HIP", -4: "E_OOM", -5: "E_UNSUPPORTED", -6: "E_STATE"}
+STATUS = {0: "OK", -1: "E_ARG", -2: "E_UNIFORM", -3: "E_HIP", -4: "E_OOM", -5: "E_UNSUPPORTED", -6: "E_STATE", -7: "E_DEVICE"}
 PASS_NAMES = ("screenuv", "jfa", "rc", "blur", "merge", "total")
 
 

@@ -15,7 +15,16 @@ if [ -n "$TESTK" ]; then
     --timeout-method thread -m gpu -k "$TESTK" tests > gpurun_out/exp_test.log 2>&1
   rc=$?; tail -3 gpurun_out/exp_test.log; [ $rc -eq 0 ] || exit $rc
 fi
-if [ -n "$LIBS" ]; then echo "== A/B libraries"; ROUNDS=${ROUNDS:-3} bash scripts/ab_lib.sh || exit $?; fi
+#   AB_ARGS     ';'-separated bench argument sets for the LIBS A/B (default: the headline only), e.g.
+#               AB_ARGS="; --size 4096 --cascades 8 --ray-range 64"
+if [ -n "$LIBS" ]; then
+  IFS=';' read -r -a ABS <<< "${AB_ARGS:-}"
+  [ ${#ABS[@]} -eq 0 ] && ABS=("")
+  for args in "${ABS[@]}"; do
+    echo "== A/B libraries: ${args:-headline}"
+    BENCH_ARGS="$args" ROUNDS=${ROUNDS:-3} bash scripts/ab_lib.sh || exit $?
+  done
+fi
 if [ -n "$CFGS" ]; then echo "== A/B knobs"; ROUNDS=${ROUNDS:-3} bash scripts/ab_knobs.sh || exit $?; fi
 if [ -n "$PROBE" ]; then
   echo "== schedule probe: $PROBE"

@@ -5,7 +5,10 @@ RC-level dispatches are identified by their order inside each frame (levels N-1.
 FETCH_SIZE / WRITE_SIZE are in KB (rocprofv3); on gfx950 FETCH_SIZE under-reports a wide
 coalesced stream by 2x (MI355X_MICROARCH.md §HBM) -- both the raw value and the x2
 calibrated value are printed.
-Usage: scripts/pmc_summary.py gpurun_out/pmc [--levels 6] [--json out.json --config 4096x4096_N6]
+Usage: scripts/pmc_summary.py gpurun_out/pmc [--levels 6] [--json out.json [--merge profiles/rc_level_pmc.json]]
+The record is keyed on what it was measured on (bench.py's `pmc_key`: config, rayRange, storage, scene, schedule,
+knobs), read from the bench line of the first pass's log; --merge replaces the record of the same key in an
+existing file and keeps the others (bench.py only uses a record whose key matches its own run).
 """
 import argparse
 import collections
@@ -35,7 +38,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--levels", type=int, default=6)
     ap.add_argument("--json")
-    ap.add_argument("--config", default="4096x4096_N6")
+    ap.add_argument("--merge", help="existing records file to merge the new record into")
     ap.add_argument("--all", action="store_true", help="print every collected counter")
     a = ap.parse_args()
     rows = load(a.dir)
@@ -86,7 +89,16 @@ def main():
         lv = {k: v for k, v in out.items() if k.startswith("k_rc_level")}
         fetch = [v.get("FETCH_SIZE") for v in lv.values()]
         write = [v.get("WRITE_SIZE") for v in lv.values()]
-        rec = {"config": a.config, "kernel": "k_rc_level",
+        key = None
+        for lg in sorted(glob.glob(os.path.join(a.dir, "g*.log"))):
+            for line in open(lg):
+                if line.startswith("{") and '"pmc_key"' in line:
+                    key = json.loads(line)["pmc_key"]
+            if key:
+                break
+        if key is None:
+            raise SystemExit("no bench line with a pmc_key in the passes' logs")
+        rec = {"key": key, "config": key["config"], "kernel": "k_rc_level",
                "note": "HBM bytes per RC-level launch from rocprofv3 PMC (separate passes): "
                        "(2*FETCH_SIZE + WRITE_SIZE)*1024, FETCH doubled per MI355X_MICROARCH.md §HBM",
                "per_level": {k: {"fetch_kb": v.get("FETCH_SIZE"), "write_kb": v.get("WRITE_SIZE"),
@@ -97,8 +109,12 @@ def main():
                                  "dur_us": v["_dur_ns"] / 1e3} for k, v in lv.items()}}
         if all(x is not None for x in fetch + write) and lv:
             rec["hbm_bytes_per_launch"] = sum(2 * f * 1024 + w * 1024 for f, w in zip(fetch, write)) / len(lv)
+        recs = []
+        if a.merge and os.path.exists(a.merge):
+            with open(a.merge) as fh:
+                recs = [r for r in json.load(fh).get("records", []) if r.get("key") != key]
         with open(a.json, "w") as fh:
-            json.dump(rec, fh, indent=1)
+            json.dump({"records": recs + [rec]}, fh, indent=1)
 
 
 if __name__ == "__main__":

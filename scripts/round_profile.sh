@@ -23,7 +23,7 @@ tail -1 gpurun_out/prof.log | cut -c1-200
 echo "== pmc"
 GROUPS_OVERRIDE="FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;SQ_INSTS_VALU SQ_WAVES" STEPS=5 BENCH_ARGS="$SCHED" \
   bash scripts/profile_pmc.sh || exit $?
-python3 scripts/pmc_summary.py gpurun_out/pmc --json gpurun_out/rc_level_pmc.json > gpurun_out/pmc_summary.txt
+python3 scripts/pmc_summary.py gpurun_out/pmc --json gpurun_out/rc_level_pmc.json --merge profiles/rc_level_pmc.json > gpurun_out/pmc_summary.txt
 cut -c1-160 gpurun_out/pmc_summary.txt
 cp gpurun_out/rc_level_pmc.json profiles/rc_level_pmc.json
 echo "== bench"

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.rc2dgi_abi_version() == 4
+    assert lib.rc2dgi_abi_version() == 5
 
 
 def _cfg(**kw):

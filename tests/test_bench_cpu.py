@@ -44,13 +44,27 @@ def test_gather_roofline_blends_the_ceiling_by_hit_rate(bench):
     assert bench.gather_roofline({"per_level": {}}, 4, [0.1] * 4) is None
 
 
-def test_committed_pmc_record_has_the_gather_fields():
-    with open(os.path.join(ROOT, "profiles", "rc_level_pmc.json")) as f:
-        rec = json.load(f)
-    assert rec["config"] == "4096x4096_N6" and rec["hbm_bytes_per_launch"] > 0
-    for L in range(6):
-        lv = rec["per_level"][f"k_rc_level L{L}"]
-        assert lv["l2_requests"] > 0 and 0.0 < lv["l2_hit"] < 1.0 and lv["dur_us"] > 0
+def test_committed_pmc_record_has_the_gather_fields(bench):
+    """Every committed PMC record is keyed on what it measured (config, rayRange, storage, scene, schedule,
+    knobs), one record per key, and the headline's record (demo scene, committed schedule) is there."""
+    path = os.path.join(ROOT, "profiles", "rc_level_pmc.json")
+    with open(path) as f:
+        recs = json.load(f)["records"]
+    keys = [json.dumps(r["key"], sort_keys=True) for r in recs]
+    assert len(set(keys)) == len(keys)
+    for rec in recs:
+        assert rec["config"] == rec["key"]["config"] and rec["hbm_bytes_per_launch"] > 0
+        N = len(rec["key"]["rc_variant"])
+        for L in range(N):
+            lv = rec["per_level"][f"k_rc_level L{L}"]
+            assert lv["l2_requests"] > 0 and 0.0 < lv["l2_hit"] < 1.0 and lv["dur_us"] > 0
+    with open(os.path.join(ROOT, "radiancecascade2dglobalillumination_amd", "tuning", "4096x4096_N6_rr2_f32.json")) as f:
+        sched = json.load(f)
+    key = bench.pmc_key(4096, 4096, 6, 2.0, "f32", "demo", sched["rc_order"], sched["rc_variant"], sched.get("knobs"))
+    assert bench.find_pmc_record(path, key) is not None
+    # another scene (or schedule) finds nothing: its line carries traffic null, not the demo's counters
+    assert bench.find_pmc_record(path, dict(key, scene="random:1")) is None
+    assert bench.find_pmc_record(path, dict(key, rc_order=[0] * 6)) is None
 
 
 def test_valu_roofline_is_issue_time_over_level_time(bench):

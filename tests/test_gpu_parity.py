@@ -654,6 +654,45 @@ def test_cascade_chain_is_bit_identical(RC2DGI, W, H, N, rr, scene):
     ctx.close()
 
 
+@pytest.mark.parametrize("report", ["sync", "download", "do"])
+def test_cascade_chain_timeout_is_an_error(RC2DGI, report):
+    """A chain workgroup that stops waiting merges upper tiles that were not written, so the frame is wrong: the
+    next rc2dgi_sync / rc2dgi_download / rc2dgi_do returns RC2DGI_E_DEVICE (-7), names the chain, and the context
+    falls back to one launch per level -- the following frame is bit-identical to the unchained one.  The
+    diagnostic knob rc_chain_spin -1 makes every wait time out at once (the product bound is 2^20 polls)."""
+    from radiancecascade2dglobalillumination_amd import RC2DGIError
+
+    W, H, N = 1200, 900, 6  # C1, where the committed schedule turns the chain on
+    color, emis = make_scene("demo", W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    ctx.do_rc2dgi()
+    want = ctx.download("color")
+    ctx.set_tuning("rc_chain", 1)
+    ctx.set_tuning("rc_chain_spin", -1)
+    ctx.do_rc2dgi()
+    with pytest.raises(RC2DGIError) as ei:
+        if report == "sync":
+            ctx.sync()
+        elif report == "download":
+            ctx.download("color")
+        else:  # (the frame has completed; rc2dgi_do itself does not synchronise)
+            import torch
+
+            torch.cuda.synchronize()
+            ctx.do_rc2dgi()
+    assert ei.value.code == -7 and "cascade chain" in str(ei.value)
+    assert ctx.get_tuning("rc_chain") == 0  # the fallback
+    assert ctx.get_tuning("rc_chain_timeouts") > 0
+    ctx.set_tuning("rc_chain_spin", 0)
+    ctx.do_rc2dgi()
+    ctx.sync()  # no stale report
+    got = ctx.download("color")
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    ctx.close()
+
+
 @pytest.mark.parametrize("scene", ["demo", "speckled", "rand:45"])
 def test_shade_split_is_bit_identical(RC2DGI, scene):
     """The records / palette pass split at the cells holding a hittable texel (tuning shade_split: k_shade_scan
