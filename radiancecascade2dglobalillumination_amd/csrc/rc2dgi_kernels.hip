@@ -1531,8 +1531,22 @@ static std::vector<uint2> rc_logical_order(int code, int tiles_x, int tiles_y, i
 // eighth of it (xcd_logical_id: a contiguous eighth each -- the occluders, hence the march, are not spread
 // evenly over those eighths); a chunk keeps its locality in one L2.  Whole rounds of 8 chunks only; the
 // remainder keeps the contiguous split.  A bijection for any n.
+// lc = 16 + t (t = 0..7): the Latin-square schedule instead.  The logical order is cut into 8 regions of S = 8 << t
+// sub-chunks each; XCD x's j-th sub-chunk (j = 0 .. S-1, in its dispatch order) is sub-chunk j of region (x + j) mod 8.
+// At any moment the 8 XCDs work in 8 different regions (disjoint working sets, each in its own L2: what the
+// contiguous split had), and every XCD visits every region S / 8 times (the balance the round-robin deal had).
 static int xcd_chunk_logical(int p, int n, int lc) {
   if (lc == 0) return xcd_logical_id(p, n);
+  if (lc >= 16) {
+    const long long S = 8ll << (lc - 16), unit = 8 * S;  // sub-chunks of all regions
+    const long long nf = (long long)n / unit * unit;    // whole sub-chunks only; the remainder stays contiguous
+    if (p < nf) {
+      const long long c = nf / unit, rs = nf / 8;  // sub-chunk and region sizes
+      const long long x = p & 7, i = p >> 3, j = i / c, r = i - j * c;
+      return (int)(((x + j) & 7) * rs + j * c + r);
+    }
+    return (int)(nf + xcd_logical_id((int)(p - nf), (int)(n - nf)));
+  }
   const long long C = 1ll << lc, round = 8 * C;
   const int full = (int)((long long)n / round * round);
   if (p < full) {

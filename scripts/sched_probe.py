@@ -42,7 +42,9 @@ def main():
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--tune", action="append", default=[])
     ap.add_argument("--xcd-chunks", default="", help="comma list of log2 XCD interleave chunks (order code bits 26-30) "
-                    "to combine with every order candidate (0 = the contiguous split)")
+                    "to combine with every order candidate (0 = the contiguous split, 16 + t the Latin-square schedule, "
+                    "c = keep the candidate's own)")
+    ap.add_argument("--scene", default="demo", help="demo | random:<seed> | dense:<seed> (bench.py's scenes)")
     ap.add_argument("cands", nargs="+")
     a = ap.parse_args()
     import bench
@@ -50,7 +52,11 @@ def main():
 
     W, H, N = a.size, a.height or a.size, a.cascades
     g = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, storage=a.storage)
-    color, emis = scenes.demo(W, H)
+    if a.scene == "demo":
+        color, emis = scenes.demo(W, H)
+    else:
+        kind, seed = a.scene.split(":")
+        color, emis = scenes.random_scene(W, H, seed=int(seed), coverage={"random": 0.05, "dense": 0.35}[kind])
     g.upload("color", color)
     g.upload("emissive", emis)
     tun = json.load(open(bench.schedule_path(W, H, N, a.ray_range, a.storage)))
@@ -64,7 +70,7 @@ def main():
         L, vs, os_ = c.split(":")
         L = int(L)
         ol = [str(x) for x in autotune_orders()] if os_ == "all" else os_.split(",")
-        chunks = [int(x) for x in a.xcd_chunks.split(",")] if a.xcd_chunks else [None]
+        chunks = [None if x == "c" else int(x) for x in a.xcd_chunks.split(",")] if a.xcd_chunks else [None]
         for v, o, lc in itertools.product(vs.split(","), ol, chunks):
             v = tun["rc_variant"][L] if v == "c" else int(v)
             o = tun["rc_order"][L] if o == "c" else int(o)

@@ -163,7 +163,7 @@ def test_xcd_interleaved_workgroup_map_is_a_bijection():
 
     _build.build()
     lib = load_library()
-    for tx, ty, ng, lc, base in itertools.product([1, 3, 8, 16], [1, 5, 16], [1, 4, 64], [0, 1, 2, 5, 9],
+    for tx, ty, ng, lc, base in itertools.product([1, 3, 8, 16], [1, 5, 16], [1, 4, 64], [0, 1, 2, 5, 9, 16, 17, 19],
                                                  [0, 4 | 8 << 8 | 4 << 16, 2 | 2 << 8 | 2 << 16 | 1 << 24]):
         n = tx * ty * ng
         m = _plan_wg_map(lib, base | lc << 26, tx, ty, ng)
@@ -180,6 +180,15 @@ def test_xcd_interleaved_workgroup_map_is_a_bijection():
     m = _plan_wg_map(lib, 4 | 8 << 8 | 4 << 16 | 4 << 26, tx, ty, ng)
     x3 = [m[p] for p in range(3, n, 8)]
     assert x3 == [lo[(k // 16) * 128 + 3 * 16 + k % 16] for k in range(n // 8)]
+    # Latin square (lc = 16 + t): 8 regions of S = 8 << t sub-chunks; XCD x's j-th sub-chunk is sub-chunk j of region
+    # (x + j) mod 8, so at each step j the 8 XCDs are in 8 different regions and each XCD visits every region
+    for t in (0, 1):
+        S = 8 << t
+        c = n // (8 * S)
+        m = _plan_wg_map(lib, 4 | 8 << 8 | 4 << 16 | (16 + t) << 26, tx, ty, ng)
+        for x in range(8):
+            xs = [m[p] for p in range(x, n, 8)]
+            assert xs == [lo[((x + k // c) % 8) * (n // 8) + (k // c) * c + k % c] for k in range(n // 8)]
 
 
 def test_oriented_order_lays_patches_along_the_rays():
