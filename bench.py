@@ -625,6 +625,7 @@ def main():
     # levels idles the GPU ~5 us (rocprofv3 trace), which a frame without timing does not.
     ctx.set_timing(2)
     rc_ms, tot_ms, lvl_ms = [], [], np.zeros(N)
+    pass_acc = {}
     rdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -633,6 +634,8 @@ def main():
         t = ctx.pass_times()  # waits for this frame's last event
         rc_ms.append(t["rc"])
         tot_ms.append(t["total"])
+        for k, v in t.items():
+            pass_acc[k] = pass_acc.get(k, 0.0) + v
     ctx.sync()
     torch.cuda.synchronize()
     rdist.barrier()
@@ -697,6 +700,7 @@ def main():
                             ("; cascade chain on: levels N-2..0 run in ONE launch, booked on level N-2 (the lower "
                              "levels' entries are event gaps, not level times)" if chain else "")),
         "full_pipeline_ms": round(t_tot / a.steps, 4),
+        "pass_ms": {k: round(v / a.steps, 4) for k, v in pass_acc.items()},
         "full_pipeline_fps": round(1e3 * a.steps / t_tot, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

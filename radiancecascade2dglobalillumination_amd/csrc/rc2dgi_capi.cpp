@@ -147,6 +147,8 @@ struct rc2dgi_ctx {
   std::vector<int> dp_ok;        // per level: its direction table fits k_dir_clear's bins (upload_tables)
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   int jfa_rt = 1;                // tuning "jfa_rt": rows per lane of the float-path steps on small screens (1, 2, 4)
+  int jfa_rows = 0;              // tuning "jfa_rows": consecutive rows per lane in the short steps (0 off, 4, 8)
+  int rc_tailbar = 0;            // tuning "rc_tailbar": staged footprint written before the tail queue's barrier
   int jfa_coset = 2;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
@@ -901,7 +903,7 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
     const unsigned *src = t == 0 ? c->occ : jfa_out(c, t - 1);
     for (auto &r : plan.jfa[t].iv)
       HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, out, dist, c->sd, ox, oy, st,
-                                r.first, r.second, nullptr, 0, c->jfa_lds, c->jfa_rt));
+                                r.first, r.second, nullptr, 0, c->jfa_lds, c->jfa_rt, c->jfa_rows));
     return RC2DGI_OK;
   }
   // row-strip shard: the own strip, into its window (global row y0 - m = local row 0)
@@ -1121,6 +1123,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
+    a.tail_bar = c->rc_tailbar;
 
     if (chain && (L < c->N - 1 || c->rc_chain == 4)) {
       chain_args.push_back(a);  // (whole levels: one process; rc_chain 4: the top level in the launch too)
@@ -1823,6 +1826,15 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
     c->jfa_lds = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "rc_tailbar") {
+    c->rc_tailbar = value != 0;
+    return RC2DGI_OK;
+  }
+  if (k == "jfa_rows") {
+    if (value != 0 && value != 4 && value != 8) return fail(c, RC2DGI_E_ARG, "jfa_rows is 0, 4 or 8");
+    c->jfa_rows = value;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_rt") {
     if (value != 1 && value != 2 && value != 4) return fail(c, RC2DGI_E_ARG, "jfa_rt is 1, 2 or 4");
     c->jfa_rt = value;
@@ -1919,6 +1931,14 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "jfa_lds") {
     *value = c->jfa_lds;
+    return RC2DGI_OK;
+  }
+  if (k == "rc_tailbar") {
+    *value = c->rc_tailbar;
+    return RC2DGI_OK;
+  }
+  if (k == "jfa_rows") {
+    *value = c->jfa_rows;
     return RC2DGI_OK;
   }
   if (k == "jfa_rt") {

@@ -60,7 +60,9 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
                            int row1 = -1,  // output rows [row0, row1) (-1 = H)
                            const JfaSrc *window = nullptr, int dst_row0 = 0,
                            int lds = 0,   // LDS-staged taps for short power-of-two steps (tuning jfa_lds)
-                           int small_rt = 1);  // rows per lane of the float-path steps on small screens (tuning jfa_rt)
+                           int small_rt = 1,   // rows per lane of the float-path steps on small screens (tuning jfa_rt)
+                           int jrows = 0);     // short isotropic power-of-two steps (S = 1, 2, 4): JR = 4 / 8
+                                               // consecutive rows per lane, each tap row loaded once (jfa_rows)
 // integer taps of the power-of-two JFA kernel (false: the float path runs); also used by the
 // row-strip planner
 bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTaps *tp);
@@ -123,6 +125,8 @@ struct RcLevelArgs {
   int cmin_screen = 0;          // the exit proof also tests the screen edge (worth it for long rays)
   int tail_k = 0;               // tail compaction after this many lockstep march iterations (0: off)
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
+  int tail_bar = 0;             // the staged footprint written before the tail queue's barrier: one barrier when
+                                // the queue is empty (tuning rc_tailbar)
 };
 
 // The cascade chain (rc2dgi_rc_chain.hip, tuning rc_chain): the levels a[0 .. n) (consecutive, downwards; a[0]

@@ -380,6 +380,45 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
   }
 }
 
+// JumpFlood.fs step with a short isotropic offset S (1, 2 or 4 texels on both axes) on a power-of-two screen: a
+// lane owns JR consecutive rows of one column instead of JT rows 4 apart, so the 3 x JR tap rows of its texels are
+// the JR + 2 S rows j0 - S .. j0 + JR - 1 + S, each loaded once (3 (JR + 2 S) loads for JR texels: S = 1 at JR = 8
+// issues 30 tap loads where k_jfa_p2 issues 72).  Same taps, scan order, keys and selection (jfa_best9) as
+// k_jfa_p2, so the same seeds and distances.  Tuning "jfa_rows" (0: off).
+template <int S, int JR, bool IKEY>
+__global__ __launch_bounds__(256) void k_jfa_rows(const unsigned *__restrict__ src, int src_pitch,
+                                                  unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
+                                                  ScreenDims s, JfaTaps o, int row0, int row1) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j0 = row0 + (int)blockIdx.y * (4 * JR) + JR * __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  if (i >= s.W) return;
+  unsigned ti[3];  // byte offsets of the tap columns (scalar row base + 32-bit lane offset addressing)
+#pragma unroll
+  for (int x = 0; x < 3; ++x) ti[x] = ((unsigned)(i + (x - 1) * S) & (unsigned)(s.W - 1)) << 2;
+  constexpr int NR = JR + 2 * S;
+  unsigned v[NR][3];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const char *row = reinterpret_cast<const char *>(src + (size_t)((unsigned)(j0 - S + r) & (unsigned)(s.H - 1)) * src_pitch);
+#pragma unroll
+    for (int x = 0; x < 3; ++x) v[r][x] = *reinterpret_cast<const unsigned *>(row + ti[x]);
+  }
+#pragma unroll
+  for (int t = 0; t < JR; ++t) {
+    const int j = j0 + t;
+    if (j >= row1) break;
+    unsigned sd[9];  // y outer (rows j - S, j, j + S), x inner: JumpFlood.fs's scan order
+#pragma unroll
+    for (int y = 0; y < 3; ++y)
+#pragma unroll
+      for (int x = 0; x < 3; ++x) sd[y * 3 + x] = v[t + y * S][x];
+    float key;
+    const unsigned best = jfa_best9<IKEY>(sd, pack_seed(i, j), o, &key);
+    dst[(size_t)j * s.pitch + i] = best;
+    if (dist) dist[(size_t)j * s.pitch + i] = jfa_dist_q(best, key, i, j, s, o);  // DistanceField.fs
+  }
+}
+
 // ---------------------------------------------------------------- JumpFlood: the long steps in one kernel
 // The long steps (JumpFlood.fs, RC2DGI.cs:296-326).  On a square power-of-two screen step t taps at
 // +-s_t = W / 2^(t+1) texels on both axes, so the texels (x0 + a g, y0 + b g) of one residue
@@ -1335,7 +1374,7 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
 
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0,
-                           int row1, const JfaSrc *window, int dst_row0, int lds, int small_rt) {
+                           int row1, const JfaSrc *window, int dst_row0, int lds, int small_rt, int jrows) {
   JfaSrc win{};
   if (window && !first) win = *window;
   if (row1 < 0 || row1 > s.H) row1 = s.H;
@@ -1359,6 +1398,27 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   const int lattice = p2 && full && (tp.dx[2] >= 128 || tp.dy[2] >= 64) && tp.dx[2] >= 0 && tp.dy[2] >= 0 &&
                       (tp.dx[2] & (tp.dx[2] - 1)) == 0 && (tp.dy[2] & (tp.dy[2] - 1)) == 0 &&
                       tp.dx[2] <= s.W && tp.dy[2] <= s.H;
+  // short isotropic steps: consecutive rows per lane, each tap row loaded once (k_jfa_rows)
+  const int sh = tp.dy[2];
+  if (p2 && !s.u8 && !first && !win.on && dst_row0 == 0 && (jrows == 4 || jrows == 8) && s.W % 64 == 0 &&
+      tp.dx[0] == -sh && tp.dx[1] == 0 && tp.dx[2] == sh && tp.dy[0] == -sh && tp.dy[1] == 0 && (sh == 1 || sh == 2 || sh == 4)) {
+    const bool ikey = s.W == s.H && s.W <= 4096;
+    const dim3 gr(s.W / 64, ceil_div(row1 - row0, 4 * jrows));
+#define RC2DGI_JR(SV, JV)                                                                                         \
+  do {                                                                                                            \
+    if (ikey)                                                                                                     \
+      hipLaunchKernelGGL((k_jfa_rows<SV, JV, true>), gr, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1); \
+    else                                                                                                          \
+      hipLaunchKernelGGL((k_jfa_rows<SV, JV, false>), gr, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1); \
+  } while (0)
+    if (jrows == 8) {
+      if (sh == 1) RC2DGI_JR(1, 8); else if (sh == 2) RC2DGI_JR(2, 8); else RC2DGI_JR(4, 8);
+    } else {
+      if (sh == 1) RC2DGI_JR(1, 4); else if (sh == 2) RC2DGI_JR(2, 4); else RC2DGI_JR(4, 4);
+    }
+#undef RC2DGI_JR
+    return hipGetLastError();
+  }
   if (s.u8 && p2) {  // RGBA8 jumpRT on a power-of-two screen: integer taps, quantized-uv distance
     if (first)
       hipLaunchKernelGGL((k_jfa_p2<true, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp,

@@ -35,6 +35,7 @@ struct RcParams {
   int cscr;             // the exit proof tests the screen edge too
   int tailk;            // tail compaction after this many lockstep iterations (0: off)
   int wgp;              // workgroup-wide exit proof of the first samples
+  int tlb;              // tail_bar (RcLevelArgs)
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
@@ -588,9 +589,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // four directions, that range lies off screen on one axis, no ray of the workgroup samples: it skips the proof
   // table's load and barrier, the march and the tail queue, and goes straight to the merge (the top level: the sky
   // terms; below it: the staged upper cascade).  Same arithmetic for every texel it stores.  At 4096^2 N=6 this is
-  // 47 % of the top level's workgroups; at rayRange 64 every workgroup of the two top levels.
+  // 47 % of the top level's workgroups; at rayRange 64 every workgroup of the two top levels (any tile shape: the
+  // several-probes-per-lane tiles of C2 / C3 skip their bound table and workgroup proof the same way).
   bool wg_off = false;
-  if constexpr (TLC && !CH) {
+  if constexpr (!Z0 && !CH) {
     if (P.t0 >= 0.25f && !(P.t0 > P.t1)) {
       const int cxl = min(cx0 + TX, P.bdx) - 1, cyl = min(cy0 + THY, P.p1) - 1;
       const bool pw = P2S || P.c.powW, ph = P2S || P.c.powH;
@@ -600,7 +602,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       const float oyh = div_res(((float)cyl + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, ph);
       bool off = cxl >= cx0 && cyl >= cy0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < ND; ++r) {
         const float2 d = ld_uniform(dirs + bi0 * 4 + r);
         const float sx = (P.t0 * d.x) * P.aspy, sy = (P.t0 * d.y) * P.aspx;
         // (-0 or NaN never count as off: the test only claims what every lane's own test concludes)
@@ -1056,6 +1058,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   RC_SECTION("tail");
   RC_TSTAMP(5);
   int qpos[TLC ? NR : 1];  // queue entry of each pending ray of this lane
+  unsigned tail_n = 1;     // (P.tlb) rays the tail queue held: workgroup-uniform after its barrier
   if (tl) {
     // pending rays (still marching after itend iterations) -> LDS queue, wave-contiguous ranges
     unsigned n = 0;
@@ -1079,10 +1082,12 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       qpos[k] = (int)pos;
       if (t[k] < kDone) s_q[pos++] = make_uint2(__float_as_uint(t[k]), (threadIdx.x << 3) | (unsigned)k);
     }
+    if (P.tlb) stage_write();  // (P.tlb: this barrier also publishes the staged footprint)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     const unsigned nq = s_qn;
+    tail_n = nq;
     for (unsigned j = (unsigned)wv * 64u + (unsigned)lane; j < nq; j += NT) {
       const uint2 e = s_q[j];
       const unsigned otid = e.y >> 3, k = e.y & 7u;
@@ -1147,8 +1152,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   RC_TSTAMP(6);
   RC_SECTION("stage_write");
-  stage_write();
-  if (stg || tl) __syncthreads();
+  // P.tlb with the tail queue: the footprint was written before the queue's barrier, so a second barrier is
+  // needed only when the queue held rays (their hit texels come back through LDS)
+  const bool fused_bar = tl && P.tlb;
+  if (!fused_bar) stage_write();
+  if (fused_bar ? tail_n != 0u : (stg || tl)) __syncthreads();
   if (tl) {  // hit texels of this lane's rays that finished in the tail
 #pragma unroll
     for (int k = 0; k < NR; ++k)
@@ -1338,6 +1346,7 @@ static inline int rc_tile_params(const RcLevelArgs &a, RcParams &P) {
   if (P.cmin && P.cscr && !P.dexit) return -1;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
+  P.tlb = a.tail_bar;
   // palettes: the plain field's march (DL 0) on power-of-two screens whose byte offsets fit 27 bits
   P.cpal = (a.cell_pal && DL == 0 && p2s && (size_t)P.s.pitch * P.s.H <= ((size_t)1 << 26)) ? a.cell_pal : nullptr;
   P.lgw = 0;

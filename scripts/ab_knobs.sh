@@ -8,6 +8,6 @@ for i in $(seq ${ROUNDS:-3}); do
   for cfg in ${CFGS:-base rc_skip=3}; do
     args=""; [ "$cfg" = base ] || for kv in ${cfg//,/ }; do args="$args --tune $kv"; done
     timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 $BENCH_ARGS $args > gpurun_out/ab.log 2>&1 || exit $?
-    python3 -c "import json; d=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]); print('$cfg', d['value'], d['rc_ms_per_frame'], d['rc_level_ms'], d['full_pipeline_ms'])"
+    python3 -c "import json; d=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]); print('$cfg', d['value'], d['rc_ms_per_frame'], d['rc_level_ms'], d['full_pipeline_ms'], 'jfa', d.get('pass_ms', {}).get('jfa'))"
   done
 done

@@ -541,6 +541,8 @@ def test_exit_proofs_and_tail_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene):
         for skip, tail in ((0, 0), (1, 0), (2, 1), (3, 3), (1, 2), (0, 5), (1, 31)):
             ctx.set_tuning("rc_skip", skip)
             ctx.set_tuning("rc_tail", tail)
+            # rc_tailbar: the staged footprint published by the tail queue's barrier (one barrier when it is empty)
+            ctx.set_tuning("rc_tailbar", (tail + v) & 1)
             assert ctx.get_tuning("rc_skip") == skip and ctx.get_tuning(f"rc_tail_L{N - 1}") == tail
             ctx.do_rc2dgi()
             ctx.sync()
@@ -570,6 +572,32 @@ def test_jfa_lds_staging_is_bit_identical(RC2DGI, W, H, N, storage):
         out[lds] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
     for k in out[0]:
         assert np.array_equal(out[0][k], out[1][k]), f"{k}: {np.count_nonzero(out[0][k] != out[1][k])}"
+    ctx.close()
+
+
+@pytest.mark.parametrize("W,H,N,storage", [(256, 256, 4, "f32"), (1024, 1024, 5, "f32"), (512, 512, 4, "rgba8"),
+                                           (512, 256, 4, "f32"), (4096, 4096, 6, "f32"), (8192, 8192, 8, "f32")])
+@pytest.mark.parametrize("scene", ["demo", "rand:61"])
+def test_jfa_rows_short_steps_are_bit_identical(RC2DGI, W, H, N, storage, scene):
+    """The short isotropic JumpFlood steps with consecutive rows per lane (tuning jfa_rows 4 / 8: k_jfa_rows, each
+    tap row loaded once) pick the same seeds: jumpRT1 / jumpRT2, the distance field (fused into the last step) and
+    the frame are unchanged, with poisoned intermediates; non-square (float keys) and RGBA8 screens keep k_jfa_p2."""
+    color, emis = make_scene(scene, W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for jr in (0, 4, 8):
+        ctx.set_tuning("jfa_rows", jr)
+        assert ctx.get_tuning("jfa_rows") == jr
+        ctx.set_tuning("poison", 1)
+        ctx.do_rc2dgi()
+        ctx.sync()
+        out[jr] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
+    for jr in (4, 8):
+        for k in out[0]:
+            assert np.array_equal(out[0][k].view(np.uint8), out[jr][k].view(np.uint8)), \
+                f"jfa_rows {jr} {k}: {np.count_nonzero(out[0][k] != out[jr][k])}"
     ctx.close()
 
 
