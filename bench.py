@@ -90,6 +90,16 @@ def cpu_baseline(W, H, N, rr, budget_s=12.0):
 GATHER_L2_GLINES, GATHER_MALL_GLINES = 260.0, 73.0
 
 
+def tuning_or_none(ctx, key):
+    """A tuning key the library may not know (A/B runs against older builds): its value, or None."""
+    from radiancecascade2dglobalillumination_amd import RC2DGIError
+
+    try:
+        return ctx.get_tuning(key)
+    except RC2DGIError:
+        return None
+
+
 def pmc_key(W, H, N, ray_range, storage, scene, orders, variants, knobs=None):
     """What a committed PMC record was measured on: counters describe one configuration, scene and schedule
     (the march's line requests and instructions follow the scene's occluders and the workgroup orders), so a
@@ -382,7 +392,8 @@ def bench_strips(a, rank, local, world):
             "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
             "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}, row strips",
                        "shards": nsh, "parallelism": f"strips{nsh}" + ("-in-process" if virtual else "-rccl"),
-                       "rc_variant": [ctxs[0].get_tuning(f"rc_variant_L{L}") for L in range(N)]},
+                       "rc_variant": [ctxs[0].get_tuning(f"rc_variant_L{L}") for L in range(N)],
+                       "strip_tables": tuning_or_none(ctxs[0], "strip_tables_active")},
             "device_bytes_per_shard": int(shard_bytes),
             "frames_per_s": round(a.steps / wall, 2)}), flush=True)
     for g in ctxs:
@@ -660,7 +671,7 @@ def main():
         knobs = {**tun.get("knobs", {}), **knobs}
     key = pmc_key(W, H, N, a.ray_range, a.storage, a.scene, orders, variants, knobs)
     rec = find_pmc_record(os.path.join(ROOT, "profiles", "rc_level_pmc.json"), key)
-    chain = ctx.get_tuning("rc_chain") != 0
+    chain = bool(tuning_or_none(ctx, "rc_chain"))
     if rec is not None and not chain:
         traffic = rec.get("hbm_bytes_per_launch")
         gather = gather_roofline(rec, N, lvl_ms / a.steps)

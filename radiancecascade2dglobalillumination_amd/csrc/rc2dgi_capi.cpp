@@ -166,6 +166,10 @@ struct rc2dgi_ctx {
   hipEvent_t ev_phase1 = nullptr;   // end of phase 1 (group exchange)
   hipEvent_t ev_frame = nullptr;    // end of the last group frame (peers copy from our distRT)
   hipEvent_t ev_jfa[2] = {nullptr, nullptr};  // end of the last even / odd JFA step (group exchange)
+  hipEvent_t ev_side = nullptr;     // end of the side pass (group exchange of the strip tables)
+  int strip_tables = 1;             // tuning "strip_tables": row-strip shards build the side tables of their own
+                                    // cell rows and exchange them (strip_tables_apply); 0: every shard builds them all
+  bool st_last = false;             // the last frame ran with strip tables
   bool gi1final = false;            // phase 1 -> phase 2 state
   bool broken = false;              // a reallocation failed: the device buffers are gone (destroy it)
   std::string err;
@@ -370,6 +374,31 @@ int jfa_buffers(rc2dgi_ctx *c) {
   return RC2DGI_OK;
 }
 
+// exit proofs on for this frame: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
+// staging and barrier cost more than the skipped samples save (RC 0.338 vs 0.376 ms, measured)
+bool proofs_on(const rc2dgi_ctx *c) { return c->rc_skip > 1 || (c->rc_skip == 1 && std::max(c->W, c->H) >= 2048); }
+
+// Strip tables (row-strip shards): the side pass of a shard covers only the bound-table cells
+// of its own rows -- their records' palettes, bound table and hit flags, and its rows of the march field -- and the
+// shards exchange those rows (the march field in place of distRT: same 2 bytes a texel; 64 B of bound table, 64 B of
+// hit flags and 16 KB of palettes a cell row).  Every level then marches on the march field and takes a hit's record
+// from its cell's palette, or (palette full) derives it from colorRT / emissiveRT, which every shard holds whole:
+// no record texture.  Applies where the side pass is the fused palette pass (square power-of-two screens >= 4096),
+// every strip boundary falls on a cell row, and every level marches on the plain field.
+bool strip_tables_apply(const rc2dgi_ctx *c) {
+  if (c->world < 2 || !c->strip_tables || !c->rc_pal || !c->shade_fused || !proofs_on(c)) return false;
+  if (!shade_cmin_fused_ok(c->W, c->H, c->sd.pitch) || (size_t)c->sd.pitch * c->H > ((size_t)1 << 26)) return false;
+  for (int v : c->rc_variant)
+    if (rc_variant_tiled(v) || rc_variant_packed(v) || rc_variant_nib(v)) return false;
+  const int cell = 1 << dist_cmin_shift(c->W, c->H);
+  for (int q = 0; q < c->world; ++q) {
+    int y0, y1;
+    strip_rows(c->H, q, c->world, y0, y1);
+    if (y0 % cell || y1 % cell || y1 <= y0) return false;
+  }
+  return true;
+}
+
 // The distRT copies the schedule's variants read ("t" / "p" / "n") and the surface-palette tables (rc_pal),
 // allocated when the schedule or the knobs are set (rc2dgi_set_tuning, rc2dgi_autotune with all = true,
 // allocate), never inside a frame: hipMalloc may synchronise the device, and an out-of-memory then surfaces
@@ -431,6 +460,15 @@ int prepare_side_buffers(rc2dgi_ctx *c, bool all = false) {
       c->shade_list = nullptr;
       return hip_fail(c, e, "records pass cell list");
     }
+  }
+  // the record texture (16 B a texel): not held by shards that run with strip tables (their hits derive records)
+  const bool st = strip_tables_apply(c);
+  if (st && c->shade) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(c->shade));
+    c->shade = nullptr;
+  } else if (!st && !c->shade) {
+    HIPCHK(c, alloc(&c->shade, (size_t)c->sd.pitch * c->H * sizeof(float4)));
   }
   return RC2DGI_OK;
 }
@@ -677,6 +715,7 @@ int rc2dgi_create(const rc2dgi_config *cfg, rc2dgi_ctx **out) {
   for (auto &ev : c->ev) (void)hipEventCreateWithFlags(&ev, timing_event_flags());
   (void)hipEventCreateWithFlags(&c->ev_phase1, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&c->ev_frame, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming);
   for (auto &ev : c->ev_jfa) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   rc = allocate(c);
   if (rc != RC2DGI_OK) {
@@ -696,6 +735,7 @@ int rc2dgi_destroy(rc2dgi_ctx *c) {
   if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
   if (c->ev_phase1) (void)hipEventDestroy(c->ev_phase1);
   if (c->ev_frame) (void)hipEventDestroy(c->ev_frame);
+  if (c->ev_side) (void)hipEventDestroy(c->ev_side);
   for (auto &ev : c->ev_jfa)
     if (ev) (void)hipEventDestroy(ev);
   free_buffers(c);
@@ -1007,11 +1047,19 @@ int do_phase1(rc2dgi_ctx *c, const FramePlan &plan) {
   return rc == RC2DGI_OK ? phase1_end(c) : rc;
 }
 
-// phase 2: cascades, blur, merge (RC2DGI.cs:342-404)
-int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
+// phase 2: cascades, blur, merge (RC2DGI.cs:342-404), in two parts: the side pass (the march's records, bound
+// table, palettes, march field and directional clear table) and the levels with blur and merge.  Row-strip shards
+// with strip tables (strip_tables_apply) exchange the side tables of their cell rows in between (rc2dgi_do over
+// RCCL, rc2dgi_do_group by device copies).
+struct SidePass {
+  bool proofs = false, mps = false, fused = false, pal = false;
+  bool st = false;            // strip tables: own cell rows only; the exchange follows
+  bool dclr_pending = false;  // k_dir_clear still to run (strip tables: it needs every shard's hit flags)
+};
+
+int phase2_side(rc2dgi_ctx *c, SidePass &f) {
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
-  const bool T = c->timing;
   // 4. radiance cascades N-1 .. 0 (RC2DGI.cs:342-362).  The "t" / "p" / "o" variants read re-laid-out
   // copies of distRT; building them is timed with the top level (it is RC work, not DistanceField's)
   // per-level events only in timing mode 1: each one idles the GPU ~5 us before the next level
@@ -1032,9 +1080,7 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   if (tiled) HIPCHK(c, launch_dist_tile(c->dist, c->sd.pitch, c->dist_t, c->W, c->H, st));
   if (packed && p2s) HIPCHK(c, launch_dist_pack(c->dist, c->sd.pitch, c->dist_p, c->W, c->H, st));
   if (nib && p2s) HIPCHK(c, launch_dist_nib(c->dist, c->sd.pitch, c->dist_n, c->W, c->H, st));
-  // exit proofs: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
-  // staging and barrier cost more than the skipped samples save (RC 0.338 vs 0.376 ms, measured)
-  const bool proofs = c->rc_skip > 1 || (c->rc_skip == 1 && std::max(c->W, c->H) >= 2048);
+  const bool proofs = proofs_on(c);
   // the directional table only where some level reads it: a one-probe tile at a level with 4^L >= kDirBins,
   // directional proofs on there and the level's direction table binnable (dp_ok)
   bool mps = false;
@@ -1047,6 +1093,14 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   const bool fused = proofs && c->shade_fused && shade_cmin_fused_ok(c->W, c->H, c->sd.pitch);
   const bool pal = fused && c->rc_pal && (size_t)c->sd.pitch * c->H <= ((size_t)1 << 26);
   if (pal && (!c->mfield || !c->cell_pal)) return fail(c, RC2DGI_E_STATE, "surface palette tables not prepared");
+  const bool stt = pal && strip_tables_apply(c);
+  if (!stt && !c->shade) return fail(c, RC2DGI_E_STATE, "record texture not prepared");
+  f.proofs = proofs;
+  f.mps = mps;
+  f.fused = fused;
+  f.pal = pal;
+  f.st = stt;
+  c->st_last = stt;
   c->built_hitc = mps;
   c->built_cmin = proofs;
   c->built_dclr = mps;
@@ -1057,14 +1111,24 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     // parity's counter for the next one)
     const bool split = pal && c->shade_split && shade_split_ok(c->W, c->H);
     // split pass with directional proofs: k_dir_clear needs only the scan's hit flags, so it runs on the side
-    // stream beside k_shade_cells (the few hundred workgroups of the hit cells leave most CUs idle)
-    side = split && mps && c->side_overlap == 1 && c->side_stream && c->ev_fork && c->ev_join;
+    // stream beside k_shade_cells (the few hundred workgroups of the hit cells leave most CUs idle); with strip
+    // tables it waits for every shard's flags (phase2_levels)
+    side = split && mps && !stt && c->side_overlap == 1 && c->side_stream && c->ev_fork && c->ev_join;
     // side_overlap 2: k_dir_clear's workgroups appended to k_shade_cells' grid instead (one launch, one stream)
-    dc_merged = split && mps && c->side_overlap == 2;
-    HIPCHK(c, launch_shade_cmin(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, c->cmin,
-                                mps ? c->hitc : nullptr, st, pal ? c->mfield : nullptr, pal ? c->cell_pal : nullptr,
+    dc_merged = split && mps && !stt && c->side_overlap == 2;
+    int cr0 = 0, ncr = kCminDim;  // (strip tables: the cell rows of the own strip)
+    if (stt) {
+      int y0, y1;
+      strip_rows(c->H, c->rank, c->world, y0, y1);
+      const int csh = dist_cmin_shift(c->W, c->H);
+      cr0 = y0 >> csh;
+      ncr = (y1 - y0) >> csh;
+    }
+    HIPCHK(c, launch_shade_cmin(c->dist, c->color_in, c->emissive, stt ? nullptr : c->shade, c->sd, c->reflectivity,
+                                c->cmin, mps ? c->hitc : nullptr, st, pal ? c->mfield : nullptr, pal ? c->cell_pal : nullptr,
                                 split ? c->shade_list : nullptr, split ? (int)(c->split_frames++ & 1u) : 0,
-                                side ? c->ev_fork : nullptr, dc_merged ? c->dboxes : nullptr, dc_merged ? c->dclr : nullptr));
+                                side ? c->ev_fork : nullptr, dc_merged ? c->dboxes : nullptr, dc_merged ? c->dclr : nullptr,
+                                cr0, ncr));
   } else {
     HIPCHK(c, launch_shade(c->dist, c->color_in, c->emissive, c->shade, c->sd, c->reflectivity, st));
     if (proofs) HIPCHK(c, launch_dist_cmin(c->dist, c->sd.pitch, c->cmin, c->W, c->H, st, mps ? c->hitc : nullptr));
@@ -1074,9 +1138,45 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, c->side_stream));
     HIPCHK(c, hipEventRecord(c->ev_join, c->side_stream));
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_join, 0));
+  } else if (mps && stt) {
+    f.dclr_pending = true;
   } else if (mps && !dc_merged) {
     HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
   }
+  return RC2DGI_OK;
+}
+
+// the pieces of shard q's strip tables (strip_tables_apply): its rows of the march field, its cell rows of the bound
+// table, hit flags and palettes -- each one contiguous run of its buffer
+struct StripPiece {
+  size_t off, bytes;
+};
+void strip_table_pieces(const rc2dgi_ctx *c, int q, StripPiece out[4]) {
+  int y0, y1;
+  strip_rows(c->H, q, c->world, y0, y1);
+  const int csh = dist_cmin_shift(c->W, c->H);
+  const size_t cr0 = (size_t)(y0 >> csh), ncr = (size_t)((y1 - y0) >> csh);
+  out[0] = {(size_t)y0 * c->sd.pitch * sizeof(unsigned short), (size_t)(y1 - y0) * c->sd.pitch * sizeof(unsigned short)};
+  out[1] = {cr0 * kCminDim * sizeof(CminT), ncr * kCminDim * sizeof(CminT)};
+  out[2] = {cr0 * kCminDim, ncr * kCminDim};
+  out[3] = {cr0 * kCminDim * kCellPalStride * sizeof(float4), ncr * kCminDim * kCellPalStride * sizeof(float4)};
+}
+char *strip_table_base(rc2dgi_ctx *c, int piece) {
+  switch (piece) {
+    case 0: return reinterpret_cast<char *>(c->mfield);
+    case 1: return reinterpret_cast<char *>(c->cmin);
+    case 2: return reinterpret_cast<char *>(c->hitc);
+    default: return reinterpret_cast<char *>(c->cell_pal);
+  }
+}
+
+int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  const bool T = c->timing;
+  const bool LT = c->timing == 1;
+  const bool proofs = f.proofs, mps = f.mps, pal = f.pal;
+  if (f.dclr_pending) HIPCHK(c, launch_dir_clear(c->hitc, c->dboxes, c->dclr, st));
   bool gi1final = false;
   // The cascade chain (tuning rc_chain, rc2dgi_rc_chain.hip): the top level as usual, then levels N-2 .. 0 in one
   // launch of 16x16x1 tiles, each level into a texture of its own -- level 0 into giRT1 / giRT2 as the loop below
@@ -1101,9 +1201,15 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
     const int var = (chain && (L < c->N - 1 || c->rc_chain == 4)) ? 0 : c->rc_variant[L];
     const bool plain = !rc_variant_tiled(var) && !rc_variant_packed(var) && !rc_variant_nib(var) &&
                        rc_variant_one_probe(var) && L > 0;
-    a.dist = (pal && plain) ? c->mfield : c->dist;  // the march field: same samples, hits carry a palette entry
+    // the march field: same samples, hits carry a palette entry (strip tables: every level marches on it -- the
+    // shard holds distRT for its own rows only -- and hit records come from the palettes or the inputs)
+    a.dist = (pal && (plain || f.st)) ? c->mfield : c->dist;
     a.cell_pal = (pal && plain) ? c->cell_pal : nullptr;
     a.shade = c->shade;
+    if (f.st) {
+      a.rec_color = c->color_in;
+      a.rec_emis = c->emissive;
+    }
     a.dirs = c->dirs + dir_table_offset(L);
     a.dexit = c->dexit + dir_table_offset(L);
     a.sky = c->sky;
@@ -1203,6 +1309,15 @@ int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
   return RC2DGI_OK;
 }
 
+// phase 2 of a context without an exchange in its middle (unsharded, or a shard without strip tables)
+int do_phase2(rc2dgi_ctx *c, const FramePlan &plan) {
+  SidePass f;
+  int rc = phase2_side(c, f);
+  if (rc != RC2DGI_OK) return rc;
+  if (f.st) return fail(c, RC2DGI_E_STATE, "strip tables exchange between the side pass and the levels");
+  return phase2_levels(c, plan, f);
+}
+
 // distRT strip of shard q: device pointer and byte count (rows are contiguous, pitch-linear)
 void dist_strip(const rc2dgi_ctx *c, int q, unsigned short **p, size_t *bytes) {
   int y0, y1;
@@ -1222,20 +1337,47 @@ int rc2dgi_do(rc2dgi_ctx *c) {
   const FramePlan plan = make_plan(c);
   int rc = do_phase1(c, plan);
   if (rc != RC2DGI_OK) return rc;
-  if (c->comm) {  // every strip of distRT to every rank: one in-place broadcast per root
+  const bool stt = c->comm && strip_tables_apply(c);
+  if (c->comm) {
+    // every strip of distRT to every rank: one in-place broadcast per root; with strip tables only row 0 (the REPEAT
+    // wrap of the last cell row's bound), the side tables' rows follow the side pass instead
     const Rccl &R = rccl();
     ncclResult_t e = R.group_start();
-    for (int q = 0; q < c->world && e == ncclSuccess; ++q) {
-      unsigned short *p;
-      size_t n;
-      dist_strip(c, q, &p, &n);
-      e = R.broadcast(p, p, n, ncclUint8, q, c->comm, c->stream);
+    if (stt) {
+      e = R.broadcast(c->dist, c->dist, (size_t)c->sd.pitch * sizeof(unsigned short), ncclUint8, 0, c->comm, c->stream);
+    } else {
+      for (int q = 0; q < c->world && e == ncclSuccess; ++q) {
+        unsigned short *p;
+        size_t n;
+        dist_strip(c, q, &p, &n);
+        e = R.broadcast(p, p, n, ncclUint8, q, c->comm, c->stream);
+      }
     }
     const ncclResult_t e2 = R.group_end();
     if (e == ncclSuccess) e = e2;
     if (e != ncclSuccess) return fail(c, RC2DGI_E_HIP, std::string("ncclBroadcast: ") + R.error_string(e));
   }
-  return do_phase2(c, plan);
+  if (!stt) return do_phase2(c, plan);
+  SidePass f;
+  rc = phase2_side(c, f);
+  if (rc != RC2DGI_OK) return rc;
+  if (!f.st) return fail(c, RC2DGI_E_STATE, "strip tables: side pass disagrees");
+  {  // the side tables' rows of every rank to every rank: four in-place broadcasts per root, one group
+    const Rccl &R = rccl();
+    ncclResult_t e = R.group_start();
+    for (int q = 0; q < c->world && e == ncclSuccess; ++q) {
+      StripPiece pc[4];
+      strip_table_pieces(c, q, pc);
+      for (int i = 0; i < 4 && e == ncclSuccess; ++i) {
+        char *p = strip_table_base(c, i) + pc[i].off;
+        e = R.broadcast(p, p, pc[i].bytes, ncclUint8, q, c->comm, c->stream);
+      }
+    }
+    const ncclResult_t e2 = R.group_end();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess) return fail(c, RC2DGI_E_HIP, std::string("ncclBroadcast (strip tables): ") + R.error_string(e));
+  }
+  return phase2_levels(c, plan, f);
 }
 
 int rc2dgi_do_phase(rc2dgi_ctx *c, int phase) {
@@ -1473,9 +1615,23 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
     if (rc != RC2DGI_OK) return rc;
     HIPCHK(cs[k], hipEventRecord(cs[k]->ev_phase1, cs[k]->stream));
   }
+  // strip tables (strip_tables_apply, the same on every shard of one configuration): no distRT exchange -- the last
+  // shard only needs row 0 for the REPEAT wrap of its last cell row's bound (k_shade_scan / shade_cell)
+  const bool stt = strip_tables_apply(cs[0]);
+  for (int k = 0; k < n; ++k)
+    if (strip_tables_apply(cs[k]) != stt)
+      return fail(cs[k], RC2DGI_E_ARG, "rc2dgi_do_group: every shard must run with the same strip_tables setting");
   for (int k = 0; k < n; ++k) {
     rc2dgi_ctx *c = cs[k];
     HIPCHK(c, hipSetDevice(c->device));
+    if (stt) {
+      if (k == n - 1) {
+        HIPCHK(c, hipStreamWaitEvent(c->stream, cs[0]->ev_phase1, 0));
+        HIPCHK(c, hipMemcpyAsync(c->dist, cs[0]->dist, (size_t)c->sd.pitch * sizeof(unsigned short),
+                                 hipMemcpyDeviceToDevice, c->stream));
+      }
+      continue;
+    }
     for (int q = 0; q < n; ++q) {
       if (q == k) continue;
       HIPCHK(c, hipStreamWaitEvent(c->stream, cs[q]->ev_phase1, 0));
@@ -1486,9 +1642,32 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
       HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
     }
   }
-  // phase 2 of a context overwrites nothing a peer still copies from (only distRT is read)
+  // phase 2 of a context overwrites nothing a peer still copies from (only distRT -- or, with strip tables, the
+  // side tables' own rows -- is read, and a context's next frame waits for every peer's frame)
+  std::vector<SidePass> sides(n);
   for (int k = 0; k < n; ++k) {
-    int rc = do_phase2(cs[k], plans[k]);
+    int rc = phase2_side(cs[k], sides[k]);
+    if (rc != RC2DGI_OK) return rc;
+    if (sides[k].st != stt) return fail(cs[k], RC2DGI_E_STATE, "strip tables: shards disagree");
+    HIPCHK(cs[k], hipEventRecord(cs[k]->ev_side, cs[k]->stream));
+  }
+  if (stt) {  // every shard's table rows to every other shard
+    for (int k = 0; k < n; ++k) {
+      rc2dgi_ctx *c = cs[k];
+      HIPCHK(c, hipSetDevice(c->device));
+      for (int q = 0; q < n; ++q) {
+        if (q == k) continue;
+        HIPCHK(c, hipStreamWaitEvent(c->stream, cs[q]->ev_side, 0));
+        StripPiece pc[4];
+        strip_table_pieces(c, q, pc);
+        for (int i = 0; i < 4; ++i)
+          HIPCHK(c, hipMemcpyAsync(strip_table_base(c, i) + pc[i].off, strip_table_base(cs[q], i) + pc[i].off, pc[i].bytes,
+                                   hipMemcpyDeviceToDevice, c->stream));
+      }
+    }
+  }
+  for (int k = 0; k < n; ++k) {
+    int rc = phase2_levels(cs[k], plans[k], sides[k]);
     if (rc != RC2DGI_OK) return rc;
     HIPCHK(cs[k], hipEventRecord(cs[k]->ev_frame, cs[k]->stream));
   }
@@ -1509,8 +1688,10 @@ int rc2dgi_set_shard(rc2dgi_ctx *c, int rank, int world) {
   c->frame_done = c->have_frame = false;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const int rc = jfa_buffers(c);  // strip windows (world > 1) or full-size jumpRT1 / jumpRT2
+  int rc = jfa_buffers(c);  // strip windows (world > 1) or full-size jumpRT1 / jumpRT2
   if (rc != RC2DGI_OK) c->broken = true;
+  if (rc == RC2DGI_OK) rc = prepare_side_buffers(c);  // (strip tables: no record texture)
+  c->st_last = false;
   return rc;
 }
 
@@ -1763,9 +1944,24 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *c, const float *rgb, int n) {
   return RC2DGI_OK;
 }
 
+namespace {
+int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value);
+}
+
 int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
+  const int rc = set_tuning_knob(c, key, value);
+  if (rc != RC2DGI_OK || !c || c->broken) return rc;
+  return prepare_side_buffers(c);  // (whether the record texture is held follows the knobs: strip_tables_apply)
+}
+
+namespace {
+int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value) {
   if (!c || !key) return fail(c, RC2DGI_E_ARG, "null argument");
   std::string k(key);
+  if (k == "strip_tables") {
+    c->strip_tables = value != 0;
+    return RC2DGI_OK;
+  }
   if (k == "rc_variant" || k.rfind("rc_variant_L", 0) == 0) {
     if (value < 0 || value >= rc_variant_count()) return fail(c, RC2DGI_E_ARG, "rc_variant out of range");
     if (k == "rc_variant") {
@@ -1899,6 +2095,7 @@ int rc2dgi_set_tuning(rc2dgi_ctx *c, const char *key, int value) {
   }
   return fail(c, RC2DGI_E_ARG, "unknown tuning key " + k);
 }
+}  // namespace
 
 int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   if (!c || !key || !value) return fail(c, RC2DGI_E_ARG, "null argument");
@@ -1931,6 +2128,14 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "jfa_lds") {
     *value = c->jfa_lds;
+    return RC2DGI_OK;
+  }
+  if (k == "strip_tables") {
+    *value = c->strip_tables;
+    return RC2DGI_OK;
+  }
+  if (k == "strip_tables_active") {  // the last frame ran with strip tables (strip_tables_apply)
+    *value = c->st_last ? 1 : 0;
     return RC2DGI_OK;
   }
   if (k == "rc_tailbar") {

@@ -127,6 +127,8 @@ struct RcLevelArgs {
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
   int tail_bar = 0;             // the staged footprint written before the tail queue's barrier: one barrier when
                                 // the queue is empty (tuning rc_tailbar)
+  const float4 *rec_color = nullptr, *rec_emis = nullptr;  // hit records derived from colorRT / emissiveRT instead
+                                                          // of read from `shade` (row-strip shards, strip tables)
 };
 
 // The cascade chain (rc2dgi_rc_chain.hip, tuning rc_chain): the levels a[0 .. n) (consecutive, downwards; a[0]
@@ -169,7 +171,9 @@ hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, co
                              ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st,
                              unsigned short *mf = nullptr, float4 *cpal = nullptr, unsigned *list = nullptr,
                              int parity = 0, hipEvent_t after_scan = nullptr,  // (split: recorded after the scan)
-                             const int4 *boxes = nullptr, unsigned char *dclr = nullptr);  // (split: k_dir_clear merged)
+                             const int4 *boxes = nullptr, unsigned char *dclr = nullptr,  // (split: k_dir_clear merged)
+                             int cr0 = 0, int ncr = kCminDim);  // cell rows [cr0, cr0 + ncr) only (with mf / cpal; shade
+                                                                // may then be nullptr: no record texture)
 hipError_t launch_dist_cmin(const unsigned short *dist, int pitch, CminT *cmin, int W, int H, hipStream_t st,
                             unsigned char *hitc = nullptr);
 // Directional clear distances of the march proofs (k_rc_level, one-probe tiles): kDirBins angular bins x

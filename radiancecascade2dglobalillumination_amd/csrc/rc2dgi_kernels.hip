@@ -674,7 +674,7 @@ __device__ __forceinline__ void shade_cell(const unsigned short *__restrict__ di
           rec[k] = make_float4(e[k].x, e[k].y, e[k].z, 1.0f);
           if (!(sqrtf(e[k].x * e[k].x + e[k].y * e[k].y + e[k].z * e[k].z) > 0.0f))
             rec[k] = make_float4(cl[k].x, cl[k].y, cl[k].z, reflectivity);
-          if (hit) shade[base + (GR * h + k) * rstep] = rec[k];
+          if (hit && shade) shade[base + (GR * h + k) * rstep] = rec[k];  // (no record texture: strip tables)
         }
         if (PAL) {
           // the wave's distinct records of these 8 rows, one at a time (usually one or two: a surface's texels
@@ -775,14 +775,15 @@ __device__ __forceinline__ void shade_cell(const unsigned short *__restrict__ di
   }
 }
 
+// (cell rows from cr0: a row-strip shard's own cells, strip tables)
 template <bool PAL, int NTH = 256>
 __global__ __launch_bounds__(NTH) void k_shade_cmin(const unsigned short *__restrict__ dist,
                                                     const float4 *__restrict__ color, const float4 *__restrict__ emis,
                                                     float4 *__restrict__ shade, ScreenDims s, float reflectivity,
                                                     int csh, CminT *__restrict__ cmin, unsigned char *__restrict__ hitc,
-                                                    unsigned short *__restrict__ mf, float4 *__restrict__ cpal) {
+                                                    unsigned short *__restrict__ mf, float4 *__restrict__ cpal, int cr0) {
   shade_cell<PAL, NTH, true>(dist, color, emis, shade, s, reflectivity, csh, cmin, hitc, mf, cpal, (int)blockIdx.x,
-                             (int)blockIdx.y);
+                             (int)blockIdx.y + cr0);
 }
 
 // The same pass split in two (tuning shade_split; round 5).  Most cells hold no hittable texel (demo frame:
@@ -795,10 +796,11 @@ template <int NR>  // runs per lane: 2 (64-texel cells)
 __global__ __launch_bounds__(256) void k_shade_scan(const unsigned short *__restrict__ dist, ScreenDims s, int csh,
                                                     CminT *__restrict__ cmin, unsigned char *__restrict__ hitc,
                                                     unsigned short *__restrict__ mf, unsigned *__restrict__ list,
-                                                    int p) {
+                                                    int p, int cr0) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cw = 1 << csh, sh = csh - 3;  // 2^sh runs of 8 texels per cell row
-  const int x0 = (int)blockIdx.x << csh, y0 = (int)blockIdx.y << csh;
+  const int cby = (int)blockIdx.y + cr0;  // (cell rows from cr0: a row-strip shard's own cells, strip tables)
+  const int x0 = (int)blockIdx.x << csh, y0 = cby << csh;
   constexpr int nr = NR;
   uint4 v[NR];
   size_t base[NR];
@@ -829,7 +831,7 @@ __global__ __launch_bounds__(256) void k_shade_scan(const unsigned short *__rest
 #pragma unroll
     for (int g = 0; g < NR; ++g) *reinterpret_cast<uint4 *>(mf + base[g]) = v[g];
   } else if (threadIdx.x == 0) {
-    list[2 + atomicAdd(&list[p], 1u)] = blockIdx.y * kCminDim + blockIdx.x;
+    list[2 + atomicAdd(&list[p], 1u)] = cby * kCminDim + blockIdx.x;
   }
   // REPEAT wrap (k_dist_cmin): samples at u = 1 / v = 1 read column 0 / row 0
   if (x0 + cw == s.W)
@@ -845,8 +847,8 @@ __global__ __launch_bounds__(256) void k_shade_scan(const unsigned short *__rest
   if (threadIdx.x == 0) {
     m = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
     const float d = decode_dist(m);
-    if (hitc) hitc[blockIdx.y * kCminDim + blockIdx.x] = d < 0.001f ? 1 : 0;
-    cmin[blockIdx.y * kCminDim + blockIdx.x] = d >= 0.001f ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
+    if (hitc) hitc[cby * kCminDim + blockIdx.x] = d < 0.001f ? 1 : 0;
+    cmin[cby * kCminDim + blockIdx.x] = d >= 0.001f ? (CminT)fminf(floorf(d * kCminScale), 255.0f) : (CminT)0;
   }
 }
 
@@ -1956,15 +1958,17 @@ bool shade_cmin_fused_ok(int W, int H, int pitch) {
 hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, const float4 *emis, float4 *shade,
                              ScreenDims s, float reflectivity, CminT *cmin, unsigned char *hitc, hipStream_t st,
                              unsigned short *mf, float4 *cpal, unsigned *list, int parity, hipEvent_t after_scan,
-                             const int4 *boxes, unsigned char *dclr) {
+                             const int4 *boxes, unsigned char *dclr, int cr0, int ncr) {
   if (!shade_cmin_fused_ok(s.W, s.H, s.pitch)) return hipErrorInvalidValue;
+  if (cr0 < 0 || ncr < 1 || cr0 + ncr > kCminDim) return hipErrorInvalidValue;
+  if ((cr0 != 0 || ncr != kCminDim || !shade) && !(mf && cpal)) return hipErrorInvalidValue;  // (partial: palettes)
   const int csh = dist_cmin_shift(s.W, s.H);
   if (mf && cpal && list) {
     // every argument check before the first launch: an error leaves nothing enqueued
     if (!shade_split_ok(s.W, s.H)) return hipErrorInvalidValue;
     if (dclr && (!hitc || !boxes)) return hipErrorInvalidValue;
     const int p = parity & 1;
-    hipLaunchKernelGGL(k_shade_scan<2>, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, s, csh, cmin, hitc, mf, list, p);
+    hipLaunchKernelGGL(k_shade_scan<2>, dim3(kCminDim, ncr), dim3(256), 0, st, dist, s, csh, cmin, hitc, mf, list, p, cr0);
     if (after_scan) {  // (the bound table and hit flags are final here)
       const hipError_t e = hipEventRecord(after_scan, st);
       if (e != hipSuccess) return e;
@@ -1984,11 +1988,11 @@ hipError_t launch_shade_cmin(const unsigned short *dist, const float4 *color, co
     return hipGetLastError();
   }
   if (mf && cpal)
-    hipLaunchKernelGGL((k_shade_cmin<true, 512>), dim3(kCminDim, kCminDim), dim3(512), 0, st, dist, color, emis, shade, s,
-                       reflectivity, dist_cmin_shift(s.W, s.H), cmin, hitc, mf, cpal);
+    hipLaunchKernelGGL((k_shade_cmin<true, 512>), dim3(kCminDim, ncr), dim3(512), 0, st, dist, color, emis, shade, s,
+                       reflectivity, dist_cmin_shift(s.W, s.H), cmin, hitc, mf, cpal, cr0);
   else
     hipLaunchKernelGGL(k_shade_cmin<false>, dim3(kCminDim, kCminDim), dim3(256), 0, st, dist, color, emis, shade, s,
-                       reflectivity, dist_cmin_shift(s.W, s.H), cmin, hitc, mf, cpal);
+                       reflectivity, dist_cmin_shift(s.W, s.H), cmin, hitc, mf, cpal, 0);
   return hipGetLastError();
 }
 

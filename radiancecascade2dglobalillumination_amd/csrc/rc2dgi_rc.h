@@ -36,6 +36,7 @@ struct RcParams {
   int tailk;            // tail compaction after this many lockstep iterations (0: off)
   int wgp;              // workgroup-wide exit proof of the first samples
   int tlb;              // tail_bar (RcLevelArgs)
+  const float4 *rcol, *remi;  // records derived from colorRT / emissiveRT (RcLevelArgs rec_color), nullptr: `shade`
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
@@ -273,13 +274,27 @@ __device__ __forceinline__ unsigned ld_dist_esc(const unsigned short *dist, unsi
 // unchanged).  A hit is kept as its byte offset with that index in bits 27-30 (screens of up to 2^26 texels),
 // kCellPal when the cell's palette had no room (the record is then read from shade).
 __device__ __forceinline__ int pal_mark(unsigned boff, unsigned q) { return (int)(boff | (min(q, (unsigned)kCellPal) << 27)); }
+// The record of texel t as k_shade resolves it (RadianceCascades.fs:79-86: (emission, 1) when length(emission) > 0,
+// else (albedo, _Reflectivity)), straight from the inputs: row-strip shards with strip tables keep no record
+// texture (rc2dgi_capi.cpp strip_tables), and colorRT / emissiveRT are whole on every shard.  Both loads in flight
+// together (one round trip), the same arithmetic as k_shade.
+__device__ __forceinline__ float4 derive_record(const float4 *col, const float4 *emi, unsigned t, float refl) {
+  const float4 e = emi[t], c = col[t];
+  return sqrtf(e.x * e.x + e.y * e.y + e.z * e.z) > 0.0f ? make_float4(e.x, e.y, e.z, 1.0f) : make_float4(c.x, c.y, c.z, refl);
+}
+// the record of texel t: the record texture, or (P.rcol) derived from the inputs
+struct RecSrc {
+  const float4 *shade, *col, *emi;
+  float refl;
+  __device__ __forceinline__ float4 operator()(unsigned t) const { return col ? derive_record(col, emi, t, refl) : shade[t]; }
+};
 // the record of hit h (byte-offset convention, pal_mark when palettes are on)
-__device__ __forceinline__ float4 hit_record(const float4 *shade, const float4 *cpal, int h, int lgw, int csh) {
+__device__ __forceinline__ float4 hit_record(const RecSrc &rs, const float4 *cpal, int h, int lgw, int csh) {
   const unsigned t = cpal ? ((unsigned)h & 0x07FFFFFFu) >> 1 : (unsigned)h >> 1, e = (unsigned)h >> 27;
   const unsigned cell = ((t >> (lgw + csh)) * (unsigned)kCminDim) + ((t & ((1u << lgw) - 1u)) >> csh);
-  // one load either way: the palette entry, or the texel's record (palettes off, or no entry)
-  const float4 *p = (cpal && e < (unsigned)kCellPal) ? cpal + (cell * kCellPalStride + e) : shade + t;
-  return *p;
+  // the palette entry, or the texel's record (palettes off, or no entry)
+  if (cpal && e < (unsigned)kCellPal) return cpal[cell * kCellPalStride + e];
+  return rs(t);
 }
 
 // Packed distance field (DL = 2, k_dist_pack): one 16-byte packet per 14 texels of a row.  Bytes
@@ -1148,7 +1163,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
     hr[k] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-    if (!TLC && hit_idx[k] >= 0) hr[k] = shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
+    if (!TLC && hit_idx[k] >= 0) hr[k] = RecSrc{shade, P.rcol, P.remi, P.reflectivity}((unsigned)(BOFF ? hit_idx[k] >> 1 : hit_idx[k]));
   }
   RC_TSTAMP(6);
   RC_SECTION("stage_write");
@@ -1169,7 +1184,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       if (hit_idx[k] >= 0) hr[k] = make_float4(0.5f, 0.5f, 0.5f, 1.0f);
 #else
       if (hit_idx[k] >= 0)
-        hr[k] = PALC ? hit_record(shade, P.cpal, hit_idx[k], P.lgw, P.csh) : shade[BOFF ? hit_idx[k] >> 1 : hit_idx[k]];
+        hr[k] = PALC ? hit_record(RecSrc{shade, P.rcol, P.remi, P.reflectivity}, P.cpal, hit_idx[k], P.lgw, P.csh)
+                     : RecSrc{shade, P.rcol, P.remi, P.reflectivity}((unsigned)(BOFF ? hit_idx[k] >> 1 : hit_idx[k]));
 #endif
   }
 
@@ -1347,6 +1363,8 @@ static inline int rc_tile_params(const RcLevelArgs &a, RcParams &P) {
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
   P.tlb = a.tail_bar;
+  P.rcol = a.rec_color;
+  P.remi = a.rec_emis;
   // palettes: the plain field's march (DL 0) on power-of-two screens whose byte offsets fit 27 bits
   P.cpal = (a.cell_pal && DL == 0 && p2s && (size_t)P.s.pitch * P.s.H <= ((size_t)1 << 26)) ? a.cell_pal : nullptr;
   P.lgw = 0;

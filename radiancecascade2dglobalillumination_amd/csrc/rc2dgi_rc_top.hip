@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     hr[r] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-    if (hit_idx[r] >= 0) hr[r] = hit_record(shade, P.cpal, hit_idx[r], P.lgw, P.csh);
+    if (hit_idx[r] >= 0) hr[r] = hit_record(RecSrc{shade, P.rcol, P.remi, P.reflectivity}, P.cpal, hit_idx[r], P.lgw, P.csh);
   }
   if (!pok) return;
   float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);

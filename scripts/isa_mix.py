@@ -134,7 +134,12 @@ def main():
         for tu in TUS:
             sec_k.update(kernels(compile_asm(tu, True, tmp)))
             prod_k.update(kernels(compile_asm(tu, False, tmp)))
-    rep = {"schedule": os.path.relpath(a.schedule, ROOT), "cost_cycles": COST, "levels": {}}
+    # keyed on the configuration and the per-level variants it was built for: bench.py prices a run's VALU
+    # instructions with this mix only when its own (config, rc_variant) match
+    m = re.match(r"(\d+)x(\d+) N=(\d+)", sched.get("config", ""))
+    cfg = f"{m.group(1)}x{m.group(2)}_N{m.group(3)}" if m else None
+    rep = {"key": {"config": cfg, "rc_variant": [int(v) for v in sched["rc_variant"]]},
+           "schedule": os.path.relpath(a.schedule, ROOT), "cost_cycles": COST, "levels": {}}
     for L in range(N):
         v = sched["rc_variant"][L]
         TX, TY, PY, PD, UNR, DL = VARIANT_SHAPE[v]

@@ -298,7 +298,8 @@ def test_c3_8192_blur_and_merge_every_row(c3_whole):
 
 def test_c3_8192_eight_row_strips(R, c3_whole):
     """8192^2, N=8, rayRange 64 split into 8 row strips, run as 8 in-process shard
-    contexts with the JumpFlood row exchange and the distRT exchange (rc2dgi_do_group), intermediates
+    contexts with the JumpFlood row exchange and the strip tables (rc2dgi_do_group: each shard's side pass over its
+    own cell rows, the march field and the side tables' rows exchanged, no record texture), intermediates
     poisoned, on the committed schedule's strips entry (bench.py --mode strips --shards 8 times it):
     every shard's colorRT / tempRT strip equals the unsharded frame bit for bit (which the tests above
     check against the oracle on every row), over two frames (the second reuses the exchange buffers)."""
@@ -317,6 +318,7 @@ def test_c3_8192_eight_row_strips(R, c3_whole):
         R.do_group(shards)
     for g in shards:
         g.sync()
+        assert g.get_tuning("strip_tables_active") == 1
         y0, y1 = g.shard_rows()
         c, t = g.download("color"), g.download("temp")
         assert np.array_equal(c[y0:y1], w["color_out"][y0:y1]), f"C3 shard rows {y0}:{y1} colorRT"

@@ -29,6 +29,10 @@ def _scene(spec, W, H):
 
     if spec == "demo":
         return scenes.demo(W, H)
+    if spec == "speckled":  # a random colour per occluder texel: the palettes overflow (test_gpu_parity)
+        from test_gpu_parity import speckled_scene
+
+        return speckled_scene(W, H)
     return scenes.random_scene(W, H, int(spec.split(":")[1]))
 
 
@@ -51,6 +55,11 @@ CASES = [
     (128, 128, 3, 4.0, 1.0, 0.0, 5, "rand:24"),   # blur off
     (1024, 1024, 6, 2.0, 1.0, 1.5, 8, "demo"),
     (1200, 900, 6, 2.0, 1.0, 1.5, 8, "demo"),     # C1 size
+    # strip tables (square power-of-two >= 4096: each shard builds the side tables of its own cell rows, the shards
+    # exchange them and the march field; no record texture, records from the palettes or the inputs)
+    (4096, 4096, 6, 2.0, 1.0, 1.5, 4, "demo"),
+    (4096, 4096, 6, 2.0, 1.0, 1.5, 8, "speckled"),  # palettes overflow: records derived from colorRT / emissiveRT
+    (4096, 4096, 8, 64.0, 1.0, 1.5, 2, "rand:27"),
 ]
 
 
@@ -79,7 +88,15 @@ def test_group_shards_match_whole_frame(R, W, H, N, rr, rs, blur, world, scene):
                 got = c.download(k)[y0:y1]
                 mism = np.count_nonzero(got != want[k][y0:y1])
                 assert mism == 0, f"shard {c.shard_rows()} {k}: {mism} values differ"
-            assert np.array_equal(c.download("dist"), want["dist"]), f"shard {c.shard_rows()}: distRT"
+            # the whole distance field (all-gathered) -- with strip tables the shards exchange the march field
+            # instead, and distRT holds the own rows
+            st = c.get_tuning("strip_tables_active")
+            assert st == (W == H and W >= 4096), (W, H, st)
+            d = c.download("dist")
+            if st:
+                assert np.array_equal(d[y0:y1], want["dist"][y0:y1]), f"shard {c.shard_rows()}: distRT rows"
+            else:
+                assert np.array_equal(d, want["dist"]), f"shard {c.shard_rows()}: distRT"
     for c in ctxs:
         c.close()
 
