@@ -190,6 +190,13 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     makes the next rc2dgi_sync / rc2dgi_download / rc2dgi_do return RC2DGI_E_DEVICE and turns
  *                     the chain off for the context (never a silent wrong frame)
  *   "rc_chain_spin"   diagnostic: polls per chain wait (0: the default bound; -1: every wait times out at once)
+ *   "rc_tailbar"      1 (default): the staged upper footprint is written before the tail queue's barrier, so a
+ *                     workgroup whose queue stays empty passes one barrier after the march instead of two
+ *   "jfa_rows"        0 (default), 4, 8: the short isotropic JumpFlood steps (offsets 1, 2, 4 on square power-of-two
+ *                     screens) with that many consecutive rows per lane, each tap row loaded once (measured no faster)
+ *   "strip_tables"    1 (default): row-strip shards build the march's side tables for their own cell rows and exchange
+ *                     them with the march field instead of all-gathering distRT; no record texture (see the sharding
+ *                     section below); get_tuning "strip_tables_active" tells whether the last frame did
  * rc2dgi_get_tuning also answers "rc_variant_count" and "rc_chain_timeouts" (workgroups of the chained
  * frames since the chain was set up that stopped waiting for their upper tiles: 0 in a correct run;
  * synchronises). */
@@ -239,7 +246,11 @@ int rc2dgi_paint(rc2dgi_ctx *ctx, int which, const unsigned char *clear_rgba, co
  * DistanceField) every rank's distRT strip goes to every other rank, then phase 2 (cascades,
  * blur, merge) runs.  Inside phase 1 the JumpFlood steps compute the own strip only and exchange
  * the rows their taps reach (ring halos for short steps, strip-sized blocks at +-offset for long
- * ones; rc2dgi_plan_jfa_exchange), into strip-sized jumpRT windows.  Ways to run a sharded frame:
+ * ones; rc2dgi_plan_jfa_exchange), into strip-sized jumpRT windows.  With strip tables (tuning
+ * "strip_tables", square power-of-two screens >= 4096 whose strips fall on the 64 x 64 bound-table cell rows)
+ * the exchange after phase 1 is instead row 0 of distRT (to every rank: the REPEAT wrap of the last cell row),
+ * then, after each rank's side pass over its own cell rows, its rows of the march field, bound table, hit flags
+ * and surface palettes to every rank; distRT then holds the own rows only.  Ways to run a sharded frame:
  *   - rc2dgi_shard_connect: an RCCL communicator owned by the context (one process per GPU,
  *     ranks = shards); rc2dgi_do then runs the frame with the exchange (ncclBroadcast of each
  *     strip, grouped) on the context stream.  rc2dgi_shard_unique_id makes the id on rank 0;
@@ -258,7 +269,8 @@ int rc2dgi_do_phase(rc2dgi_ctx *ctx, int phase);
 int rc2dgi_do_group(rc2dgi_ctx **ctxs, int n);
 /* raw device storage of a render texture: float4 texels (COLOR = merged output after a frame,
  * else the input; GI1/GI2/BLUR/TEMP/EMISSIVE), uint16 q (DIST), uint32 packed seeds (JUMP1/2; on
- * a row-strip shard its window: row 0 = global row y0 - m, see rc2dgi_plan_jfa_exchange) */
+ * a row-strip shard its window: row 0 = global row y0 - m, see rc2dgi_plan_jfa_exchange).  On a row-strip
+ * shard TEMP and the merged COLOR hold the shard's own rows only (row 0 = global row y0). */
 int rc2dgi_device_buffer(rc2dgi_ctx *ctx, int which, void **dev, int *pitch_bytes);
 
 /* host-only planner (no device needed): the rows a shard computes for one pass.

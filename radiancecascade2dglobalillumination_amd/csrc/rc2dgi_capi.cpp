@@ -148,7 +148,7 @@ struct rc2dgi_ctx {
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   int jfa_rt = 1;                // tuning "jfa_rt": rows per lane of the float-path steps on small screens (1, 2, 4)
   int jfa_rows = 0;              // tuning "jfa_rows": consecutive rows per lane in the short steps (0 off, 4, 8)
-  int rc_tailbar = 0;            // tuning "rc_tailbar": staged footprint written before the tail queue's barrier
+  int rc_tailbar = 1;            // tuning "rc_tailbar": staged footprint written before the tail queue's barrier (default on: RC -0.5 %, profiles/r06/ab/tailbar.txt)
   int jfa_coset = 2;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
@@ -162,6 +162,8 @@ struct rc2dgi_ctx {
   RcMapCache rc_maps;  // host-built k_rc_level workgroup maps
   PaintBuffers paint_buf;  // rc2dgi_paint primitive setup
   int rank = 0, world = 1;
+  int ow0 = 0, ow1 = 0;  // screen rows tempRT / the merged colorRT hold (their row 0 = row ow0): [0, H), or a row-strip
+                         // shard's own rows (out_buffers)
   ncclComm_t comm = nullptr;
   hipEvent_t ev_phase1 = nullptr;   // end of phase 1 (group exchange)
   hipEvent_t ev_frame = nullptr;    // end of the last group frame (peers copy from our distRT)
@@ -399,6 +401,27 @@ bool strip_tables_apply(const rc2dgi_ctx *c) {
   return true;
 }
 
+// tempRT and the merged colorRT of a row-strip shard hold its own rows only (the merge writes nothing else; the
+// kernels take the window's first row, launch_blur_rows / launch_merge m0): 2 x 16 B a texel of the strip instead of
+// the screen.  Unsharded: the whole screen.
+int out_buffers(rc2dgi_ctx *c) {
+  int y0 = 0, y1 = c->H;
+  if (c->world > 1) strip_rows(c->H, c->rank, c->world, y0, y1);
+  if (c->temp && c->color_out && y0 == c->ow0 && y1 == c->ow1) return RC2DGI_OK;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (float4 **b : {&c->temp, &c->color_out}) {
+    if (*b) HIPCHK(c, hipFree(*b));
+    *b = nullptr;
+  }
+  c->ow0 = c->ow1 = 0;
+  const size_t n = (size_t)c->sd.pitch * (size_t)(y1 - y0);
+  HIPCHK(c, alloc(&c->temp, n * sizeof(float4)));
+  HIPCHK(c, alloc(&c->color_out, n * sizeof(float4)));
+  c->ow0 = y0;
+  c->ow1 = y1;
+  return RC2DGI_OK;
+}
+
 // The distRT copies the schedule's variants read ("t" / "p" / "n") and the surface-palette tables (rc_pal),
 // allocated when the schedule or the knobs are set (rc2dgi_set_tuning, rc2dgi_autotune with all = true,
 // allocate), never inside a frame: hipMalloc may synchronise the device, and an out-of-memory then surfaces
@@ -485,6 +508,8 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->emissive, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->temp, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->color_out, ns * sizeof(float4)));
+  c->ow0 = 0;
+  c->ow1 = c->H;
   c->strip = false;
   c->jwin_rows = (size_t)c->H;
   HIPCHK(c, alloc(&c->jump1, ns * sizeof(unsigned)));
@@ -978,8 +1003,9 @@ int phase1_begin(rc2dgi_ctx *c, const FramePlan &plan) {
     HIPCHK(c, hipMemsetAsync(c->jump2, 0xFF, (size_t)c->sd.pitch * c->jwin_rows * 4, st));
     HIPCHK(c, hipMemsetAsync(c->occ, 0xFF, (size_t)c->mpitch * c->H * 4, st));
     HIPCHK(c, hipMemsetAsync(c->dist, 0xFF, ns * 2, st));
-    HIPCHK(c, hipMemsetAsync(c->temp, 0xFF, ns * 16, st));
-    HIPCHK(c, hipMemsetAsync(c->color_out, 0xFF, ns * 16, st));
+    const size_t nw = (size_t)c->sd.pitch * (size_t)(c->ow1 - c->ow0);  // (the own rows on a shard)
+    HIPCHK(c, hipMemsetAsync(c->temp, 0xFF, nw * 16, st));
+    HIPCHK(c, hipMemsetAsync(c->color_out, 0xFF, nw * 16, st));
     for (float4 *b : {c->gi1, c->gi2, c->gi_spare}) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * gi_bytes(c), st));
     for (float4 *b : c->chain_bufs)
       if (b) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * 16, st));
@@ -1277,7 +1303,7 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
       bool ok = true;
       for (auto &r : plan.blur.iv)
         ok = ok && launch_blur_rows(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, c->color_in, c->temp,
-                                    c->color_out, c->sd, mrg, st, r.first, r.second);
+                                    c->color_out, c->sd, mrg, st, r.first, r.second, c->ow0, c->ow1);
       if (!ok && plan.blur.iv.size() > 1) return fail(c, RC2DGI_E_HIP, "fixed-tap blur refused a row interval");
       fused = ok;
       merged = ok && mrg;
@@ -1301,7 +1327,7 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
   if (!merged)
     for (auto &r : plan.merge.iv)
       HIPCHK(c, launch_merge(c->color_in, finalGI, c->temp, c->color_out, c->sd, c->cd, st, r.first, r.second,
-                             c->linux_merge));
+                             c->linux_merge, c->ow0));
   if (T) HIPCHK(c, hipEventRecord(c->ev[5], st));
   c->frame_done = true;
   c->have_frame = true;
@@ -1689,6 +1715,7 @@ int rc2dgi_set_shard(rc2dgi_ctx *c, int rank, int world) {
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   int rc = jfa_buffers(c);  // strip windows (world > 1) or full-size jumpRT1 / jumpRT2
+  if (rc == RC2DGI_OK) rc = out_buffers(c);  // tempRT / merged colorRT: the own rows
   if (rc != RC2DGI_OK) c->broken = true;
   if (rc == RC2DGI_OK) rc = prepare_side_buffers(c);  // (strip tables: no record texture)
   c->st_last = false;
@@ -2263,12 +2290,19 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
                           hipMemcpyDeviceToHost));
     return RC2DGI_OK;
   };
+  // tempRT / the merged colorRT: the rows the context holds (a row-strip shard: its own rows; the others read NaN)
+  auto fetch_out = [&](const float4 *src) -> int {
+    if (c->ow0 > 0 || c->ow1 < h) std::memset(img.data(), 0xFF, img.size() * sizeof(float4));
+    HIPCHK(c, hipMemcpy2D(img.data() + (size_t)c->ow0 * w, (size_t)w * 16, src, (size_t)pitch * 16, (size_t)w * 16,
+                          c->ow1 - c->ow0, hipMemcpyDeviceToHost));
+    return RC2DGI_OK;
+  };
   int rc = RC2DGI_OK;
   const bool n1 = c->N == 1;
   switch (which) {
-    case RC2DGI_RT_COLOR: rc = fetch4(c->frame_done ? c->color_out : c->color_in); break;
+    case RC2DGI_RT_COLOR: rc = c->frame_done ? fetch_out(c->color_out) : fetch4(c->color_in); break;
     case RC2DGI_RT_EMISSIVE: rc = fetch4(c->emissive); break;
-    case RC2DGI_RT_TEMP: rc = fetch4(c->temp); break;
+    case RC2DGI_RT_TEMP: rc = fetch_out(c->temp); break;
     case RC2DGI_RT_GI1: rc = fetch_gi(c, c->gi1, img, gi_bytes(c)); break;
     case RC2DGI_RT_BLUR: rc = fetch_gi(c, c->blur, img, rgba8(c) ? 4 : 16); break;  // RGBA8 mode: bytes
     case RC2DGI_RT_GI2:

@@ -261,14 +261,17 @@ bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Ca
 // Blur + copy-back (+ merge and its copy-back when `merge`) with fixed taps; false when the
 // radius / sizes do not allow it (see k_blur_rows).  blur_rows_plan: F = floor(radius) or -1.
 int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt);
+// (merge outputs: only screen rows [m0, m1) are written, temp / color_out holding row m0 as their row 0 -- a
+// row-strip shard's own rows; m1 = -1: every row)
 bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
                       const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
-                      hipStream_t st, int row0 = 0, int row1 = -1);
+                      hipStream_t st, int row0 = 0, int row1 = -1, int m0 = 0, int m1 = -1);
 
 // merge.fs into temp, then tempRT -> colorRT copy-back (RC2DGI.cs:389-404); linux_merge: raylib's default
 // shader in place of merge.fs (RC2DGI_FLAG_LINUX_MERGE_FALLBACK)
+// (temp / color_out hold screen row m0 as their row 0)
 hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,
-                        CascadeDims c, hipStream_t st, int row0 = 0, int row1 = -1, bool linux_merge = false);
+                        CascadeDims c, hipStream_t st, int row0 = 0, int row1 = -1, bool linux_merge = false, int m0 = 0);
 
 // format conversion for uploads from device memory: RGBA8 unorm -> float4 (k/255; u8: k*(1/255),
 // the value an RGBA8 texture fetch returns)

@@ -1230,7 +1230,7 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
                                                    float4 *__restrict__ blur_out, typename GI::T *__restrict__ gi_out,
                                                    CascadeDims c, BlurTaps bt,
                                                    const float4 *__restrict__ color_in, float4 *__restrict__ temp,
-                                                   float4 *__restrict__ color_out, int spitch, int tile0) {
+                                                   float4 *__restrict__ color_out, int spitch, int tile0, int m0, int m1) {
   constexpr int RPT = RC2DGI_BLUR_RPT, TR = 4 * RPT;  // rows per thread, rows per tile
   constexpr int HALO = F + 1, TW = 64 + 2 * HALO, TH = TR + 2 * HALO, NR = RPT + 2 * HALO;
   __shared__ float4 tile[TH * TW];
@@ -1291,13 +1291,15 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
     blur_out[o] = b;
     GI::st(&gi_out[o], g);
     if constexpr (MERGE) {  // merge.fs:10-15 + tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
-      const size_t so = (size_t)j * spitch + i;
-      const float4 col = color_in[so];
-      const float4 src =
-          make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
-      const float4 tt = blend_over_black(src);
-      temp[so] = tt;
-      color_out[so] = blend(tt, col);
+      if (j >= m0 && j < m1) {  // (the rows temp / color_out hold: a shard's own rows)
+        const size_t so = (size_t)j * spitch + i, mo = (size_t)(j - m0) * spitch + i;
+        const float4 col = color_in[so];
+        const float4 src =
+            make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
+        const float4 tt = blend_over_black(src);
+        temp[mo] = tt;
+        color_out[mo] = blend(tt, col);
+      }
     }
   }
 }
@@ -1319,12 +1321,13 @@ __global__ __launch_bounds__(256) void k_blur_copyback(const typename GI::RT::T 
 template <class GI>
 __global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_in, const typename GI::T *__restrict__ gi,
                                                float4 *__restrict__ temp, float4 *__restrict__ color_out,
-                                               ScreenDims s, CascadeDims c, int row0, int row1, int linux_merge) {
+                                               ScreenDims s, CascadeDims c, int row0, int row1, int linux_merge,
+                                               int m0) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = row0 + blockIdx.y * 4 + (threadIdx.x >> 6);
   if (i >= s.W || j >= row1) return;
   const float u = texcoord(i, Axis{s.W, s.powW}), v = texcoord(j, Axis{s.H, s.powH});
-  const size_t o = (size_t)j * s.pitch + i;
+  const size_t o = (size_t)j * s.pitch + i, mo = (size_t)(j - m0) * s.pitch + i;  // (temp / color_out: from row m0)
   const float4 col = color_in[o];
   float4 src = col;  // Linux: raylib's default shader, texel * colDiffuse (1) * vertex colour (1) = the texel
   if (!linux_merge) {
@@ -1332,8 +1335,8 @@ __global__ __launch_bounds__(256) void k_merge(const float4 *__restrict__ color_
     src = make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
   }
   const float4 t = GI::RT::blend_black(src);  // tempRT as cleared by ClearAllRTs
-  temp[o] = t;
-  color_out[o] = GI::RT::blend(t, col);       // tempRT -> colorRT, default shader, blended
+  temp[mo] = t;
+  color_out[mo] = GI::RT::blend(t, col);      // tempRT -> colorRT, default shader, blended
 }
 
 __global__ __launch_bounds__(256) void k_unorm8_to_f32(const unsigned char *__restrict__ src, int src_pitch,
@@ -1799,8 +1802,9 @@ int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt) {
 
 bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
                       const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
-                      hipStream_t st, int row0, int row1) {
+                      hipStream_t st, int row0, int row1, int m0, int m1) {
   BlurTaps bt;
+  if (m1 < 0) m1 = s.H;
   const int F = blur_rows_plan(c, radius, &bt);
   if (F < 0) return false;
   if (merge && !(s.W == c.CW && s.H == c.CH)) return false;
@@ -1814,10 +1818,10 @@ bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Cas
     if (c.gi_f16)                                                                                              \
       hipLaunchKernelGGL((k_blur_rows<FV, MV, GiF16>), grid, dim3(256), 0, st,                                 \
                          reinterpret_cast<const GiF16::T *>(gi_in), blur_out, reinterpret_cast<GiF16::T *>(gi_out), \
-                         c, bt, color_in, temp, color_out, s.pitch, t0);                                        \
+                         c, bt, color_in, temp, color_out, s.pitch, t0, m0, m1);                                \
     else                                                                                                       \
       hipLaunchKernelGGL((k_blur_rows<FV, MV, GiF32>), grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, bt,  \
-                         color_in, temp, color_out, s.pitch, t0);                                               \
+                         color_in, temp, color_out, s.pitch, t0, m0, m1);                                       \
   } while (0)
   if (merge) {
     if (F == 0) RC2DGI_BLUR_ROWS(0, true); else if (F == 1) RC2DGI_BLUR_ROWS(1, true); else RC2DGI_BLUR_ROWS(2, true);
@@ -1843,18 +1847,19 @@ hipError_t launch_blur_copyback(const float4 *blur, float4 *gi, CascadeDims c, h
 }
 
 hipError_t launch_merge(const float4 *color_in, const float4 *gi, float4 *temp, float4 *color_out, ScreenDims s,
-                        CascadeDims c, hipStream_t st, int row0, int row1, bool linux_merge) {
+                        CascadeDims c, hipStream_t st, int row0, int row1, bool linux_merge, int m0) {
   clamp_rows(s.H, row0, row1);
   if (row0 >= row1) return hipSuccess;
+  if (row0 < m0) return hipErrorInvalidValue;  // (temp / color_out start at row m0)
   if (c.gi_u8)
     hipLaunchKernelGGL(k_merge<GiU8>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in,
-                       reinterpret_cast<const GiU8::T *>(gi), temp, color_out, s, c, row0, row1, (int)linux_merge);
+                       reinterpret_cast<const GiU8::T *>(gi), temp, color_out, s, c, row0, row1, (int)linux_merge, m0);
   else if (c.gi_f16)
     hipLaunchKernelGGL(k_merge<GiF16>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in,
-                       reinterpret_cast<const GiF16::T *>(gi), temp, color_out, s, c, row0, row1, (int)linux_merge);
+                       reinterpret_cast<const GiF16::T *>(gi), temp, color_out, s, c, row0, row1, (int)linux_merge, m0);
   else
     hipLaunchKernelGGL(k_merge<GiF32>, grid2d(s.W, row1 - row0), dim3(256), 0, st, color_in, gi, temp, color_out, s,
-                       c, row0, row1, (int)linux_merge);
+                       c, row0, row1, (int)linux_merge, m0);
   return hipGetLastError();
 }
 
