@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-end evidence on one box, in one call: the GPU suite, the headline bench with its rocprofv3 kernel stats
-# and PMC traffic (scripts/round_profile.sh), one line per BASELINE config and storage mode, the C3 strips and
-# the C4 batch lines.  Results under gpurun_out/ (copied into profiles/r<NN>/final by hand).
+# and PMC traffic per scene (scripts/round_profile.sh), one line per BASELINE config and storage mode, the C3 strips,
+# the C4 batch lines and the scene sweep (scripts/scene_sweep.sh).  Results under gpurun_out/ (copied into
+# profiles/r<NN>/final by hand; gpurun_out/rc_level_pmc.json to profiles/).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out; export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
@@ -22,3 +23,5 @@ for bs in 1 0; do
     > gpurun_out/cfg/c4_streams$bs.log 2>&1 || exit $?
   tail -1 gpurun_out/cfg/c4_streams$bs.log | cut -c1-300
 done
+echo "== scenes"
+bash scripts/scene_sweep.sh || exit $?

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: per-kernel time of the C3 frame (8192^2, N=8, rayRange 64) unsharded and as 8 in-process row strips
+# Per-kernel time of the C3 frame (8192^2, N=8, rayRange 64) unsharded and as 8 in-process row strips
 # (rocprofv3 kernel-trace stats; scripts/frame_kernel_sums.py).  Output: gpurun_out/strips_prof/
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out/strips_prof; export TMPDIR=/tmp
