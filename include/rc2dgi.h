@@ -190,11 +190,9 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     makes the next rc2dgi_sync / rc2dgi_download / rc2dgi_do return RC2DGI_E_DEVICE and turns
  *                     the chain off for the context (never a silent wrong frame)
  *   "rc_chain_spin"   diagnostic: polls per chain wait (0: the default bound; -1: every wait times out at once)
- *   "rc_tailbar"      1 (default): the staged upper footprint is written before the tail queue's barrier, so a
- *                     workgroup whose queue stays empty passes one barrier after the march instead of two
  *   "jfa_rows"        0 (default), 4, 8: the short isotropic JumpFlood steps (offsets 1, 2, 4 on square power-of-two
  *                     screens) with that many consecutive rows per lane, each tap row loaded once (measured no faster)
- *   "strip_tables"    1 (default): row-strip shards build the march's side tables for their own cell rows and exchange
+ *   "strip_tables"    1 (default; f32 storage): row-strip shards build the march's side tables for their own cell rows and exchange
  *                     them with the march field instead of all-gathering distRT; no record texture (see the sharding
  *                     section below); get_tuning "strip_tables_active" tells whether the last frame did
  * rc2dgi_get_tuning also answers "rc_variant_count" and "rc_chain_timeouts" (workgroups of the chained

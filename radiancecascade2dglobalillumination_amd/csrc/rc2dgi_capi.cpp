@@ -148,7 +148,6 @@ struct rc2dgi_ctx {
   int jfa_lds = 0;               // tuning "jfa_lds": LDS-staged taps for the short JumpFlood steps
   int jfa_rt = 1;                // tuning "jfa_rt": rows per lane of the float-path steps on small screens (1, 2, 4)
   int jfa_rows = 0;              // tuning "jfa_rows": consecutive rows per lane in the short steps (0 off, 4, 8)
-  int rc_tailbar = 1;            // tuning "rc_tailbar": staged footprint written before the tail queue's barrier (default on: RC -0.5 %, profiles/r06/ab/tailbar.txt)
   int jfa_coset = 2;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
@@ -389,6 +388,7 @@ bool proofs_on(const rc2dgi_ctx *c) { return c->rc_skip > 1 || (c->rc_skip == 1 
 // every strip boundary falls on a cell row, and every level marches on the plain field.
 bool strip_tables_apply(const rc2dgi_ctx *c) {
   if (c->world < 2 || !c->strip_tables || !c->rc_pal || !c->shade_fused || !proofs_on(c)) return false;
+  if (c->storage != RC2DGI_STORAGE_F32) return false;  // (the derived-record marches are built for f32 cascades)
   if (!shade_cmin_fused_ok(c->W, c->H, c->sd.pitch) || (size_t)c->sd.pitch * c->H > ((size_t)1 << 26)) return false;
   for (int v : c->rc_variant)
     if (rc_variant_tiled(v) || rc_variant_packed(v) || rc_variant_nib(v)) return false;
@@ -414,7 +414,7 @@ int out_buffers(rc2dgi_ctx *c) {
     *b = nullptr;
   }
   c->ow0 = c->ow1 = 0;
-  const size_t n = (size_t)c->sd.pitch * (size_t)(y1 - y0);
+  const size_t n = (size_t)c->sd.pitch * (size_t)(y1 - y0 + 1);  // (+ the guard row k_blur_rows writes outside rows to)
   HIPCHK(c, alloc(&c->temp, n * sizeof(float4)));
   HIPCHK(c, alloc(&c->color_out, n * sizeof(float4)));
   c->ow0 = y0;
@@ -506,8 +506,10 @@ int allocate(rc2dgi_ctx *c) {
   const size_t ns = (size_t)sp * c->H, nc = (size_t)cp * c->CH;
   HIPCHK(c, alloc(&c->color_in, ns * sizeof(float4)));
   HIPCHK(c, alloc(&c->emissive, ns * sizeof(float4)));
-  HIPCHK(c, alloc(&c->temp, ns * sizeof(float4)));
-  HIPCHK(c, alloc(&c->color_out, ns * sizeof(float4)));
+  // (tempRT / merged colorRT: one guard row after the screen, which k_blur_rows' merge writes the rows outside the
+  // held window into, out_buffers)
+  HIPCHK(c, alloc(&c->temp, (ns + sp) * sizeof(float4)));
+  HIPCHK(c, alloc(&c->color_out, (ns + sp) * sizeof(float4)));
   c->ow0 = 0;
   c->ow1 = c->H;
   c->strip = false;
@@ -1255,7 +1257,6 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
-    a.tail_bar = c->rc_tailbar;
 
     if (chain && (L < c->N - 1 || c->rc_chain == 4)) {
       chain_args.push_back(a);  // (whole levels: one process; rc_chain 4: the top level in the launch too)
@@ -2049,10 +2050,6 @@ int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value) {
     c->jfa_lds = value != 0;
     return RC2DGI_OK;
   }
-  if (k == "rc_tailbar") {
-    c->rc_tailbar = value != 0;
-    return RC2DGI_OK;
-  }
   if (k == "jfa_rows") {
     if (value != 0 && value != 4 && value != 8) return fail(c, RC2DGI_E_ARG, "jfa_rows is 0, 4 or 8");
     c->jfa_rows = value;
@@ -2163,10 +2160,6 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "strip_tables_active") {  // the last frame ran with strip tables (strip_tables_apply)
     *value = c->st_last ? 1 : 0;
-    return RC2DGI_OK;
-  }
-  if (k == "rc_tailbar") {
-    *value = c->rc_tailbar;
     return RC2DGI_OK;
   }
   if (k == "jfa_rows") {

@@ -125,8 +125,6 @@ struct RcLevelArgs {
   int cmin_screen = 0;          // the exit proof also tests the screen edge (worth it for long rays)
   int tail_k = 0;               // tail compaction after this many lockstep march iterations (0: off)
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
-  int tail_bar = 0;             // the staged footprint written before the tail queue's barrier: one barrier when
-                                // the queue is empty (tuning rc_tailbar)
   const float4 *rec_color = nullptr, *rec_emis = nullptr;  // hit records derived from colorRT / emissiveRT instead
                                                           // of read from `shade` (row-strip shards, strip tables)
 };
@@ -261,8 +259,8 @@ bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Ca
 // Blur + copy-back (+ merge and its copy-back when `merge`) with fixed taps; false when the
 // radius / sizes do not allow it (see k_blur_rows).  blur_rows_plan: F = floor(radius) or -1.
 int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt);
-// (merge outputs: only screen rows [m0, m1) are written, temp / color_out holding row m0 as their row 0 -- a
-// row-strip shard's own rows; m1 = -1: every row)
+// (merge outputs: temp / color_out hold screen rows [m0, m1) from their row 0 -- a row-strip shard's own rows; m1 = -1:
+// every row -- and one guard row after those, which receives the merge of every row outside them)
 bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
                       const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
                       hipStream_t st, int row0 = 0, int row1 = -1, int m0 = 0, int m1 = -1);

@@ -1291,15 +1291,16 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
     blur_out[o] = b;
     GI::st(&gi_out[o], g);
     if constexpr (MERGE) {  // merge.fs:10-15 + tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
-      if (j >= m0 && j < m1) {  // (the rows temp / color_out hold: a shard's own rows)
-        const size_t so = (size_t)j * spitch + i, mo = (size_t)(j - m0) * spitch + i;
-        const float4 col = color_in[so];
-        const float4 src =
-            make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
-        const float4 tt = blend_over_black(src);
-        temp[mo] = tt;
-        color_out[mo] = blend(tt, col);
-      }
+      // temp / color_out hold rows [m0, m1) (a shard's own rows) and one guard row after them, which takes the
+      // rows outside (unconditional stores: a branch around them doubled the kernel's registers)
+      const int jr = (j >= m0 && j < m1) ? j - m0 : m1 - m0;
+      const size_t so = (size_t)j * spitch + i, mo = (size_t)jr * spitch + i;
+      const float4 col = color_in[so];
+      const float4 src =
+          make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);
+      const float4 tt = blend_over_black(src);
+      temp[mo] = tt;
+      color_out[mo] = blend(tt, col);
     }
   }
 }

@@ -35,7 +35,6 @@ struct RcParams {
   int cscr;             // the exit proof tests the screen edge too
   int tailk;            // tail compaction after this many lockstep iterations (0: off)
   int wgp;              // workgroup-wide exit proof of the first samples
-  int tlb;              // tail_bar (RcLevelArgs)
   const float4 *rcol, *remi;  // records derived from colorRT / emissiveRT (RcLevelArgs rec_color), nullptr: `shade`
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
@@ -409,7 +408,10 @@ __device__ __forceinline__ void st_sc1(float4 *base, unsigned off, float4 v) {
 // the upper level is an sc1 load.  The footprint is widened to whole 128-byte lines, so no line a consumer reads
 // holds texels of a tile it did not wait for.  A poll gives up after kChainSpin tries (counted in the error word):
 // a broken assumption shows as wrong results, never as a hung GPU.
-template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false, bool CH = false>
+// RD: hit records derived from colorRT / emissiveRT (P.rcol; row-strip shards with strip tables) -- its own
+// instantiations, since the derivation's registers and code cost the other marches ~1 % (profiles/r06/ab/rdr.txt)
+template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false, bool CH = false,
+          bool RD = false>
 __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
@@ -553,6 +555,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   constexpr int CMN = kCminDim * kCminDim;
   __shared__ __attribute__((aligned(16))) CminT s_cm[CMS ? CMN : 1];
   constexpr bool TLC = !Z0 && NR == 4;  // one probe and one direction block per lane (the high-level tiles)
+  // records derived from the inputs (RD, P.rcol: row-strip shards with strip tables) only in the plain-field marches,
+  // the only ones strip tables run (strip_tables_apply); the other instantiations keep the record texture's single load
+  constexpr bool RDR = RD;
+  static_assert(!RD || (DL == 0 && !CH), "derived records: the plain-field marches");
   constexpr bool PALC = TLC && !TILED && !PACKED;  // surface palettes (P.cpal): the one-probe tiles of the plain field
   // Tail compaction.  A lane marches its NR rays in lockstep and a wave runs until its longest ray
   // ends, so the few rays that pass close to a surface (steps shrink, then grow geometrically) set
@@ -607,7 +613,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   // 47 % of the top level's workgroups; at rayRange 64 every workgroup of the two top levels (any tile shape: the
   // several-probes-per-lane tiles of C2 / C3 skip their bound table and workgroup proof the same way).
   bool wg_off = false;
+#ifdef RC2DGI_AB_NO_WGOFF  // (A/B builds: no whole-workgroup far-interval test)
+  if constexpr (false) {
+#else
   if constexpr (!Z0 && !CH) {
+#endif
     if (P.t0 >= 0.25f && !(P.t0 > P.t1)) {
       const int cxl = min(cx0 + TX, P.bdx) - 1, cyl = min(cy0 + THY, P.p1) - 1;
       const bool pw = P2S || P.c.powW, ph = P2S || P.c.powH;
@@ -1073,7 +1083,6 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
   RC_SECTION("tail");
   RC_TSTAMP(5);
   int qpos[TLC ? NR : 1];  // queue entry of each pending ray of this lane
-  unsigned tail_n = 1;     // (P.tlb) rays the tail queue held: workgroup-uniform after its barrier
   if (tl) {
     // pending rays (still marching after itend iterations) -> LDS queue, wave-contiguous ranges
     unsigned n = 0;
@@ -1097,12 +1106,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       qpos[k] = (int)pos;
       if (t[k] < kDone) s_q[pos++] = make_uint2(__float_as_uint(t[k]), (threadIdx.x << 3) | (unsigned)k);
     }
-    if (P.tlb) stage_write();  // (P.tlb: this barrier also publishes the staged footprint)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     const unsigned nq = s_qn;
-    tail_n = nq;
     for (unsigned j = (unsigned)wv * 64u + (unsigned)lane; j < nq; j += NT) {
       const uint2 e = s_q[j];
       const unsigned otid = e.y >> 3, k = e.y & 7u;
@@ -1163,15 +1170,12 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
     hr[k] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-    if (!TLC && hit_idx[k] >= 0) hr[k] = RecSrc{shade, P.rcol, P.remi, P.reflectivity}((unsigned)(BOFF ? hit_idx[k] >> 1 : hit_idx[k]));
+    if (!TLC && hit_idx[k] >= 0) hr[k] = RecSrc{shade, RDR ? P.rcol : nullptr, P.remi, P.reflectivity}((unsigned)(BOFF ? hit_idx[k] >> 1 : hit_idx[k]));
   }
   RC_TSTAMP(6);
   RC_SECTION("stage_write");
-  // P.tlb with the tail queue: the footprint was written before the queue's barrier, so a second barrier is
-  // needed only when the queue held rays (their hit texels come back through LDS)
-  const bool fused_bar = tl && P.tlb;
-  if (!fused_bar) stage_write();
-  if (fused_bar ? tail_n != 0u : (stg || tl)) __syncthreads();
+  stage_write();
+  if (stg || tl) __syncthreads();
   if (tl) {  // hit texels of this lane's rays that finished in the tail
 #pragma unroll
     for (int k = 0; k < NR; ++k)
@@ -1184,8 +1188,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
       if (hit_idx[k] >= 0) hr[k] = make_float4(0.5f, 0.5f, 0.5f, 1.0f);
 #else
       if (hit_idx[k] >= 0)
-        hr[k] = PALC ? hit_record(RecSrc{shade, P.rcol, P.remi, P.reflectivity}, P.cpal, hit_idx[k], P.lgw, P.csh)
-                     : RecSrc{shade, P.rcol, P.remi, P.reflectivity}((unsigned)(BOFF ? hit_idx[k] >> 1 : hit_idx[k]));
+        hr[k] = PALC ? hit_record(RecSrc{shade, RDR ? P.rcol : nullptr, P.remi, P.reflectivity}, P.cpal, hit_idx[k], P.lgw, P.csh)
+                     : RecSrc{shade, RDR ? P.rcol : nullptr, P.remi, P.reflectivity}((unsigned)(BOFF ? hit_idx[k] >> 1 : hit_idx[k]));
 #endif
   }
 
@@ -1362,7 +1366,6 @@ static inline int rc_tile_params(const RcLevelArgs &a, RcParams &P) {
   if (P.cmin && P.cscr && !P.dexit) return -1;
   P.tailk = a.tail_k;
   P.wgp = a.wg_proof;
-  P.tlb = a.tail_bar;
   P.rcol = a.rec_color;
   P.remi = a.rec_emis;
   // palettes: the plain field's march (DL 0) on power-of-two screens whose byte offsets fit 27 bits
@@ -1383,12 +1386,24 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   const int nwg = rc_tile_params<TX, TY, PY, PD, DL>(a, P);
   if (nwg == 0) return hipErrorOutOfMemory;
   if (nwg < 0) return hipErrorInvalidValue;
-#define RC2DGI_RC(TOPV, P2V, Z0V)                                                                            \
-  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL >= 2 ? 0 : DL)), GI, Z0V>), \
-                     dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),   \
-                     reinterpret_cast<typename GI::T *>(a.out), DL == 1 ? a.dist_tiled : a.dist, a.shade,     \
+#define RC2DGI_RC_RD(TOPV, P2V, Z0V, RDV)                                                                          \
+  hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL >= 2 ? 0 : DL)), GI, Z0V, false, RDV>), \
+                     dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),          \
+                     reinterpret_cast<typename GI::T *>(a.out), DL == 1 ? a.dist_tiled : a.dist, a.shade,            \
                      a.dirs, a.sky, DL == 3 ? a.dist_nib : a.dist_packed)
+#define RC2DGI_RC(TOPV, P2V, Z0V) RC2DGI_RC_RD(TOPV, P2V, Z0V, false)
   const bool top = a.level == a.N - 1;
+  if (P.rcol) {  // derived records (strip tables: f32 cascades, power-of-two screens, the plain field)
+    if constexpr (DL == 0 && std::is_same<GI, GiF32>::value) {
+      if (!p2s) return hipErrorInvalidValue;
+      if (top) RC2DGI_RC_RD(true, true, false, true);
+      else if (a.level == 0 && P.t0 == 0.0f) RC2DGI_RC_RD(false, true, true, true);
+      else RC2DGI_RC_RD(false, true, false, true);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
+  }
   if (top) {
     if (p2s) RC2DGI_RC(true, true, false); else RC2DGI_RC(true, false, false);
   } else if (p2s) {
@@ -1398,6 +1413,7 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
     RC2DGI_RC(false, false, false);
   }
 #undef RC2DGI_RC
+#undef RC2DGI_RC_RD
   return hipGetLastError();
 }
 

@@ -541,8 +541,6 @@ def test_exit_proofs_and_tail_are_bit_identical(RC2DGI, W, H, N, rr, rs, scene):
         for skip, tail in ((0, 0), (1, 0), (2, 1), (3, 3), (1, 2), (0, 5), (1, 31)):
             ctx.set_tuning("rc_skip", skip)
             ctx.set_tuning("rc_tail", tail)
-            # rc_tailbar: the staged footprint published by the tail queue's barrier (one barrier when it is empty)
-            ctx.set_tuning("rc_tailbar", (tail + v) & 1)
             assert ctx.get_tuning("rc_skip") == skip and ctx.get_tuning(f"rc_tail_L{N - 1}") == tail
             ctx.do_rc2dgi()
             ctx.sync()
