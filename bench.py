@@ -383,6 +383,24 @@ def bench_strips(a, rank, local, world):
     rdist.barrier()
     wall = rdist.max_over_ranks([time.perf_counter() - t0], device="cuda")[0]
     units = CW * CH * N * a.steps  # one frame per step, whatever the shard count
+    cfg_line = {"rc_variant": [ctxs[0].get_tuning(f"rc_variant_L{L}") for L in range(N)],
+                "strip_tables": tuning_or_none(ctxs[0], "strip_tables_active"),
+                "blur_strip_sized": tuning_or_none(ctxs[0], "blur_strip_sized")}
+    for g in ctxs:
+        g.close()
+    mem = {"device_bytes_per_shard": int(shard_bytes)}
+    if rank == 0 and nsh > 1:  # the same frame as one unsharded context, for the per-shard fraction
+        free1 = torch.cuda.mem_get_info(local)[0]
+        g = RC2DGI(W, H, cascade_count=N, ray_range=a.ray_range, device=local)
+        g.upload("color", color)
+        g.upload("emissive", emis)
+        if tun:
+            apply_schedule(g, tun, N)
+        g.do_rc2dgi()
+        g.sync()
+        whole = free1 - torch.cuda.mem_get_info(local)[0]
+        g.close()
+        mem.update(device_bytes_one_context=int(whole), shard_memory_frac=round(shard_bytes / whole, 3))
     if rank == 0:
         print(json.dumps({
             "metric": f"Mpixel*cascades/s (whole DoRC2DGI frame, row strips) at {W}x{H}, cascadeCount={N}",
@@ -392,12 +410,9 @@ def bench_strips(a, rank, local, world):
             "data": f"synthetic (reference demo scene painted at {W}x{H}, resident in HBM)",
             "config": {"workload": f"DoRC2DGI {W}x{H} cascadeCount={N} rayRange={a.ray_range}, row strips",
                        "shards": nsh, "parallelism": f"strips{nsh}" + ("-in-process" if virtual else "-rccl"),
-                       "rc_variant": [ctxs[0].get_tuning(f"rc_variant_L{L}") for L in range(N)],
-                       "strip_tables": tuning_or_none(ctxs[0], "strip_tables_active")},
-            "device_bytes_per_shard": int(shard_bytes),
+                       **cfg_line},
+            **mem,
             "frames_per_s": round(a.steps / wall, 2)}), flush=True)
-    for g in ctxs:
-        g.close()
 
 
 def strips_launch_check(a, rank, world):

@@ -195,7 +195,8 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *   "strip_tables"    1 (default; f32 storage): row-strip shards build the march's side tables for their own cell rows and exchange
  *                     them with the march field instead of all-gathering distRT; no record texture (see the sharding
  *                     section below); get_tuning "strip_tables_active" tells whether the last frame did
- * rc2dgi_get_tuning also answers "rc_variant_count" and "rc_chain_timeouts" (workgroups of the chained
+ * rc2dgi_get_tuning also answers "blur_strip_sized" (1: a shard's BLUR / FINAL_GI textures hold its own rows,
+ * rc2dgi_device_buffer), "rc_variant_count" and "rc_chain_timeouts" (workgroups of the chained
  * frames since the chain was set up that stopped waiting for their upper tiles: 0 in a correct run;
  * synchronises). */
 int rc2dgi_set_tuning(rc2dgi_ctx *ctx, const char *key, int value);
@@ -268,7 +269,11 @@ int rc2dgi_do_group(rc2dgi_ctx **ctxs, int n);
 /* raw device storage of a render texture: float4 texels (COLOR = merged output after a frame,
  * else the input; GI1/GI2/BLUR/TEMP/EMISSIVE), uint16 q (DIST), uint32 packed seeds (JUMP1/2; on
  * a row-strip shard its window: row 0 = global row y0 - m, see rc2dgi_plan_jfa_exchange).  On a row-strip
- * shard TEMP and the merged COLOR hold the shard's own rows only (row 0 = global row y0). */
+ * shard TEMP and the merged COLOR hold the shard's own rows only (row 0 = global row y0); so do BLUR and, after a
+ * frame, FINAL_GI when the blur runs fused with the merge (power-of-two cascades the size of the screen, a dyadic
+ * _BlurRadius below 3, blur_path 0, no LINUX_MERGE flag): the blurred copy-back then stays in a strip-sized texture
+ * of its own, and GI1 / GI2 keep the cascade's unblurred level 0 (rc2dgi_download of FINAL_GI / BLUR: the own
+ * rows, the others NaN).  These textures are resized before a frame when the blur settings change. */
 int rc2dgi_device_buffer(rc2dgi_ctx *ctx, int which, void **dev, int *pitch_bytes);
 
 /* host-only planner (no device needed): the rows a shard computes for one pass.

@@ -163,6 +163,9 @@ struct rc2dgi_ctx {
   int rank = 0, world = 1;
   int ow0 = 0, ow1 = 0;  // screen rows tempRT / the merged colorRT hold (their row 0 = row ow0): [0, H), or a row-strip
                          // shard's own rows (out_buffers)
+  bool gwin = false;     // cascadeBlurRT and the blur's copy-back texture (gi_spare) hold rows [ow0, ow1) too
+                         // (a shard on the fused blur + merge, gi_window_apply); the copy-back then stays in
+                         // gi_spare (no buffer swap) and is the frame's final GI
   ncclComm_t comm = nullptr;
   hipEvent_t ev_phase1 = nullptr;   // end of phase 1 (group exchange)
   hipEvent_t ev_frame = nullptr;    // end of the last group frame (peers copy from our distRT)
@@ -401,24 +404,44 @@ bool strip_tables_apply(const rc2dgi_ctx *c) {
   return true;
 }
 
+// A row-strip shard whose blur runs as k_blur_rows with the merge fused (power-of-two cascades the size of the
+// screen, a dyadic radius, raylib's merge shader not asked for) writes cascadeBlurRT and the copied-back GI of the
+// rows it merges only: those two textures then hold the own rows as well (out_buffers).
+bool gi_window_apply(const rc2dgi_ctx *c) {
+  BlurTaps bt;
+  return c->world > 1 && c->blur_radius > 0.0f && c->blur_path == 0 && c->sd.W == c->CW && c->sd.H == c->CH &&
+         !c->linux_merge && blur_rows_plan(c->cd, c->blur_radius, &bt) >= 0;
+}
+
 // tempRT and the merged colorRT of a row-strip shard hold its own rows only (the merge writes nothing else; the
 // kernels take the window's first row, launch_blur_rows / launch_merge m0): 2 x 16 B a texel of the strip instead of
-// the screen.  Unsharded: the whole screen.
+// the screen; on the fused blur + merge (gi_window_apply) cascadeBlurRT and the copy-back texture too.  Unsharded:
+// the whole screen.  Called when the shard is set and before every frame (the blur radius and path may change
+// between frames), before anything of the frame is enqueued.
 int out_buffers(rc2dgi_ctx *c) {
   int y0 = 0, y1 = c->H;
   if (c->world > 1) strip_rows(c->H, c->rank, c->world, y0, y1);
-  if (c->temp && c->color_out && y0 == c->ow0 && y1 == c->ow1) return RC2DGI_OK;
+  const bool gw = gi_window_apply(c);
+  if (c->temp && c->color_out && c->blur && c->gi_spare && y0 == c->ow0 && y1 == c->ow1 && gw == c->gwin)
+    return RC2DGI_OK;
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (float4 **b : {&c->temp, &c->color_out}) {
+  for (float4 **b : {&c->temp, &c->color_out, &c->blur, &c->gi_spare}) {
     if (*b) HIPCHK(c, hipFree(*b));
     *b = nullptr;
   }
   c->ow0 = c->ow1 = 0;
+  c->gwin = false;
   const size_t n = (size_t)c->sd.pitch * (size_t)(y1 - y0 + 1);  // (+ the guard row k_blur_rows writes outside rows to)
   HIPCHK(c, alloc(&c->temp, n * sizeof(float4)));
   HIPCHK(c, alloc(&c->color_out, n * sizeof(float4)));
+  // (gw: the cascade is the screen, one pitch)
+  const size_t nc = gw ? n : (size_t)c->cd.pitch * c->CH;
+  HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
+  HIPCHK(c, alloc(&c->gi_spare, nc * gi_bytes(c)));
+  HIPCHK(c, hipMemsetAsync(c->blur, 0, nc * sizeof(float4), c->stream));  // (a fresh texture, as allocate())
   c->ow0 = y0;
   c->ow1 = y1;
+  c->gwin = gw;
   return RC2DGI_OK;
 }
 
@@ -512,6 +535,7 @@ int allocate(rc2dgi_ctx *c) {
   HIPCHK(c, alloc(&c->color_out, (ns + sp) * sizeof(float4)));
   c->ow0 = 0;
   c->ow1 = c->H;
+  c->gwin = false;
   c->strip = false;
   c->jwin_rows = (size_t)c->H;
   HIPCHK(c, alloc(&c->jump1, ns * sizeof(unsigned)));
@@ -661,28 +685,32 @@ float half_to_float(uint16_t h) {  // exact
   return s ? -v : v;
 }
 
-// a GI-format cascade texture -> float4 (CW x CH, tight); texels of RGBA8 storage read as k * (1/255)
-int fetch_gi(rc2dgi_ctx *c, const void *src, std::vector<float4> &img, size_t gsz) {
+// a GI-format cascade texture -> float4 (CW x CH, tight); texels of RGBA8 storage read as k * (1/255).  The source
+// holds rows [y0, y1) from its row 0 (a shard's strip-sized blur textures); the other rows read as NaN.
+int fetch_gi(rc2dgi_ctx *c, const void *src, std::vector<float4> &img, size_t gsz, int y0 = 0, int y1 = -1) {
+  if (y1 < 0) y1 = c->CH;
+  const size_t nr = (size_t)(y1 - y0), off = (size_t)y0 * c->CW, nt = nr * c->CW;
+  if (y0 > 0 || y1 < c->CH) std::memset(img.data(), 0xFF, img.size() * sizeof(float4));
   if (gsz == 16) {
-    HIPCHK(c, hipMemcpy2D(img.data(), (size_t)c->CW * 16, src, (size_t)c->cd.pitch * 16, (size_t)c->CW * 16, c->CH,
+    HIPCHK(c, hipMemcpy2D(img.data() + off, (size_t)c->CW * 16, src, (size_t)c->cd.pitch * 16, (size_t)c->CW * 16, nr,
                           hipMemcpyDeviceToHost));
     return RC2DGI_OK;
   }
   if (gsz == 4) {
-    std::vector<uint8_t> b((size_t)c->CW * c->CH * 4);
-    HIPCHK(c, hipMemcpy2D(b.data(), (size_t)c->CW * 4, src, (size_t)c->cd.pitch * 4, (size_t)c->CW * 4, c->CH,
+    std::vector<uint8_t> b(nt * 4);
+    HIPCHK(c, hipMemcpy2D(b.data(), (size_t)c->CW * 4, src, (size_t)c->cd.pitch * 4, (size_t)c->CW * 4, nr,
                           hipMemcpyDeviceToHost));
-    for (size_t k = 0; k < img.size(); ++k)
-      img[k] = make_float4((float)b[4 * k] * kInv255h, (float)b[4 * k + 1] * kInv255h, (float)b[4 * k + 2] * kInv255h,
-                           (float)b[4 * k + 3] * kInv255h);
+    for (size_t k = 0; k < nt; ++k)
+      img[off + k] = make_float4((float)b[4 * k] * kInv255h, (float)b[4 * k + 1] * kInv255h,
+                                 (float)b[4 * k + 2] * kInv255h, (float)b[4 * k + 3] * kInv255h);
     return RC2DGI_OK;
   }
-  std::vector<uint16_t> h((size_t)c->CW * c->CH * 4);
-  HIPCHK(c, hipMemcpy2D(h.data(), (size_t)c->CW * 8, src, (size_t)c->cd.pitch * 8, (size_t)c->CW * 8, c->CH,
+  std::vector<uint16_t> h(nt * 4);
+  HIPCHK(c, hipMemcpy2D(h.data(), (size_t)c->CW * 8, src, (size_t)c->cd.pitch * 8, (size_t)c->CW * 8, nr,
                         hipMemcpyDeviceToHost));
-  for (size_t k = 0; k < img.size(); ++k)
-    img[k] = make_float4(half_to_float(h[4 * k]), half_to_float(h[4 * k + 1]), half_to_float(h[4 * k + 2]),
-                         half_to_float(h[4 * k + 3]));
+  for (size_t k = 0; k < nt; ++k)
+    img[off + k] = make_float4(half_to_float(h[4 * k]), half_to_float(h[4 * k + 1]), half_to_float(h[4 * k + 2]),
+                               half_to_float(h[4 * k + 3]));
   return RC2DGI_OK;
 }
 
@@ -1008,10 +1036,12 @@ int phase1_begin(rc2dgi_ctx *c, const FramePlan &plan) {
     const size_t nw = (size_t)c->sd.pitch * (size_t)(c->ow1 - c->ow0);  // (the own rows on a shard)
     HIPCHK(c, hipMemsetAsync(c->temp, 0xFF, nw * 16, st));
     HIPCHK(c, hipMemsetAsync(c->color_out, 0xFF, nw * 16, st));
-    for (float4 *b : {c->gi1, c->gi2, c->gi_spare}) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * gi_bytes(c), st));
+    const size_t nb = c->gwin ? (size_t)c->cd.pitch * (size_t)(c->ow1 - c->ow0) : nc;  // (cascadeBlurRT, spare)
+    for (float4 *b : {c->gi1, c->gi2}) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * gi_bytes(c), st));
+    HIPCHK(c, hipMemsetAsync(c->gi_spare, 0xFF, nb * gi_bytes(c), st));
     for (float4 *b : c->chain_bufs)
       if (b) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * 16, st));
-    HIPCHK(c, hipMemsetAsync(c->blur, 0xFF, nc * 16, st));
+    HIPCHK(c, hipMemsetAsync(c->blur, 0xFF, nb * 16, st));
   }
   if (T) HIPCHK(c, hipEventRecord(c->ev[0], st));
 
@@ -1309,6 +1339,9 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
       fused = ok;
       merged = ok && mrg;
     }
+    // (strip-sized cascadeBlurRT / copy-back texture: only the fused blur + merge writes them; out_buffers sized them
+    // for this frame's settings)
+    if (c->gwin && !merged) return fail(c, RC2DGI_E_STATE, "strip-sized blur textures without the fused blur + merge");
     if (!fused && c->blur_path <= 1 && blur_fused_ok(c->cd, c->blur_radius)) {
       bool ok = true;
       for (auto &r : plan.blur.iv)
@@ -1318,7 +1351,7 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
     }
     if (fused) {
       HIPCHK(c, hipGetLastError());
-      std::swap(finalGI, c->gi_spare);
+      if (!c->gwin) std::swap(finalGI, c->gi_spare);  // (gwin: the final GI stays in the strip-sized gi_spare)
     } else {
       for (auto &r : plan.blur.iv) HIPCHK(c, launch_blur(finalGI, c->blur, c->cd, c->blur_radius, st, r.first, r.second));
       for (auto &r : plan.blur.iv) HIPCHK(c, launch_blur_copyback(c->blur, finalGI, c->cd, st, r.first, r.second));
@@ -1361,6 +1394,7 @@ int rc2dgi_do(rc2dgi_ctx *c) {
   if (int rc = check_chain(c)) return rc;  // (an earlier chained frame that has completed)
   if (c->world > 1 && !c->comm)
     return fail(c, RC2DGI_E_STATE, "sharded context: use rc2dgi_shard_connect, rc2dgi_do_group or rc2dgi_do_phase");
+  if (int rc = out_buffers(c)) return rc;  // (the strip-sized outputs follow the blur settings)
   const FramePlan plan = make_plan(c);
   int rc = do_phase1(c, plan);
   if (rc != RC2DGI_OK) return rc;
@@ -1415,6 +1449,7 @@ int rc2dgi_do_phase(rc2dgi_ctx *c, int phase) {
     return fail(c, RC2DGI_E_STATE,
                 "phase 1 of a row-strip shard exchanges JumpFlood rows between its steps: use rc2dgi_do with a "
                 "communicator, or rc2dgi_do_group");
+  if (int rc = out_buffers(c)) return rc;
   const FramePlan plan = make_plan(c);
   return phase == 1 ? do_phase1(c, plan) : do_phase2(c, plan);
 }
@@ -1595,6 +1630,10 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
         c->CW != cs[0]->CW || c->CH != cs[0]->CH)
       return fail(cs[k], RC2DGI_E_ARG, "rc2dgi_do_group: context k must be shard k of n of one configuration");
   }
+  for (int k = 0; k < n; ++k) {  // (the strip-sized outputs follow the blur settings; before anything is enqueued)
+    HIPCHK(cs[k], hipSetDevice(cs[k]->device));
+    if (int rc = out_buffers(cs[k])) return rc;
+  }
   // a peer may still be copying our previous distRT strip: wait for every peer's last frame
   for (int k = 0; k < n; ++k) {
     HIPCHK(cs[k], hipSetDevice(cs[k]->device));
@@ -1761,8 +1800,13 @@ int rc2dgi_shard_connect(rc2dgi_ctx *c, const void *id, int nbytes) {
 int rc2dgi_device_buffer(rc2dgi_ctx *c, int which, void **dev, int *pitch_bytes) {
   if (!c || !dev || !pitch_bytes) return RC2DGI_E_ARG;
   RC2DGI_USABLE(c);
-  if (which == RC2DGI_RT_FINAL_GI) which = c->final_gi == 2 ? RC2DGI_RT_GI2 : RC2DGI_RT_GI1;
   const int sp = c->sd.pitch, cp = c->cd.pitch;
+  if (which == RC2DGI_RT_FINAL_GI && c->gwin && c->frame_done) {  // a shard's strip-sized copy-back texture
+    *dev = c->gi_spare;
+    *pitch_bytes = cp * (int)gi_bytes(c);
+    return RC2DGI_OK;
+  }
+  if (which == RC2DGI_RT_FINAL_GI) which = c->final_gi == 2 ? RC2DGI_RT_GI2 : RC2DGI_RT_GI1;
   switch (which) {
     case RC2DGI_RT_COLOR: *dev = c->frame_done ? c->color_out : c->color_in; *pitch_bytes = sp * 16; break;
     case RC2DGI_RT_EMISSIVE: *dev = c->emissive; *pitch_bytes = sp * 16; break;
@@ -2162,6 +2206,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
     *value = c->st_last ? 1 : 0;
     return RC2DGI_OK;
   }
+  if (k == "blur_strip_sized") {  // cascadeBlurRT / the copy-back texture hold the own rows (gi_window_apply)
+    *value = c->gwin ? 1 : 0;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_rows") {
     *value = c->jfa_rows;
     return RC2DGI_OK;
@@ -2265,6 +2313,8 @@ int rc2dgi_download_level(rc2dgi_ctx *c, int level, void *host, int pitch_bytes,
 int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int format) {
   if (!c || !host) return fail(c, RC2DGI_E_ARG, "null argument");
   RC2DGI_USABLE(c);
+  // (a shard on strip-sized blur textures: the final GI is the copy-back texture's own rows)
+  const bool win_final = which == RC2DGI_RT_FINAL_GI && c->gwin && c->frame_done;
   if (which == RC2DGI_RT_FINAL_GI) which = (c->N % 2 == 0) ? RC2DGI_RT_GI2 : RC2DGI_RT_GI1;
   if (which < RC2DGI_RT_COLOR || which > RC2DGI_RT_BLUR) return fail(c, RC2DGI_E_ARG, "bad render texture id");
   if (format != RC2DGI_FMT_RGBA32F && format != RC2DGI_FMT_RGBA8) return fail(c, RC2DGI_E_ARG, "bad format");
@@ -2292,12 +2342,15 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
   };
   int rc = RC2DGI_OK;
   const bool n1 = c->N == 1;
+  const int gw0 = c->gwin ? c->ow0 : 0, gw1 = c->gwin ? c->ow1 : c->CH;  // rows cascadeBlurRT / gi_spare hold
+  if (win_final) which = -1;
   switch (which) {
+    case -1: rc = fetch_gi(c, c->gi_spare, img, gi_bytes(c), gw0, gw1); break;
     case RC2DGI_RT_COLOR: rc = c->frame_done ? fetch_out(c->color_out) : fetch4(c->color_in); break;
     case RC2DGI_RT_EMISSIVE: rc = fetch4(c->emissive); break;
     case RC2DGI_RT_TEMP: rc = fetch_out(c->temp); break;
     case RC2DGI_RT_GI1: rc = fetch_gi(c, c->gi1, img, gi_bytes(c)); break;
-    case RC2DGI_RT_BLUR: rc = fetch_gi(c, c->blur, img, rgba8(c) ? 4 : 16); break;  // RGBA8 mode: bytes
+    case RC2DGI_RT_BLUR: rc = fetch_gi(c, c->blur, img, rgba8(c) ? 4 : 16, gw0, gw1); break;  // RGBA8 mode: bytes
     case RC2DGI_RT_GI2:
       if (n1) {  // giRT2 is never drawn with one cascade: ClearAllRTs content
         for (auto &p : img) p = make_float4(0.0f, 0.0f, 0.0f, 1.0f);

@@ -1287,14 +1287,18 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
     const float4 b = blend_over_black(res);  // cascadeBlurRT cleared to (0,0,0,1)
     const float4 g = GI::round(blend(b, h[m][1]));  // copy-back onto finalGI, blended (as stored)
     const int j = by * TR + r0 + t;
-    const size_t o = (size_t)j * c.pitch + i;
-    blur_out[o] = b;
-    GI::st(&gi_out[o], g);
-    if constexpr (MERGE) {  // merge.fs:10-15 + tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
-      // temp / color_out hold rows [m0, m1) (a shard's own rows) and one guard row after them, which takes the
-      // rows outside (unconditional stores: a branch around them doubled the kernel's registers)
+    if constexpr (!MERGE) {
+      const size_t o = (size_t)j * c.pitch + i;
+      blur_out[o] = b;
+      GI::st(&gi_out[o], g);
+    } else {  // merge.fs:10-15 + tempRT -> colorRT copy-back (RC2DGI.cs:389-404)
+      // every output texture (cascadeBlurRT, the copied-back GI, temp, color_out; cascade == screen here, so one
+      // pitch) holds rows [m0, m1) -- a shard's own rows -- and one guard row after them, which takes the rows
+      // outside (unconditional stores: a branch around them doubled the kernel's registers)
       const int jr = (j >= m0 && j < m1) ? j - m0 : m1 - m0;
       const size_t so = (size_t)j * spitch + i, mo = (size_t)jr * spitch + i;
+      blur_out[mo] = b;
+      GI::st(&gi_out[mo], g);
       const float4 col = color_in[so];
       const float4 src =
           make_float4(fminf(col.x + g.x, 1.0f), fminf(col.y + g.y, 1.0f), fminf(col.z + g.z, 1.0f), col.w);

@@ -41,7 +41,7 @@ def _full(R, W, H, N, rr, rs, blur, color, emis):
     ctx.set_shader_value("_BlurRadius", blur)
     ctx.frame(color, emis)
     ctx.sync()
-    out = {k: ctx.download(k) for k in ("color", "temp", "dist", "jump1", "jump2")}
+    out = {k: ctx.download(k) for k in ("color", "temp", "dist", "jump1", "jump2", "blur", "final_gi")}
     ctx.close()
     return out
 
@@ -90,6 +90,15 @@ def test_group_shards_match_whole_frame(R, W, H, N, rr, rs, blur, world, scene):
                 assert mism == 0, f"shard {c.shard_rows()} {k}: {mism} values differ"
             # the whole distance field (all-gathered) -- with strip tables the shards exchange the march field
             # instead, and distRT holds the own rows
+            # cascadeBlurRT and the blurred final GI (cascades the size of the screen): the own rows; on the fused blur + merge
+            # (power-of-two sizes) the shard holds only those (strip-sized textures)
+            if c.cascade_resolution == (W, H) and blur > 0:
+                for k in ("blur", "final_gi"):
+                    got = c.download(k)[y0:y1]
+                    mism = np.count_nonzero(got != want[k][y0:y1])
+                    assert mism == 0, f"shard {c.shard_rows()} {k}: {mism} values differ"
+            pow2 = (W & (W - 1)) == 0 and (H & (H - 1)) == 0
+            assert c.get_tuning("blur_strip_sized") == (pow2 and c.cascade_resolution == (W, H) and 0 < blur < 3)
             st = c.get_tuning("strip_tables_active")
             assert st == (W == H and W >= 4096), (W, H, st)
             d = c.download("dist")
@@ -97,6 +106,37 @@ def test_group_shards_match_whole_frame(R, W, H, N, rr, rs, blur, world, scene):
                 assert np.array_equal(d[y0:y1], want["dist"][y0:y1]), f"shard {c.shard_rows()}: distRT rows"
             else:
                 assert np.array_equal(d, want["dist"]), f"shard {c.shard_rows()}: distRT"
+    for c in ctxs:
+        c.close()
+
+
+def test_shards_follow_blur_changes_between_frames(R):
+    """The strip-sized blur textures (a dyadic radius on the fused blur + merge) are resized before a frame whose
+    blur settings no longer take them (a non-dyadic radius, another blur path, blur off) and back: every frame's
+    colorRT / final GI strips equal the unsharded frame's."""
+    W = H = 256
+    N, world = 4, 2
+    color, emis = _scene("rand:28", W, H)
+    ctxs = []
+    for k in range(world):
+        c = R.RC2DGI(W, H, cascade_count=N, ray_range=2.0)
+        c.set_shard(k, world)
+        c.set_tuning("poison", 1)
+        c.upload("color", color)
+        c.upload("emissive", emis)
+        ctxs.append(c)
+    for blur, path, sized in ((1.5, 0, 1), (1.37, 0, 0), (1.5, 2, 0), (0.0, 0, 0), (2.5, 0, 1)):
+        want = _full(R, W, H, N, 2.0, 1.0, blur, color, emis)
+        for c in ctxs:
+            c.set_shader_value("_BlurRadius", blur)
+            c.set_tuning("blur_path", path)
+        R.do_group(ctxs)
+        for c in ctxs:
+            c.sync()
+            y0, y1 = c.shard_rows()
+            assert c.get_tuning("blur_strip_sized") == sized, (blur, path)
+            for k in ("color", "temp") + (("final_gi",) if blur > 0 else ()):
+                assert np.array_equal(c.download(k)[y0:y1], want[k][y0:y1]), (blur, path, k)
     for c in ctxs:
         c.close()
 
