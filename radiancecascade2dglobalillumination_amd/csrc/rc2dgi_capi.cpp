@@ -149,6 +149,8 @@ struct rc2dgi_ctx {
   int jfa_rt = 1;                // tuning "jfa_rt": rows per lane of the float-path steps on small screens (1, 2, 4)
   int jfa_rows = 0;              // tuning "jfa_rows": consecutive rows per lane in the short steps (0 off, 4, 8)
   int jfa_coset = 2;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
+  int jfa_tail = 0;              // tuning "jfa_tail": the last 2..4 steps in one kernel (k_jfa_tail; 0 off)
+  unsigned *jtail = nullptr;     // J_{S-jfa_tail-1}, which the fused tail reads (it writes both ping-pong textures)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
@@ -285,7 +287,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
-                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes, c->mfield, c->cell_pal, c->shade_list};
+                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes, c->mfield, c->cell_pal, c->shade_list, c->jtail};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -304,6 +306,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->mfield = nullptr;
   c->cell_pal = nullptr;
   c->shade_list = nullptr;
+  c->jtail = nullptr;
   c->built_hitc = c->built_cmin = c->built_dclr = c->built_pal = false;
   c->dboxes = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
@@ -376,6 +379,11 @@ int jfa_buffers(rc2dgi_ctx *c) {
     HIPCHK(c, alloc(&c->jblk[1], sp * br * sizeof(unsigned)));
   }
   return RC2DGI_OK;
+}
+
+// the last jfa_tail JumpFlood steps run as one kernel (k_jfa_tail): whole-frame contexts on the screens it takes
+bool jfa_tail_apply(const rc2dgi_ctx *c) {
+  return c->jfa_tail > 0 && !c->strip && c->world == 1 && jfa_tail_ok(c->sd, c->S, c->jfa_tail);
 }
 
 // exit proofs on for this frame: auto (1) turns them on for large screens only -- at 1200x900 the bound table's
@@ -507,6 +515,7 @@ int prepare_side_buffers(rc2dgi_ctx *c, bool all = false) {
       return hip_fail(c, e, "records pass cell list");
     }
   }
+  if (jfa_tail_apply(c) && !c->jtail) HIPCHK(c, alloc(&c->jtail, (size_t)c->sd.pitch * c->H * sizeof(unsigned)));
   // the record texture (16 B a texel): not held by shards that run with strip tables (their hits derive records)
   const bool st = strip_tables_apply(c);
   if (st && c->shade) {
@@ -990,12 +999,24 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
     int cs = c->jfa_coset ? jfa_coset_steps(c->sd, c->S, lat) : 0;
     for (int q = 0; q < cs; ++q)
       if (!plan.jfa[q].is_full()) cs = 0;
+    // the last nt steps in one kernel (k_jfa_tail), which writes J_{S-2} and J_{S-1} into the two ping-pong textures:
+    // the step before it writes its result into a texture of its own (jtail) instead
+    int nt = jfa_tail_apply(c) && c->jtail ? c->jfa_tail : 0;
+    for (int q = c->S - nt; q < c->S; ++q)
+      if (!plan.jfa[q].is_full()) nt = 0;
+    if (cs > c->S - nt) nt = 0;
+    auto out_of = [&](int q) { return (nt && q == c->S - nt - 1) ? c->jtail : jfa_out(c, q); };
     if (t < cs) {
-      if (t == 0) HIPCHK(c, launch_jfa_coset(c->occ, c->mpitch, jfa_out(c, cs - 1), c->sd, st, lat));
+      if (t == 0) HIPCHK(c, launch_jfa_coset(c->occ, c->mpitch, out_of(cs - 1), c->sd, st, lat));
       return RC2DGI_OK;
     }
-    unsigned *out = jfa_out(c, t);
-    const unsigned *src = t == 0 ? c->occ : jfa_out(c, t - 1);
+    if (nt && t >= c->S - nt) {
+      if (t == c->S - nt)
+        HIPCHK(c, launch_jfa_tail(out_of(t - 1), jfa_out(c, c->S - 1), jfa_out(c, c->S - 2), c->dist, c->sd, c->S, nt, st));
+      return RC2DGI_OK;
+    }
+    unsigned *out = out_of(t);
+    const unsigned *src = t == 0 ? c->occ : out_of(t - 1);
     for (auto &r : plan.jfa[t].iv)
       HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, out, dist, c->sd, ox, oy, st,
                                 r.first, r.second, nullptr, 0, c->jfa_lds, c->jfa_rt, c->jfa_rows));
@@ -2063,6 +2084,11 @@ int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_wgproof = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "jfa_tail") {
+    if (value < 0 || value == 1 || value > 4) return fail(c, RC2DGI_E_ARG, "jfa_tail is 0 (off) or 2..4 steps");
+    c->jfa_tail = value;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_coset") {
     if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "jfa_coset is 0 (off), 1 (4 steps), 2 (5 steps)");
     c->jfa_coset = value;
@@ -2216,6 +2242,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "jfa_rt") {
     *value = c->jfa_rt;
+    return RC2DGI_OK;
+  }
+  if (k == "jfa_tail") {
+    *value = c->jfa_tail;
     return RC2DGI_OK;
   }
   if (k == "jfa_coset") {

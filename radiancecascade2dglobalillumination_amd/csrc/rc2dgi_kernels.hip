@@ -1538,6 +1538,157 @@ hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, Scr
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- JumpFlood: the last steps in one kernel
+// One step of k_jfa_tail: offset D texels, from `in` (the tile grown by 2D - 1 texels, the ring the later steps
+// still need plus this step's reach) to `out` (grown by D - 1).  Texel (lx, ly) of `out` is screen texel
+// (x0 - (D - 1) + lx, y0 - (D - 1) + ly) wrapped (REPEAT); its taps sit at in columns lx, lx + D, lx + 2D.
+template <int D, int T, int NTHR>
+__device__ __forceinline__ void jfa_tail_step(const unsigned *in, unsigned *out, int x0, int y0, unsigned mw,
+                                              unsigned mh, const JfaTaps &o) {
+  constexpr int RO = D - 1, WI = T + 2 * (2 * D - 1), WO = T + 2 * RO, NO = WO * WO;
+  constexpr int NIT = (NO + NTHR - 1) / NTHR, NP = 2;  // texels per thread, taken NP at a time (their LDS reads overlap)
+#pragma unroll
+  for (int it = 0; it < NIT; it += NP) {
+    unsigned sd[NP][9], here[NP];
+    int kk[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      kk[p] = (int)threadIdx.x + (it + p) * NTHR;
+      const int k = min(kk[p], NO - 1);  // (past the end: a valid texel, not stored)
+      const int ly = k / WO, lx = k - ly * WO;
+#pragma unroll
+      for (int y = 0; y < 3; ++y)
+#pragma unroll
+        for (int x = 0; x < 3; ++x) sd[p][y * 3 + x] = in[(ly + y * D) * WI + lx + x * D];
+      here[p] = pack_seed((int)((unsigned)(x0 - RO + lx) & mw), (int)((unsigned)(y0 - RO + ly) & mh));
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      float key;
+      const unsigned b = jfa_best9<true>(sd[p], here[p], o, &key);
+      if (it + p < NIT && kk[p] < NO) out[kk[p]] = b;
+    }
+  }
+}
+
+// The last NT JumpFlood steps (offsets 2^(NT-1) .. 2, 1 texels) of a square power-of-two screen up to 4096 (integer
+// keys) in one kernel.  A workgroup loads a T x T tile of J_{S-NT-1} grown by the 2^NT - 1 texels the steps reach
+// (rows and columns wrap) into LDS once, runs the steps there -- the step of offset d on the tile grown by d - 1,
+// the ring the later steps still read -- and writes its tile of J_{S-1} with the DistanceField, and of J_{S-2} (the
+// centre tap of the last step): the two JumpFlood textures a frame leaves visible.  Same taps, keys and selection
+// (jfa_best9) as k_jfa_p2: the same seeds and distances.  Per texel one 4-byte read (plus the ring, mostly from L2)
+// and 10 bytes written, where NT separate steps read and write 4 bytes each per step; the grown tiles cost
+// 1.19 x the texel-steps at NT = 4, T = 64.  XCD-contiguous tile order (neighbours share their rings in one L2).
+template <int NT, int T, int NTHR>
+__global__ __launch_bounds__(NTHR) void k_jfa_tail(const unsigned *__restrict__ src, unsigned *__restrict__ dst,
+                                                   unsigned *__restrict__ dst_prev, unsigned short *__restrict__ dist,
+                                                   ScreenDims s, JfaTaps o) {
+  static_assert(NT >= 2 && NT <= 4, "two to four fused steps");
+  constexpr int W0 = T + 2 * ((1 << NT) - 1), W1 = T + 2 * ((1 << (NT - 1)) - 1);
+  __shared__ unsigned bufA[W0 * W0];
+  __shared__ unsigned bufB[W1 * W1];
+  const int gx = (int)gridDim.x, n = gx * (int)gridDim.y;
+  const int l = xcd_logical_id((int)(blockIdx.y * gridDim.x + blockIdx.x), n);
+  const int x0 = (l % gx) * T, y0 = (l / gx) * T;
+  const unsigned mw = (unsigned)s.W - 1u, mh = (unsigned)s.H - 1u;
+  constexpr int R0 = (1 << NT) - 1, N0 = W0 * W0, NL = (N0 + NTHR - 1) / NTHR;
+  {  // every load issued before the first LDS store
+    unsigned v[NL];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      const int k = min((int)threadIdx.x + q * NTHR, N0 - 1);
+      const int ly = k / W0, lx = k - ly * W0;
+      v[q] = src[((unsigned)(y0 - R0 + ly) & mh) * (unsigned)s.pitch + ((unsigned)(x0 - R0 + lx) & mw)];
+    }
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      const int k = (int)threadIdx.x + q * NTHR;
+      if (k < N0) bufA[k] = v[q];
+    }
+  }
+  __syncthreads();
+  if constexpr (NT == 4) {
+    jfa_tail_step<8, T, NTHR>(bufA, bufB, x0, y0, mw, mh, o);
+    __syncthreads();
+    jfa_tail_step<4, T, NTHR>(bufB, bufA, x0, y0, mw, mh, o);
+    __syncthreads();
+    jfa_tail_step<2, T, NTHR>(bufA, bufB, x0, y0, mw, mh, o);
+  } else if constexpr (NT == 3) {
+    jfa_tail_step<4, T, NTHR>(bufA, bufB, x0, y0, mw, mh, o);
+    __syncthreads();
+    jfa_tail_step<2, T, NTHR>(bufB, bufA, x0, y0, mw, mh, o);
+  } else {
+    jfa_tail_step<2, T, NTHR>(bufA, bufB, x0, y0, mw, mh, o);
+  }
+  __syncthreads();
+  const unsigned *in = NT == 3 ? bufA : bufB;  // J_{S-2} on the tile grown by 1
+  constexpr int WI = T + 2, NIT = T * T / NTHR;
+  static_assert(T * T % (2 * NTHR) == 0, "whole pairs of texels per thread");
+#pragma unroll
+  for (int it = 0; it < NIT; it += 2) {
+    unsigned sd[2][9];
+    int i[2], j[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int k = (int)threadIdx.x + (it + p) * NTHR, ly = k / T, lx = k - ly * T;
+#pragma unroll
+      for (int y = 0; y < 3; ++y)
+#pragma unroll
+        for (int x = 0; x < 3; ++x) sd[p][y * 3 + x] = in[(ly + y) * WI + lx + x];
+      i[p] = x0 + lx;
+      j[p] = y0 + ly;
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      float key;
+      const unsigned best = jfa_best9<true>(sd[p], pack_seed(i[p], j[p]), o, &key);
+      const unsigned g = (unsigned)j[p] * (unsigned)s.pitch + (unsigned)i[p];
+      dst[g] = best;
+      dst_prev[g] = sd[p][4];
+      dist[g] = jfa_dist_q(best, key, i[p], j[p], s, o);  // DistanceField.fs
+    }
+  }
+}
+
+constexpr int kJfaTailT = 64, kJfaTailThreads = 512;
+
+bool jfa_tail_ok(ScreenDims s, int S, int nt) {
+  if (nt < 2 || nt > 4 || s.u8 || !(s.powW && s.powH) || s.W != s.H || s.W > 4096 || s.W < kJfaTailT ||
+      s.W % kJfaTailT != 0 || S < nt + 1)
+    return false;
+  for (int t = S - nt; t < S; ++t) {  // offsets 2^(nt-1) .. 1 texels, both axes, in the shader's tap order
+    float ox[3], oy[3];
+    jfa_offsets(s.W, s.H, t, ox, oy);
+    JfaTaps tp;
+    if (!jfa_p2_taps(s, ox, oy, &tp)) return false;
+    const int d = 1 << (S - 1 - t);
+    if (tp.dx[0] != -d || tp.dx[1] != 0 || tp.dx[2] != d || tp.dy[0] != -d || tp.dy[1] != 0 || tp.dy[2] != d) return false;
+  }
+  return true;
+}
+
+hipError_t launch_jfa_tail(const unsigned *src, unsigned *dst, unsigned *dst_prev, unsigned short *dist, ScreenDims s,
+                           int S, int nt, hipStream_t st) {
+  if (!jfa_tail_ok(s, S, nt) || !src || !dst || !dst_prev || !dist || src == dst || src == dst_prev)
+    return hipErrorInvalidValue;
+  float ox[3] = {-1.0f, 0.0f, 1.0f}, oy[3] = {-1.0f, 0.0f, 1.0f};
+  for (int k = 0; k < 3; ++k) {
+    ox[k] /= (float)s.W;
+    oy[k] /= (float)s.H;
+  }
+  JfaTaps tp;  // (the key scale, dinit and 1 / max(W, H): the same for every step)
+  if (!jfa_p2_taps(s, ox, oy, &tp)) return hipErrorInvalidValue;
+  const dim3 grid(s.W / kJfaTailT, s.H / kJfaTailT);
+  constexpr int T = kJfaTailT, NTHR = kJfaTailThreads;
+  if (nt == 4)
+    hipLaunchKernelGGL((k_jfa_tail<4, T, NTHR>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);
+  else if (nt == 3)
+    hipLaunchKernelGGL((k_jfa_tail<3, T, NTHR>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);
+  else
+    hipLaunchKernelGGL((k_jfa_tail<2, T, NTHR>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);
+  return hipGetLastError();
+}
+
 RcMapCache::~RcMapCache() { clear(); }
 
 void RcMapCache::retain(const std::vector<int> &codes) {

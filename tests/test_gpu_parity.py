@@ -599,6 +599,38 @@ def test_jfa_rows_short_steps_are_bit_identical(RC2DGI, W, H, N, storage, scene)
     ctx.close()
 
 
+@pytest.mark.parametrize("W,H,N,storage", [(64, 64, 3, "f32"), (128, 128, 3, "f32"), (256, 256, 4, "f32"),
+                                           (1024, 1024, 5, "f32"), (4096, 4096, 6, "f32"), (512, 256, 4, "f32"),
+                                           (512, 512, 4, "rgba8"), (8192, 8192, 8, "f32")])
+@pytest.mark.parametrize("scene", ["demo", "rand:62", "empty", "full"])
+def test_jfa_tail_steps_are_bit_identical(RC2DGI, W, H, N, storage, scene):
+    """The last two to four JumpFlood steps in one kernel (tuning jfa_tail: k_jfa_tail, the tile and the ring the
+    steps reach staged in LDS once, J_{S-2} / J_{S-1} / the distance field written) leave the same jumpRT1 / jumpRT2,
+    distance field and frame as the per-step kernels, with poisoned intermediates, over two frames; on an empty
+    screen (no seed anywhere) and a full one (every texel a seed) too.  Screens it does not take (non-square, RGBA8,
+    above 4096) are unchanged."""
+    color, emis = make_scene(scene, W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for nt in (0, 2, 3, 4):
+        ctx.set_tuning("jfa_tail", nt)
+        assert ctx.get_tuning("jfa_tail") == nt
+        ctx.set_tuning("poison", 1)
+        for _ in range(2):
+            ctx.do_rc2dgi()
+        ctx.sync()
+        out[nt] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
+    for nt in (2, 3, 4):
+        for k in out[0]:
+            assert np.array_equal(out[0][k].view(np.uint8), out[nt][k].view(np.uint8)), \
+                f"jfa_tail {nt} {k}: {np.count_nonzero(out[0][k] != out[nt][k])}"
+    with pytest.raises(Exception):
+        ctx.set_tuning("jfa_tail", 1)
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,N,storage", [(256, 256, 4, "f32"), (512, 512, 4, "f32"), (1024, 1024, 5, "f32"),
                                            (512, 256, 4, "f32"), (512, 512, 4, "rgba8"), (4096, 4096, 6, "f32"),
                                            (8192, 8192, 8, "f32")])
