@@ -385,7 +385,8 @@ def bench_strips(a, rank, local, world):
     units = CW * CH * N * a.steps  # one frame per step, whatever the shard count
     cfg_line = {"rc_variant": [ctxs[0].get_tuning(f"rc_variant_L{L}") for L in range(N)],
                 "strip_tables": tuning_or_none(ctxs[0], "strip_tables_active"),
-                "blur_strip_sized": tuning_or_none(ctxs[0], "blur_strip_sized")}
+                "blur_strip_sized": tuning_or_none(ctxs[0], "blur_strip_sized"),
+                "cascade_banded": tuning_or_none(ctxs[0], "cascade_banded")}
     for g in ctxs:
         g.close()
     mem = {"device_bytes_per_shard": int(shard_bytes)}

@@ -192,10 +192,15 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *   "rc_chain_spin"   diagnostic: polls per chain wait (0: the default bound; -1: every wait times out at once)
  *   "jfa_rows"        0 (default), 4, 8: the short isotropic JumpFlood steps (offsets 1, 2, 4 on square power-of-two
  *                     screens) with that many consecutive rows per lane, each tap row loaded once (measured no faster)
+ *   "cascade_band"    1 (default): row-strip shards on strip tables and the fused blur + merge band GI1 / GI2 (see
+ *                     rc2dgi_device_buffer); 0: whole textures
+ *   "jfa_tail"        0 (default), 2, 3, 4: the last that many JumpFlood steps in one LDS-tiled kernel (square
+ *                     power-of-two screens up to 4096; measured slower than the separate steps)
  *   "strip_tables"    1 (default; f32 storage): row-strip shards build the march's side tables for their own cell rows and exchange
  *                     them with the march field instead of all-gathering distRT; no record texture (see the sharding
  *                     section below); get_tuning "strip_tables_active" tells whether the last frame did
  * rc2dgi_get_tuning also answers "blur_strip_sized" (1: a shard's BLUR / FINAL_GI textures hold its own rows,
+ * rc2dgi_device_buffer), "cascade_banded" (1: a shard's GI1 / GI2 hold its band of every direction block,
  * rc2dgi_device_buffer), "rc_variant_count" and "rc_chain_timeouts" (workgroups of the chained
  * frames since the chain was set up that stopped waiting for their upper tiles: 0 in a correct run;
  * synchronises). */
@@ -273,7 +278,10 @@ int rc2dgi_do_group(rc2dgi_ctx **ctxs, int n);
  * frame, FINAL_GI when the blur runs fused with the merge (power-of-two cascades the size of the screen, a dyadic
  * _BlurRadius below 3, blur_path 0, no LINUX_MERGE flag): the blurred copy-back then stays in a strip-sized texture
  * of its own, and GI1 / GI2 keep the cascade's unblurred level 0 (rc2dgi_download of FINAL_GI / BLUR: the own
- * rows, the others NaN).  These textures are resized before a frame when the blur settings change. */
+ * rows, the others NaN).  With strip tables on top of that (f32, no variant 25, no rc_chain or kept levels) GI1 / GI2
+ * are banded: the texture of level L holds, for each of its 2^L block rows in turn, the block-local probe rows the
+ * shard computes (one cyclic range per level, rc2dgi_plan_rows), so it is a fraction of CW x CH; rc2dgi_download maps
+ * the band back (other rows NaN).  These textures are resized before a frame when the blur settings change. */
 int rc2dgi_device_buffer(rc2dgi_ctx *ctx, int which, void **dev, int *pitch_bytes);
 
 /* host-only planner (no device needed): the rows a shard computes for one pass.

@@ -168,6 +168,11 @@ struct rc2dgi_ctx {
   bool gwin = false;     // cascadeBlurRT and the blur's copy-back texture (gi_spare) hold rows [ow0, ow1) too
                          // (a shard on the fused blur + merge, gi_window_apply); the copy-back then stays in
                          // gi_spare (no buffer swap) and is the frame's final GI
+  bool gband = false;    // giRT1 / giRT2 banded (gi_band_apply): level L's texture holds, per block row, the gbn[L]
+                         // block-local rows from gb0[L] on (cyclically) -- the rows the shard's plan computes
+  std::vector<int> gb0, gbn;
+  size_t gi_rows[2] = {0, 0};  // rows giRT1 / giRT2 hold (CH when whole)
+  int cascade_band = 1;        // tuning "cascade_band": band giRT1 / giRT2 where gi_band_apply allows (0: whole)
   ncclComm_t comm = nullptr;
   hipEvent_t ev_phase1 = nullptr;   // end of phase 1 (group exchange)
   hipEvent_t ev_frame = nullptr;    // end of the last group frame (peers copy from our distRT)
@@ -421,6 +426,75 @@ bool gi_window_apply(const rc2dgi_ctx *c) {
          !c->linux_merge && blur_rows_plan(c->cd, c->blur_radius, &bt) >= 0;
 }
 
+FramePlan make_plan(const rc2dgi_ctx *c);
+
+// Banded cascade textures (row-strip shards with strip tables on the fused blur + merge, f32, no top-level variant
+// 25, no chain or kept levels): a level's rows the shard computes are a band of every direction block
+// (RadianceCascades.fs:131-139 keeps the taps block-local), so giRT1 / giRT2 hold only those bands (k_rc_level's RD
+// marches and k_blur_rows map a row to its band row).
+bool gi_band_apply(const rc2dgi_ctx *c) {
+  if (!c->cascade_band || !gi_window_apply(c) || !strip_tables_apply(c) || c->keep_levels || chain_active(c))
+    return false;
+  if (c->storage != RC2DGI_STORAGE_F32) return false;
+  for (int v : c->rc_variant)
+    if (v == 25) return false;
+  return true;
+}
+
+// the shortest cyclic range of rows holding every row of r: first row, rows (0 rows: r is empty)
+void circ_band(const RowSet &r, int &b0, int &bn) {
+  b0 = bn = 0;
+  const int m = (int)r.iv.size();
+  if (m == 0) return;
+  int gap = -1, k0 = 0;
+  for (int k = 0; k < m; ++k) {  // the largest gap between consecutive intervals (cyclically) is left out
+    const int nx = k + 1 < m ? r.iv[k + 1].first : r.iv[0].first + r.n;
+    if (nx - r.iv[k].second > gap) {
+      gap = nx - r.iv[k].second;
+      k0 = k;
+    }
+  }
+  b0 = r.iv[(k0 + 1) % m].first;
+  bn = r.n - gap;
+}
+
+// giRT1 / giRT2 for this frame's plan: the bands of the levels each one receives (level L: giRT1 when N-1-L is even,
+// phase2_levels), or whole.  Before anything of the frame is enqueued (out_buffers).
+int gi_buffers(rc2dgi_ctx *c) {
+  const bool gb = gi_band_apply(c);
+  std::vector<int> b0(c->N, 0), bn(c->N, 0);
+  size_t rows[2] = {(size_t)c->CH, (size_t)c->CH};
+  if (gb) {
+    const FramePlan plan = make_plan(c);
+    rows[0] = rows[1] = 1;
+    for (int L = 0; L < c->N; ++L) {
+      circ_band(plan.level[L], b0[L], bn[L]);
+      if (bn[L] <= 0) bn[L] = 1;  // (a level the shard computes no row of: one dummy row per block)
+      size_t &r = rows[(c->N - 1 - L) & 1];
+      r = std::max(r, (size_t)bn[L] << L);
+    }
+  }
+  c->gb0 = b0;
+  c->gbn = bn;
+  if (c->gi1 && c->gi2 && gb == c->gband && rows[0] == c->gi_rows[0] && rows[1] == c->gi_rows[1]) {
+    c->gband = gb;
+    return RC2DGI_OK;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (float4 **b : {&c->gi1, &c->gi2}) {
+    if (*b) HIPCHK(c, hipFree(*b));
+    *b = nullptr;
+  }
+  c->gi_rows[0] = c->gi_rows[1] = 0;
+  c->gband = false;
+  HIPCHK(c, alloc(&c->gi1, rows[0] * c->cd.pitch * gi_bytes(c)));
+  HIPCHK(c, alloc(&c->gi2, rows[1] * c->cd.pitch * gi_bytes(c)));
+  c->gi_rows[0] = rows[0];
+  c->gi_rows[1] = rows[1];
+  c->gband = gb;
+  return RC2DGI_OK;
+}
+
 // tempRT and the merged colorRT of a row-strip shard hold its own rows only (the merge writes nothing else; the
 // kernels take the window's first row, launch_blur_rows / launch_merge m0): 2 x 16 B a texel of the strip instead of
 // the screen; on the fused blur + merge (gi_window_apply) cascadeBlurRT and the copy-back texture too.  Unsharded:
@@ -430,6 +504,7 @@ int out_buffers(rc2dgi_ctx *c) {
   int y0 = 0, y1 = c->H;
   if (c->world > 1) strip_rows(c->H, c->rank, c->world, y0, y1);
   const bool gw = gi_window_apply(c);
+  if (int rc = gi_buffers(c)) return rc;
   if (c->temp && c->color_out && c->blur && c->gi_spare && y0 == c->ow0 && y1 == c->ow1 && gw == c->gwin)
     return RC2DGI_OK;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -566,6 +641,8 @@ int allocate(rc2dgi_ctx *c) {
   const size_t gsz = gi_bytes(c);  // giRT1 / giRT2 texel size (storage)
   HIPCHK(c, alloc(&c->gi1, nc * gsz));
   HIPCHK(c, alloc(&c->gi2, nc * gsz));
+  c->gi_rows[0] = c->gi_rows[1] = (size_t)c->CH;
+  c->gband = false;
   HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->gi_spare, nc * gsz));
   HIPCHK(c, alloc(&c->dirs, dir_table_len(c->N) * sizeof(float2)));
@@ -1058,7 +1135,8 @@ int phase1_begin(rc2dgi_ctx *c, const FramePlan &plan) {
     HIPCHK(c, hipMemsetAsync(c->temp, 0xFF, nw * 16, st));
     HIPCHK(c, hipMemsetAsync(c->color_out, 0xFF, nw * 16, st));
     const size_t nb = c->gwin ? (size_t)c->cd.pitch * (size_t)(c->ow1 - c->ow0) : nc;  // (cascadeBlurRT, spare)
-    for (float4 *b : {c->gi1, c->gi2}) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * gi_bytes(c), st));
+    for (int b = 0; b < 2; ++b)
+      HIPCHK(c, hipMemsetAsync(b ? c->gi2 : c->gi1, 0xFF, c->gi_rows[b] * c->cd.pitch * gi_bytes(c), st));
     HIPCHK(c, hipMemsetAsync(c->gi_spare, 0xFF, nb * gi_bytes(c), st));
     for (float4 *b : c->chain_bufs)
       if (b) HIPCHK(c, hipMemsetAsync(b, 0xFF, nc * 16, st));
@@ -1308,6 +1386,15 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
+    if (c->gband) {  // banded cascade textures (gi_buffers)
+      if (!f.st) return fail(c, RC2DGI_E_STATE, "banded cascade textures without strip tables");
+      a.out_b0 = c->gb0[L];
+      a.out_bn = c->gbn[L];
+      if (L + 1 < c->N) {
+        a.up_b0 = c->gb0[L + 1];
+        a.up_bn = c->gbn[L + 1];
+      }
+    }
 
     if (chain && (L < c->N - 1 || c->rc_chain == 4)) {
       chain_args.push_back(a);  // (whole levels: one process; rc_chain 4: the top level in the launch too)
@@ -1355,7 +1442,8 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
       bool ok = true;
       for (auto &r : plan.blur.iv)
         ok = ok && launch_blur_rows(finalGI, c->blur, c->gi_spare, c->cd, c->blur_radius, c->color_in, c->temp,
-                                    c->color_out, c->sd, mrg, st, r.first, r.second, c->ow0, c->ow1);
+                                    c->color_out, c->sd, mrg, st, r.first, r.second, c->ow0, c->ow1,
+                                    c->gband ? c->gb0[0] : 0, c->gband ? c->gbn[0] : 0);
       if (!ok && plan.blur.iv.size() > 1) return fail(c, RC2DGI_E_HIP, "fixed-tap blur refused a row interval");
       fused = ok;
       merged = ok && mrg;
@@ -2084,6 +2172,11 @@ int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value) {
     c->rc_wgproof = value != 0;
     return RC2DGI_OK;
   }
+  if (k == "cascade_band") {
+    if (value != 0 && value != 1) return fail(c, RC2DGI_E_ARG, "cascade_band is 0 or 1");
+    c->cascade_band = value;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_tail") {
     if (value < 0 || value == 1 || value > 4) return fail(c, RC2DGI_E_ARG, "jfa_tail is 0 (off) or 2..4 steps");
     c->jfa_tail = value;
@@ -2236,12 +2329,20 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
     *value = c->gwin ? 1 : 0;
     return RC2DGI_OK;
   }
+  if (k == "cascade_banded") {  // giRT1 / giRT2 hold the shard's band of every direction block (gi_band_apply)
+    *value = c->gband ? 1 : 0;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_rows") {
     *value = c->jfa_rows;
     return RC2DGI_OK;
   }
   if (k == "jfa_rt") {
     *value = c->jfa_rt;
+    return RC2DGI_OK;
+  }
+  if (k == "cascade_band") {
+    *value = c->cascade_band;
     return RC2DGI_OK;
   }
   if (k == "jfa_tail") {
@@ -2373,19 +2474,38 @@ int rc2dgi_download(rc2dgi_ctx *c, int which, void *host, int pitch_bytes, int f
   int rc = RC2DGI_OK;
   const bool n1 = c->N == 1;
   const int gw0 = c->gwin ? c->ow0 : 0, gw1 = c->gwin ? c->ow1 : c->CH;  // rows cascadeBlurRT / gi_spare hold
+  // a banded giRT1 / giRT2 (gi_buffers): the band rows of the lowest level it received, the other rows NaN
+  auto fetch_band = [&](const float4 *src, int b) -> int {
+    int L = -1;
+    for (int l = c->N - 1; l >= 0; --l)
+      if (((c->N - 1 - l) & 1) == b) L = l;
+    std::memset(img.data(), 0xFF, img.size() * sizeof(float4));
+    if (L < 0) return RC2DGI_OK;
+    const int bh = c->CH >> L, b0 = c->gb0[L], bn = c->gbn[L];
+    for (int by = 0; by < (1 << L); ++by) {
+      const int n1 = std::min(bn, bh - b0);  // band rows b0 .. bh - 1, then 0 .. (the cyclic rest)
+      const float4 *row = src + (size_t)by * bn * c->cd.pitch;
+      HIPCHK(c, hipMemcpy2D(img.data() + (size_t)(by * bh + b0) * w, (size_t)w * 16, row, (size_t)pitch * 16,
+                            (size_t)w * 16, n1, hipMemcpyDeviceToHost));
+      if (bn > n1)
+        HIPCHK(c, hipMemcpy2D(img.data() + (size_t)(by * bh) * w, (size_t)w * 16, row + (size_t)n1 * c->cd.pitch,
+                              (size_t)pitch * 16, (size_t)w * 16, bn - n1, hipMemcpyDeviceToHost));
+    }
+    return RC2DGI_OK;
+  };
   if (win_final) which = -1;
   switch (which) {
     case -1: rc = fetch_gi(c, c->gi_spare, img, gi_bytes(c), gw0, gw1); break;
     case RC2DGI_RT_COLOR: rc = c->frame_done ? fetch_out(c->color_out) : fetch4(c->color_in); break;
     case RC2DGI_RT_EMISSIVE: rc = fetch4(c->emissive); break;
     case RC2DGI_RT_TEMP: rc = fetch_out(c->temp); break;
-    case RC2DGI_RT_GI1: rc = fetch_gi(c, c->gi1, img, gi_bytes(c)); break;
+    case RC2DGI_RT_GI1: rc = c->gband ? fetch_band(c->gi1, 0) : fetch_gi(c, c->gi1, img, gi_bytes(c)); break;
     case RC2DGI_RT_BLUR: rc = fetch_gi(c, c->blur, img, rgba8(c) ? 4 : 16, gw0, gw1); break;  // RGBA8 mode: bytes
     case RC2DGI_RT_GI2:
       if (n1) {  // giRT2 is never drawn with one cascade: ClearAllRTs content
         for (auto &p : img) p = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
       } else {
-        rc = fetch_gi(c, c->gi2, img, gi_bytes(c));
+        rc = c->gband ? fetch_band(c->gi2, 1) : fetch_gi(c, c->gi2, img, gi_bytes(c));
       }
       break;
     case RC2DGI_RT_JUMP1:

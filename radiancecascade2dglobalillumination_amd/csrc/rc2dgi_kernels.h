@@ -133,6 +133,9 @@ struct RcLevelArgs {
   int wg_proof = 1;             // workgroup-wide exit proof of the first samples (needs cmin)
   const float4 *rec_color = nullptr, *rec_emis = nullptr;  // hit records derived from colorRT / emissiveRT instead
                                                           // of read from `shade` (row-strip shards, strip tables)
+  // banded cascade textures (with rec_color only): `out` holds, per block row, out_bn block-local rows from out_b0 on
+  // (cyclically), `upper` up_bn rows from up_b0 on; 0 rows: the whole texture
+  int out_b0 = 0, out_bn = 0, up_b0 = 0, up_bn = 0;
 };
 
 // The cascade chain (rc2dgi_rc_chain.hip, tuning rc_chain): the levels a[0 .. n) (consecutive, downwards; a[0]
@@ -266,10 +269,11 @@ bool launch_blur_fused(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Ca
 // radius / sizes do not allow it (see k_blur_rows).  blur_rows_plan: F = floor(radius) or -1.
 int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt);
 // (merge outputs: temp / color_out hold screen rows [m0, m1) from their row 0 -- a row-strip shard's own rows; m1 = -1:
-// every row -- and one guard row after those, which receives the merge of every row outside them)
+// every row -- and one guard row after those, which receives the merge of every row outside them; gi_in holds the
+// gn cascade rows from g0 on, cyclically -- a shard's banded level 0; gn <= 0: every row)
 bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
                       const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
-                      hipStream_t st, int row0 = 0, int row1 = -1, int m0 = 0, int m1 = -1);
+                      hipStream_t st, int row0 = 0, int row1 = -1, int m0 = 0, int m1 = -1, int g0 = 0, int gn = 0);
 
 // merge.fs into temp, then tempRT -> colorRT copy-back (RC2DGI.cs:389-404); linux_merge: raylib's default
 // shader in place of merge.fs (RC2DGI_FLAG_LINUX_MERGE_FALLBACK)

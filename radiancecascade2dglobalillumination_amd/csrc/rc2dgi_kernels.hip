@@ -1230,7 +1230,8 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
                                                    float4 *__restrict__ blur_out, typename GI::T *__restrict__ gi_out,
                                                    CascadeDims c, BlurTaps bt,
                                                    const float4 *__restrict__ color_in, float4 *__restrict__ temp,
-                                                   float4 *__restrict__ color_out, int spitch, int tile0, int m0, int m1) {
+                                                   float4 *__restrict__ color_out, int spitch, int tile0, int m0, int m1,
+                                                   int g0, int gn) {
   constexpr int RPT = RC2DGI_BLUR_RPT, TR = 4 * RPT;  // rows per thread, rows per tile
   constexpr int HALO = F + 1, TW = 64 + 2 * HALO, TH = TR + 2 * HALO, NR = RPT + 2 * HALO;
   __shared__ float4 tile[TH * TW];
@@ -1238,7 +1239,9 @@ __global__ __launch_bounds__(256) void k_blur_rows(const typename GI::T *__restr
   const int x0 = blockIdx.x * 64 - HALO, y0 = by * TR - HALO;
   for (int k = threadIdx.x; k < TW * TH; k += 256) {
     const int ty = k / TW, tx = k - ty * TW;
-    const int gx = (x0 + tx) & (c.CW - 1), gy = (y0 + ty) & (c.CH - 1);
+    // gi_in holds rows [g0, g0 + gn) cyclically (a row-strip shard's banded level 0; else g0 0, gn CH): the band
+    // row, rows past the band read its last row (only for texels the launch does not store)
+    const int gx = (x0 + tx) & (c.CW - 1), gy = min((y0 + ty - g0) & (c.CH - 1), gn - 1);
     tile[k] = GI::ld(&gi_in[(size_t)gy * c.pitch + gx]);
   }
   __syncthreads();
@@ -1872,11 +1875,18 @@ RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c) {
   P.t0 = ((float)start / (float)maxValue) * a.ray_range;
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
+  P.ob0 = a.out_b0;
+  P.obn = a.out_bn;
+  P.ub0 = a.up_b0;
+  P.ubn = a.up_bn;
   return P;
 }
 
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st) {
   const RcParams P = rc_level_params(a, s, c);
+  // banded cascade textures: the derived-record marches only (launch_rc_tiles, P.rcol), never the top-level variant
+  if ((a.out_bn > 0 || a.up_bn > 0) && (!a.rec_color || a.variant == 25 || c.gi_u8 || c.gi_f16))
+    return hipErrorInvalidValue;
   hipError_t e;
   if (a.variant == 25)
     e = launch_rc_top(a, P, st);  // the barrier-free top level (any storage; elsewhere variant 13)
@@ -1958,9 +1968,13 @@ int blur_rows_plan(CascadeDims c, float radius, BlurTaps *bt) {
 
 bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, CascadeDims c, float radius,
                       const float4 *color_in, float4 *temp, float4 *color_out, ScreenDims s, bool merge,
-                      hipStream_t st, int row0, int row1, int m0, int m1) {
+                      hipStream_t st, int row0, int row1, int m0, int m1, int g0, int gn) {
   BlurTaps bt;
   if (m1 < 0) m1 = s.H;
+  if (gn <= 0) {
+    g0 = 0;
+    gn = c.CH;
+  }
   const int F = blur_rows_plan(c, radius, &bt);
   if (F < 0) return false;
   if (merge && !(s.W == c.CW && s.H == c.CH)) return false;
@@ -1974,10 +1988,10 @@ bool launch_blur_rows(const float4 *gi_in, float4 *blur_out, float4 *gi_out, Cas
     if (c.gi_f16)                                                                                              \
       hipLaunchKernelGGL((k_blur_rows<FV, MV, GiF16>), grid, dim3(256), 0, st,                                 \
                          reinterpret_cast<const GiF16::T *>(gi_in), blur_out, reinterpret_cast<GiF16::T *>(gi_out), \
-                         c, bt, color_in, temp, color_out, s.pitch, t0, m0, m1);                                \
+                         c, bt, color_in, temp, color_out, s.pitch, t0, m0, m1, g0, gn);                        \
     else                                                                                                       \
       hipLaunchKernelGGL((k_blur_rows<FV, MV, GiF32>), grid, dim3(256), 0, st, gi_in, blur_out, gi_out, c, bt,  \
-                         color_in, temp, color_out, s.pitch, t0, m0, m1);                                       \
+                         color_in, temp, color_out, s.pitch, t0, m0, m1, g0, gn);                               \
   } while (0)
   if (merge) {
     if (F == 0) RC2DGI_BLUR_ROWS(0, true); else if (F == 1) RC2DGI_BLUR_ROWS(1, true); else RC2DGI_BLUR_ROWS(2, true);

@@ -39,6 +39,8 @@ struct RcParams {
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
+  int ob0, obn, ub0, ubn;     // banded G_L / G_{L+1} (RD only; row-strip shards): a level's texture holds, per block
+                              // row, the obn (ubn) block-local rows from ob0 (ub0) on, cyclically; 0 rows: whole
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
   unsigned long long *stats;  // diagnostic builds: [16 levels][16] counters (rc2dgi_diag_stats)
 #endif
@@ -659,6 +661,7 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
 
   // upper block of angleIndex a = 4*bi + r: (a mod 2b, a div 2b) in blocks of (bdx/2, bdy/2)
   const int ubx = P.bdx >> 1, uby = P.bdy >> 1;
+  const int ulg = RDR ? __builtin_ctz((unsigned)max(uby, 1)) : 0;  // (banded G_{L+1}: log2 of its block height)
   const int umask = 2 * P.bsc - 1, ushift = P.level + 1;
   // staged texels as plain 32-bit components (HIP's vector unions defeat SROA -> scratch); raw
   // storage bits, converted when written to LDS after the march
@@ -702,7 +705,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
             gx = gx < 0 ? gx + P.c.CW : (gx >= P.c.CW ? gx - P.c.CW : gx);
             gy = gy < 0 ? gy + P.c.CH : (gy >= P.c.CH ? gy - P.c.CH : gy);
           }
-          const unsigned off = __umul24((unsigned)gy, (unsigned)P.c.pitch) + (unsigned)gx;
+          unsigned grow = (unsigned)gy;
+          if constexpr (RDR) {  // banded G_{L+1}: the block's band row (footprint rows past the band: its last row,
+                                // read only for probes the launch does not store)
+            if (P.ubn > 0)
+              grow = (unsigned)((gy >> ulg) * P.ubn + min((gy - P.ub0) & (uby - 1), P.ubn - 1));
+          }
+          const unsigned off = __umul24(grow, (unsigned)P.c.pitch) + (unsigned)gx;
           typename GI::T v;  // issued now, consumed after the march
           if constexpr (CH)
             v = ld_sc1(upper, off);
@@ -1299,7 +1308,11 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) voi
         acc = make_float4(axy.x, axy.y, azw.x, azw.y);
       }
       const int blkx = bi & (P.bsc - 1), blky = bi >> P.level;
-      const int i = blkx * P.bdx + cx, j = blky * P.bdy + cy;  // pixelIndex
+      const int i = blkx * P.bdx + cx;  // pixelIndex
+      int j = blky * P.bdy + cy;
+      if constexpr (RDR) {  // banded G_L: the block's band row
+        if (P.obn > 0) j = blky * P.obn + ((cy - P.ob0) & (P.bdy - 1));
+      }
       if constexpr (CH)
         st_sc1(out, (unsigned)(j * P.c.pitch + i), GI::blend_black(acc));
       else

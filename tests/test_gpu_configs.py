@@ -318,7 +318,7 @@ def test_c3_8192_eight_row_strips(R, c3_whole):
         R.do_group(shards)
     for g in shards:
         g.sync()
-        assert g.get_tuning("strip_tables_active") == 1
+        assert g.get_tuning("strip_tables_active") == 1 and g.get_tuning("cascade_banded") == 1
         y0, y1 = g.shard_rows()
         c, t = g.download("color"), g.download("temp")
         assert np.array_equal(c[y0:y1], w["color_out"][y0:y1]), f"C3 shard rows {y0}:{y1} colorRT"

@@ -101,6 +101,8 @@ def test_group_shards_match_whole_frame(R, W, H, N, rr, rs, blur, world, scene):
             assert c.get_tuning("blur_strip_sized") == (pow2 and c.cascade_resolution == (W, H) and 0 < blur < 3)
             st = c.get_tuning("strip_tables_active")
             assert st == (W == H and W >= 4096), (W, H, st)
+            # strip tables on the fused blur + merge: giRT1 / giRT2 hold the shard's band of every direction block
+            assert c.get_tuning("cascade_banded") == (st and blur > 0), (W, H, blur)
             d = c.download("dist")
             if st:
                 assert np.array_equal(d[y0:y1], want["dist"][y0:y1]), f"shard {c.shard_rows()}: distRT rows"
