@@ -411,10 +411,11 @@ __device__ __forceinline__ void st_sc1(float4 *base, unsigned off, float4 v) {
 // holds texels of a tile it did not wait for.  A poll gives up after kChainSpin tries (counted in the error word):
 // a broken assumption shows as wrong results, never as a hung GPU.
 // RD: hit records derived from colorRT / emissiveRT (P.rcol; row-strip shards with strip tables) -- its own
-// instantiations, since the derivation's registers and code cost the other marches ~1 % (profiles/r06/ab/rdr.txt)
+// instantiations, since the derivation's registers and code cost the other marches ~1 %; with the
+// banded textures' row map they get seven waves per SIMD's registers (at eight they spilled)
 template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false, bool CH = false,
           bool RD = false>
-__global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
+__global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 : 8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
                                                      const float4 *__restrict__ shade,
