@@ -194,6 +194,8 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     screens) with that many consecutive rows per lane, each tap row loaded once (measured no faster)
  *   "cascade_band"    1 (default): row-strip shards on strip tables and the fused blur + merge band GI1 / GI2 (see
  *                     rc2dgi_device_buffer); 0: whole textures
+ *   "jfa_tab"         1 (default): the float-path JumpFlood steps (non-power-of-two screens, W + H <= 8192) read every
+ *                     fragTexCoord from a per-context table of (i + 0.5) / n instead of dividing per tap; 0: divide
  *   "jfa_tail"        0 (default), 2, 3, 4: the last that many JumpFlood steps in one LDS-tiled kernel (square
  *                     power-of-two screens up to 4096; measured slower than the separate steps)
  *   "strip_tables"    1 (default; f32 storage): row-strip shards build the march's side tables for their own cell rows and exchange

@@ -151,6 +151,8 @@ struct rc2dgi_ctx {
   int jfa_coset = 2;             // tuning "jfa_coset": the first four (1) or five (2) steps in one kernel (k_jfa_coset)
   int jfa_tail = 0;              // tuning "jfa_tail": the last 2..4 steps in one kernel (k_jfa_tail; 0 off)
   unsigned *jtail = nullptr;     // J_{S-jfa_tail-1}, which the fused tail reads (it writes both ping-pong textures)
+  float *tc = nullptr;           // texcoords of the W columns and H rows (tc_table) for the float-path JumpFlood
+  int jfa_tab = 1;               // tuning "jfa_tab": the float-path steps read texcoords from tc (0: divide per tap)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
@@ -292,7 +294,8 @@ void free_buffers(rc2dgi_ctx *c) {
   c->paint_buf.release();
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
-                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes, c->mfield, c->cell_pal, c->shade_list, c->jtail};
+                  c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes, c->mfield, c->cell_pal, c->shade_list, c->jtail,
+                  c->tc};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -312,6 +315,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->cell_pal = nullptr;
   c->shade_list = nullptr;
   c->jtail = nullptr;
+  c->tc = nullptr;
   c->built_hitc = c->built_cmin = c->built_dclr = c->built_pal = false;
   c->dboxes = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
@@ -645,6 +649,12 @@ int allocate(rc2dgi_ctx *c) {
   c->gband = false;
   HIPCHK(c, alloc(&c->blur, nc * sizeof(float4)));
   HIPCHK(c, alloc(&c->gi_spare, nc * gsz));
+  {  // texcoord table of the float-path JumpFlood (non-power-of-two screens)
+    std::vector<float> t((size_t)c->W + c->H);
+    tc_table(c->W, c->H, t.data());
+    HIPCHK(c, alloc(&c->tc, t.size() * sizeof(float)));
+    HIPCHK(c, hipMemcpy(c->tc, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   HIPCHK(c, alloc(&c->dirs, dir_table_len(c->N) * sizeof(float2)));
   HIPCHK(c, alloc(&c->dexit, dir_table_len(c->N) * sizeof(float4)));
   HIPCHK(c, alloc(&c->sky, ((size_t)4 << (2 * (c->N - 1))) * sizeof(float4)));
@@ -1096,7 +1106,8 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
     const unsigned *src = t == 0 ? c->occ : out_of(t - 1);
     for (auto &r : plan.jfa[t].iv)
       HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, out, dist, c->sd, ox, oy, st,
-                                r.first, r.second, nullptr, 0, c->jfa_lds, c->jfa_rt, c->jfa_rows));
+                                r.first, r.second, nullptr, 0, c->jfa_lds, c->jfa_rt, c->jfa_rows,
+                                c->jfa_tab ? c->tc : nullptr));
     return RC2DGI_OK;
   }
   // row-strip shard: the own strip, into its window (global row y0 - m = local row 0)
@@ -1104,7 +1115,8 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
   strip_rows(c->H, c->rank, c->world, y0, y1);
   const int wrow0 = y0 - c->jx.m;
   if (t == 0) {
-    HIPCHK(c, launch_jfa_step(true, c->occ, c->mpitch, jfa_out(c, 0), dist, c->sd, ox, oy, st, y0, y1, nullptr, wrow0));
+    HIPCHK(c, launch_jfa_step(true, c->occ, c->mpitch, jfa_out(c, 0), dist, c->sd, ox, oy, st, y0, y1, nullptr, wrow0,
+                              0, 1, 0, c->jfa_tab ? c->tc : nullptr));
     return RC2DGI_OK;
   }
   int buf[3], row0[3];
@@ -1115,7 +1127,8 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
     win.base[y] = buf[y] == 0 ? jfa_out(c, t - 1) : c->jblk[buf[y] - 1];
     win.row0[y] = row0[y];
   }
-  HIPCHK(c, launch_jfa_step(false, nullptr, c->sd.pitch, jfa_out(c, t), dist, c->sd, ox, oy, st, y0, y1, &win, wrow0));
+  HIPCHK(c, launch_jfa_step(false, nullptr, c->sd.pitch, jfa_out(c, t), dist, c->sd, ox, oy, st, y0, y1, &win, wrow0,
+                            0, 1, 0, c->jfa_tab ? c->tc : nullptr));
   return RC2DGI_OK;
 }
 
@@ -2177,6 +2190,11 @@ int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value) {
     c->cascade_band = value;
     return RC2DGI_OK;
   }
+  if (k == "jfa_tab") {
+    if (value != 0 && value != 1) return fail(c, RC2DGI_E_ARG, "jfa_tab is 0 or 1");
+    c->jfa_tab = value;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_tail") {
     if (value < 0 || value == 1 || value > 4) return fail(c, RC2DGI_E_ARG, "jfa_tail is 0 (off) or 2..4 steps");
     c->jfa_tail = value;
@@ -2343,6 +2361,10 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "cascade_band") {
     *value = c->cascade_band;
+    return RC2DGI_OK;
+  }
+  if (k == "jfa_tab") {
+    *value = c->jfa_tab;
     return RC2DGI_OK;
   }
   if (k == "jfa_tail") {

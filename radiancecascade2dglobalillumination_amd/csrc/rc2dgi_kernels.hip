@@ -107,16 +107,27 @@ constexpr int JT = 4;
 
 // RT: rows per lane (JT on large screens; 1 on small ones, where 4 rows per lane left about one wave per SIMD:
 // 1200 x 900 = 1083 workgroups, each step a few exposed round trips)
-template <bool FIRST, bool U8, int RT = JT>
+// TAB (non-power-of-two screens with W + H <= kTcTabMax): every fragTexCoord the step needs -- the texel's, each
+// tap seed's -- read from a table of the W column and H row texcoords ((i + 0.5) / n, the same correctly rounded
+// division, made once per context: tc_table) staged in LDS, instead of two IEEE divisions per tap.
+constexpr int kTcTabMax = 8192;
+template <bool FIRST, bool U8, int RT = JT, bool TAB = false>
 __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ src, int src_pitch,
                                                   unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                   ScreenDims s, JfaOffsets o, int row0, int row1, JfaSrc win,
-                                                  int dst_row0) {
+                                                  int dst_row0, const float *__restrict__ tc) {
+  extern __shared__ float s_tc[];  // (TAB: W column texcoords, then H row texcoords)
+  if constexpr (TAB) {
+    for (int k = (int)threadIdx.x; k < s.W + s.H; k += 256) s_tc[k] = tc[k];
+    __syncthreads();
+  }
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j0 = row0 + blockIdx.y * (4 * RT) + (threadIdx.x >> 6);
   if (i >= s.W) return;
   const Axis ax{s.W, s.powW}, ay{s.H, s.powH};
-  const float u = texcoord(i, ax);
+  auto tcx = [&](int q) { return TAB ? s_tc[q] : texcoord(q, ax); };
+  auto tcy = [&](int q) { return TAB ? s_tc[s.W + q] : texcoord(q, ay); };
+  const float u = tcx(i);
   int ti[3];
 #pragma unroll
   for (int x = 0; x < 3; ++x) ti[x] = wrap_nearest(u + o.ox[x], ax);
@@ -124,7 +135,7 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const int j = min(j0 + 4 * t, row1 - 1);  // clamped rows are computed but not stored
-    const float v = texcoord(j, ay);
+    const float v = tcy(j);
 #pragma unroll
     for (int y = 0; y < 3; ++y) {
       const int tj = wrap_nearest(v + o.oy[y], ay);
@@ -150,15 +161,15 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
   for (int t = 0; t < RT; ++t) {
     const int j = j0 + 4 * t;
     if (j >= row1) break;
-    const float v = texcoord(j, ay);
+    const float v = tcy(j);
     float minDist = 1.0f, bx = 0.0f, by = 0.0f;
     unsigned best = U8 ? 0u : kNoSeed;
 #pragma unroll
     for (int k = 0; k < 9; ++k) {  // y outer, x inner: the first of equal distances wins
       const unsigned sd = seed[t][k];
       if (U8 ? seed_u8_ok(sd) : sd != kNoSeed) {  // peek.x != 0 && peek.y != 0 (f32: a seed's uv is never 0)
-        const float px = U8 ? (float)(sd & 0xFFFFu) * kInv255 : texcoord((int)(sd & 0xFFFFu), ax);
-        const float py = U8 ? (float)(sd >> 16) * kInv255 : texcoord((int)(sd >> 16), ay);
+        const float px = U8 ? (float)(sd & 0xFFFFu) * kInv255 : tcx((int)(sd & 0xFFFFu));
+        const float py = U8 ? (float)(sd >> 16) * kInv255 : tcy((int)(sd >> 16));
         const float dx = px - u, dy = py - v;
         const float d = dx * dx + dy * dy;
         if (d < minDist) {
@@ -1387,7 +1398,8 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
 
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0,
-                           int row1, const JfaSrc *window, int dst_row0, int lds, int small_rt, int jrows) {
+                           int row1, const JfaSrc *window, int dst_row0, int lds, int small_rt, int jrows,
+                           const float *tc) {
   JfaSrc win{};
   if (window && !first) win = *window;
   if (row1 < 0 || row1 > s.H) row1 = s.H;
@@ -1442,21 +1454,21 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   } else if (s.u8) {  // RGBA8 jumpRT: quantized seed uv, the float path
     if (small && rt2) {
       if (first)
-        hipLaunchKernelGGL((k_jfa_step<true, true, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
+        hipLaunchKernelGGL((k_jfa_step<true, true, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0, nullptr);
       else
         hipLaunchKernelGGL((k_jfa_step<false, true, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
-                           row1, win, dst_row0);
+                           row1, win, dst_row0, nullptr);
     } else if (small) {
       if (first)
-        hipLaunchKernelGGL((k_jfa_step<true, true, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
+        hipLaunchKernelGGL((k_jfa_step<true, true, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0, nullptr);
       else
         hipLaunchKernelGGL((k_jfa_step<false, true, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
-                           row1, win, dst_row0);
+                           row1, win, dst_row0, nullptr);
     } else if (first) {
-      hipLaunchKernelGGL((k_jfa_step<true, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
+      hipLaunchKernelGGL((k_jfa_step<true, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0, nullptr);
     } else {
       hipLaunchKernelGGL((k_jfa_step<false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
-                         row1, win, dst_row0);
+                         row1, win, dst_row0, nullptr);
     }
   } else if (p2 && lds && !first && !win.on && tp.dx[2] == tp.dy[2] && tp.dy[2] >= 1 && tp.dy[2] <= kJfaLdsMax &&
              (row1 - row0) % (4 * JT) == 0 && s.W % 64 == 0) {
@@ -1478,25 +1490,34 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
       if (ikey) RC2DGI_JFA(false, true); else RC2DGI_JFA(false, false);
     }
 #undef RC2DGI_JFA
-  } else if (small && rt2) {
-    if (first)
-      hipLaunchKernelGGL((k_jfa_step<true, false, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
-    else
-      hipLaunchKernelGGL((k_jfa_step<false, false, 2>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
-                         row1, win, dst_row0);
-  } else if (small) {
-    if (first)
-      hipLaunchKernelGGL((k_jfa_step<true, false, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
-    else
-      hipLaunchKernelGGL((k_jfa_step<false, false, 1>), grid1, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
-                         row1, win, dst_row0);
-  } else if (first) {
-    hipLaunchKernelGGL((k_jfa_step<true, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, row1, win, dst_row0);
   } else {
-    hipLaunchKernelGGL((k_jfa_step<false, false>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0,
-                       row1, win, dst_row0);
+    // the float path: texcoords from the context's table where it has one (k_jfa_step TAB)
+    const bool tab = tc && s.W + s.H <= kTcTabMax;
+    const size_t lds = tab ? (size_t)(s.W + s.H) * sizeof(float) : 0;
+#define RC2DGI_JFA_F(G, FV, RV)                                                                                     \
+  do {                                                                                                            \
+    if (tab)                                                                                                      \
+      hipLaunchKernelGGL((k_jfa_step<FV, false, RV, true>), G, dim3(256), lds, st, src, src_pitch, dst, dist, s, o, \
+                         row0, row1, win, dst_row0, tc);                                                          \
+    else                                                                                                          \
+      hipLaunchKernelGGL((k_jfa_step<FV, false, RV>), G, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, \
+                         row1, win, dst_row0, nullptr);                                                           \
+  } while (0)
+    if (small && rt2) {
+      if (first) RC2DGI_JFA_F(grid1, true, 2); else RC2DGI_JFA_F(grid1, false, 2);
+    } else if (small) {
+      if (first) RC2DGI_JFA_F(grid1, true, 1); else RC2DGI_JFA_F(grid1, false, 1);
+    } else {
+      if (first) RC2DGI_JFA_F(grid, true, JT); else RC2DGI_JFA_F(grid, false, JT);
+    }
+#undef RC2DGI_JFA_F
   }
   return hipGetLastError();
+}
+
+void tc_table(int W, int H, float *out) {
+  for (int i = 0; i < W; ++i) out[i] = ((float)i + 0.5f) / (float)W;  // (IEEE division: texcoord's, bit for bit)
+  for (int j = 0; j < H; ++j) out[W + j] = ((float)j + 0.5f) / (float)H;
 }
 
 int jfa_coset_steps(ScreenDims s, int S, int lat) {
