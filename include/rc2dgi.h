@@ -197,7 +197,7 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *   "jfa_tab"         1 (default): the float-path JumpFlood steps (non-power-of-two screens, W + H <= 8192) read every
  *                     fragTexCoord from a per-context table of (i + 0.5) / n instead of dividing per tap; 0: divide
  *   "jfa_tail"        0 (default), 2, 3, 4: the last that many JumpFlood steps in one LDS-tiled kernel (square
- *                     power-of-two screens up to 4096; measured slower than the separate steps)
+ *                     power-of-two screens up to 16384)
  *   "strip_tables"    1 (default; f32 storage): row-strip shards build the march's side tables for their own cell rows and exchange
  *                     them with the march field instead of all-gathering distRT; no record texture (see the sharding
  *                     section below); get_tuning "strip_tables_active" tells whether the last frame did

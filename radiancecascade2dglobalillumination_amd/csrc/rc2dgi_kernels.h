@@ -74,7 +74,7 @@ bool jfa_p2_taps(ScreenDims s, const float off_x[3], const float off_y[3], JfaTa
 // 512 texels or more), else 0.  launch_jfa_coset reads the ScreenUV mask and writes J_3.
 // (lat 16: steps 0-3 in one kernel; lat 32: steps 0-4)
 int jfa_coset_steps(ScreenDims s, int S, int lat = 16);
-// the last nt (2..4) JumpFlood steps in one kernel (k_jfa_tail): square power-of-two screens up to 4096 whose last
+// the last nt (2..4) JumpFlood steps in one kernel (k_jfa_tail): square power-of-two screens up to 16384 whose last
 // steps tap +-2^(nt-1) .. +-1 texels.  Reads J_{S-nt-1} from src (which must be neither output), writes J_{S-1} to
 // dst, J_{S-2} to dst_prev and the DistanceField.
 bool jfa_tail_ok(ScreenDims s, int S, int nt);

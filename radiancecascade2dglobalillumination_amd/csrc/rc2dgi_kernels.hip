@@ -203,12 +203,36 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
 //     subtract and one clamped 16-bit dot product per tap, compared as integers.
 //   otherwise: the packed 16-bit difference converted (exact: |si - i| < 2^15; the no-seed value
 //     0x8000 wraps to the same magnitude), scaled, squared and added in fp32 as the shader rounds.
+//   hybrid (KM 2; W == H, 4096 < W <= 16384): the integer keys first.  When their minimum m is below 2^24, every
+//     tap that can win has an integer key below 2^24 -- exact in fp32, so its float key equals it -- and every
+//     other tap's float key is >= 2^24 (rounding never leaves the binade), so the integer argmin (first of
+//     equal) is the shader's; m < 2^24 <= dinit is a seed.  Otherwise (the nearest candidate 4096 texels or
+//     more away) the lane takes the float keys.
 // A key >= dinit = mx^2 loses to the initial minDist (kNoSeed's is >= 2^28 >= dinit).  *key: the
 // winner's key as a float; sqrt(*key) / mx is its distance (DistanceField.fs) to the bit, the same
-// power-of-two argument.
-template <bool IKEY>
+// power-of-two argument.  KM: 0 float keys, 1 integer keys (IKEY), 2 hybrid.
+template <int KM>
 __device__ __forceinline__ unsigned jfa_best9(const unsigned sd[9], unsigned here, const JfaTaps &o, float *key) {
   typedef short v2s __attribute__((ext_vector_type(2)));
+  if constexpr (KM == 2) {
+    unsigned kb[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const v2s d = __builtin_bit_cast(v2s, sd[k]) - __builtin_bit_cast(v2s, here);
+      kb[k] = (unsigned)__builtin_amdgcn_sdot2(d, d, 0, true);
+    }
+    const unsigned m =
+        min(min(min(kb[0], kb[1]), min(kb[2], kb[3])), min(min(kb[4], kb[5]), min(min(kb[6], kb[7]), kb[8])));
+    if (m < (1u << 24)) {
+      unsigned best = sd[8];
+#pragma unroll
+      for (int k = 7; k >= 0; --k) best = kb[k] == m ? sd[k] : best;
+      *key = (float)m;
+      return best;
+    }
+    return jfa_best9<0>(sd, here, o, key);
+  }
+  constexpr bool IKEY = KM == 1;
   unsigned kb[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
@@ -259,7 +283,7 @@ __host__ __device__ __forceinline__ int xcd_logical_id(int p, int n) {
 // an s-texel ring of the previous step in LDS (each texel loaded once, rows wrapped), then reads the
 // 9 taps of every texel from LDS (tuning "jfa_lds"; same seeds, same bits).
 constexpr int kJfaLdsMax = 8;
-template <bool FIRST, bool IKEY, bool U8 = false, bool LDS = false>
+template <bool FIRST, int IKEY, bool U8 = false, bool LDS = false>  // (IKEY: the key mode of jfa_best9)
 __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src, int src_pitch,
                                                 unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                 ScreenDims s, JfaTaps o, int row0, int row1, int lattice,
@@ -396,7 +420,7 @@ __global__ __launch_bounds__(256) void k_jfa_p2(const unsigned *__restrict__ src
 // the JR + 2 S rows j0 - S .. j0 + JR - 1 + S, each loaded once (3 (JR + 2 S) loads for JR texels: S = 1 at JR = 8
 // issues 30 tap loads where k_jfa_p2 issues 72).  Same taps, scan order, keys and selection (jfa_best9) as
 // k_jfa_p2, so the same seeds and distances.  Tuning "jfa_rows" (0: off).
-template <int S, int JR, bool IKEY>
+template <int S, int JR, int IKEY>
 __global__ __launch_bounds__(256) void k_jfa_rows(const unsigned *__restrict__ src, int src_pitch,
                                                   unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                   ScreenDims s, JfaTaps o, int row0, int row1) {
@@ -454,7 +478,7 @@ struct CosetGeo {
 // threads: one per (segment a, texel u) and all (LAT 16) or half (LAT 32) of the lattice rows (the float keys
 // spill a few row coordinates at 128 VGPRs; splitting the rows over two threads to avoid it measured slower at
 // 8192^2: 0.72 vs 0.58 ms)
-template <bool IKEY, int LAT>
+template <int IKEY, int LAT>
 __global__ __launch_bounds__(CosetGeo<LAT>::NTHR) __attribute__((amdgpu_waves_per_eu(4))) void k_jfa_coset(
     const unsigned *__restrict__ mask, int mpitch, unsigned *__restrict__ dst, ScreenDims s, JfaTaps o) {
   using G = CosetGeo<LAT>;
@@ -1480,14 +1504,15 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
       hipLaunchKernelGGL((k_jfa_p2<false, false, false, true>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s,
                          tp, row0, row1, 0, win, dst_row0);
   } else if (p2) {
-    const bool ikey = s.W == s.H && s.W <= 4096;
+    // key mode (jfa_best9): integer keys on square screens up to 4096, hybrid up to 16384, else float
+    const int km = s.W == s.H ? (s.W <= 4096 ? 1 : (s.W <= 16384 ? 2 : 0)) : 0;
 #define RC2DGI_JFA(F, K)                                                                                      \
   hipLaunchKernelGGL((k_jfa_p2<F, K>), grid, dim3(256), 0, st, src, src_pitch, dst, dist, s, tp, row0, row1, \
                      lattice, win, dst_row0)
     if (first) {
-      if (ikey) RC2DGI_JFA(true, true); else RC2DGI_JFA(true, false);
+      if (km == 1) RC2DGI_JFA(true, 1); else if (km == 2) RC2DGI_JFA(true, 2); else RC2DGI_JFA(true, 0);
     } else {
-      if (ikey) RC2DGI_JFA(false, true); else RC2DGI_JFA(false, false);
+      if (km == 1) RC2DGI_JFA(false, 1); else if (km == 2) RC2DGI_JFA(false, 2); else RC2DGI_JFA(false, 0);
     }
 #undef RC2DGI_JFA
   } else {
@@ -1545,19 +1570,21 @@ hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, Scr
   }
   JfaTaps tp;
   if (!jfa_p2_taps(s, ox, oy, &tp)) return hipErrorInvalidValue;
-#define RC2DGI_COSET(L)                                                                                           \
+  // key mode: integer up to 4096 (lattice 32 runs there only), hybrid above (jfa_coset_steps: square, <= 16384)
+#define RC2DGI_COSET(L, K)                                                                                        \
   do {                                                                                                            \
     const int g = s.W / L;                                                                                        \
     const dim3 grid((g / CosetGeo<L>::SEG) * g);                                                                  \
-    if (s.W <= 4096)                                                                                              \
-      hipLaunchKernelGGL((k_jfa_coset<true, L>), grid, dim3(CosetGeo<L>::NTHR), 0, st, mask, mpitch, dst, s, tp);  \
-    else                                                                                                          \
-      hipLaunchKernelGGL((k_jfa_coset<false, L>), grid, dim3(CosetGeo<L>::NTHR), 0, st, mask, mpitch, dst, s, tp); \
+    hipLaunchKernelGGL((k_jfa_coset<K, L>), grid, dim3(CosetGeo<L>::NTHR), 0, st, mask, mpitch, dst, s, tp);       \
   } while (0)
-  if (lat == 32)
-    RC2DGI_COSET(32);
-  else
-    RC2DGI_COSET(16);
+  if (lat == 32) {
+    if (s.W > 4096) return hipErrorInvalidValue;
+    RC2DGI_COSET(32, 1);
+  } else if (s.W <= 4096) {
+    RC2DGI_COSET(16, 1);
+  } else {
+    RC2DGI_COSET(16, 2);
+  }
 #undef RC2DGI_COSET
   return hipGetLastError();
 }
@@ -1566,7 +1593,7 @@ hipError_t launch_jfa_coset(const unsigned *mask, int mpitch, unsigned *dst, Scr
 // One step of k_jfa_tail: offset D texels, from `in` (the tile grown by 2D - 1 texels, the ring the later steps
 // still need plus this step's reach) to `out` (grown by D - 1).  Texel (lx, ly) of `out` is screen texel
 // (x0 - (D - 1) + lx, y0 - (D - 1) + ly) wrapped (REPEAT); its taps sit at in columns lx, lx + D, lx + 2D.
-template <int D, int T, int NTHR>
+template <int D, int T, int NTHR, int KM>
 __device__ __forceinline__ void jfa_tail_step(const unsigned *in, unsigned *out, int x0, int y0, unsigned mw,
                                               unsigned mh, const JfaTaps &o) {
   constexpr int RO = D - 1, WI = T + 2 * (2 * D - 1), WO = T + 2 * RO, NO = WO * WO;
@@ -1589,21 +1616,21 @@ __device__ __forceinline__ void jfa_tail_step(const unsigned *in, unsigned *out,
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       float key;
-      const unsigned b = jfa_best9<true>(sd[p], here[p], o, &key);
+      const unsigned b = jfa_best9<KM>(sd[p], here[p], o, &key);
       if (it + p < NIT && kk[p] < NO) out[kk[p]] = b;
     }
   }
 }
 
-// The last NT JumpFlood steps (offsets 2^(NT-1) .. 2, 1 texels) of a square power-of-two screen up to 4096 (integer
-// keys) in one kernel.  A workgroup loads a T x T tile of J_{S-NT-1} grown by the 2^NT - 1 texels the steps reach
+// The last NT JumpFlood steps (offsets 2^(NT-1) .. 2, 1 texels) of a square power-of-two screen up to 16384 (integer
+// keys up to 4096, hybrid above) in one kernel.  A workgroup loads a T x T tile of J_{S-NT-1} grown by the 2^NT - 1 texels the steps reach
 // (rows and columns wrap) into LDS once, runs the steps there -- the step of offset d on the tile grown by d - 1,
 // the ring the later steps still read -- and writes its tile of J_{S-1} with the DistanceField, and of J_{S-2} (the
 // centre tap of the last step): the two JumpFlood textures a frame leaves visible.  Same taps, keys and selection
 // (jfa_best9) as k_jfa_p2: the same seeds and distances.  Per texel one 4-byte read (plus the ring, mostly from L2)
 // and 10 bytes written, where NT separate steps read and write 4 bytes each per step; the grown tiles cost
 // 1.19 x the texel-steps at NT = 4, T = 64.  XCD-contiguous tile order (neighbours share their rings in one L2).
-template <int NT, int T, int NTHR>
+template <int NT, int T, int NTHR, int KM>  // (KM: the key mode of jfa_best9, integer or hybrid)
 __global__ __launch_bounds__(NTHR) void k_jfa_tail(const unsigned *__restrict__ src, unsigned *__restrict__ dst,
                                                    unsigned *__restrict__ dst_prev, unsigned short *__restrict__ dist,
                                                    ScreenDims s, JfaTaps o) {
@@ -1632,17 +1659,17 @@ __global__ __launch_bounds__(NTHR) void k_jfa_tail(const unsigned *__restrict__ 
   }
   __syncthreads();
   if constexpr (NT == 4) {
-    jfa_tail_step<8, T, NTHR>(bufA, bufB, x0, y0, mw, mh, o);
+    jfa_tail_step<8, T, NTHR, KM>(bufA, bufB, x0, y0, mw, mh, o);
     __syncthreads();
-    jfa_tail_step<4, T, NTHR>(bufB, bufA, x0, y0, mw, mh, o);
+    jfa_tail_step<4, T, NTHR, KM>(bufB, bufA, x0, y0, mw, mh, o);
     __syncthreads();
-    jfa_tail_step<2, T, NTHR>(bufA, bufB, x0, y0, mw, mh, o);
+    jfa_tail_step<2, T, NTHR, KM>(bufA, bufB, x0, y0, mw, mh, o);
   } else if constexpr (NT == 3) {
-    jfa_tail_step<4, T, NTHR>(bufA, bufB, x0, y0, mw, mh, o);
+    jfa_tail_step<4, T, NTHR, KM>(bufA, bufB, x0, y0, mw, mh, o);
     __syncthreads();
-    jfa_tail_step<2, T, NTHR>(bufB, bufA, x0, y0, mw, mh, o);
+    jfa_tail_step<2, T, NTHR, KM>(bufB, bufA, x0, y0, mw, mh, o);
   } else {
-    jfa_tail_step<2, T, NTHR>(bufA, bufB, x0, y0, mw, mh, o);
+    jfa_tail_step<2, T, NTHR, KM>(bufA, bufB, x0, y0, mw, mh, o);
   }
   __syncthreads();
   const unsigned *in = NT == 3 ? bufA : bufB;  // J_{S-2} on the tile grown by 1
@@ -1665,7 +1692,7 @@ __global__ __launch_bounds__(NTHR) void k_jfa_tail(const unsigned *__restrict__ 
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       float key;
-      const unsigned best = jfa_best9<true>(sd[p], pack_seed(i[p], j[p]), o, &key);
+      const unsigned best = jfa_best9<KM>(sd[p], pack_seed(i[p], j[p]), o, &key);
       const unsigned g = (unsigned)j[p] * (unsigned)s.pitch + (unsigned)i[p];
       dst[g] = best;
       dst_prev[g] = sd[p][4];
@@ -1677,7 +1704,7 @@ __global__ __launch_bounds__(NTHR) void k_jfa_tail(const unsigned *__restrict__ 
 constexpr int kJfaTailT = 64, kJfaTailThreads = 512;
 
 bool jfa_tail_ok(ScreenDims s, int S, int nt) {
-  if (nt < 2 || nt > 4 || s.u8 || !(s.powW && s.powH) || s.W != s.H || s.W > 4096 || s.W < kJfaTailT ||
+  if (nt < 2 || nt > 4 || s.u8 || !(s.powW && s.powH) || s.W != s.H || s.W > 16384 || s.W < kJfaTailT ||
       s.W % kJfaTailT != 0 || S < nt + 1)
     return false;
   for (int t = S - nt; t < S; ++t) {  // offsets 2^(nt-1) .. 1 texels, both axes, in the shader's tap order
@@ -1704,12 +1731,17 @@ hipError_t launch_jfa_tail(const unsigned *src, unsigned *dst, unsigned *dst_pre
   if (!jfa_p2_taps(s, ox, oy, &tp)) return hipErrorInvalidValue;
   const dim3 grid(s.W / kJfaTailT, s.H / kJfaTailT);
   constexpr int T = kJfaTailT, NTHR = kJfaTailThreads;
-  if (nt == 4)
-    hipLaunchKernelGGL((k_jfa_tail<4, T, NTHR>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);
-  else if (nt == 3)
-    hipLaunchKernelGGL((k_jfa_tail<3, T, NTHR>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);
-  else
-    hipLaunchKernelGGL((k_jfa_tail<2, T, NTHR>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);
+#define RC2DGI_TAIL(K)                                                                                           \
+  do {                                                                                                           \
+    if (nt == 4)                                                                                                 \
+      hipLaunchKernelGGL((k_jfa_tail<4, T, NTHR, K>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);  \
+    else if (nt == 3)                                                                                            \
+      hipLaunchKernelGGL((k_jfa_tail<3, T, NTHR, K>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);  \
+    else                                                                                                         \
+      hipLaunchKernelGGL((k_jfa_tail<2, T, NTHR, K>), grid, dim3(NTHR), 0, st, src, dst, dst_prev, dist, s, tp);  \
+  } while (0)
+  if (s.W <= 4096) RC2DGI_TAIL(1); else RC2DGI_TAIL(2);  // integer keys, hybrid above 4096 (jfa_best9)
+#undef RC2DGI_TAIL
   return hipGetLastError();
 }
 

@@ -632,8 +632,8 @@ def test_jfa_tail_steps_are_bit_identical(RC2DGI, W, H, N, storage, scene):
     """The last two to four JumpFlood steps in one kernel (tuning jfa_tail: k_jfa_tail, the tile and the ring the
     steps reach staged in LDS once, J_{S-2} / J_{S-1} / the distance field written) leave the same jumpRT1 / jumpRT2,
     distance field and frame as the per-step kernels, with poisoned intermediates, over two frames; on an empty
-    screen (no seed anywhere) and a full one (every texel a seed) too.  Screens it does not take (non-square, RGBA8,
-    above 4096) are unchanged."""
+    screen (no seed anywhere) and a full one (every texel a seed) too; 8192^2 takes the hybrid keys.  Screens it does
+    not take (non-square, RGBA8) are unchanged."""
     color, emis = make_scene(scene, W, H)
     ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0, storage=storage)
     ctx.upload("color", color)
