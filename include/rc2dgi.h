@@ -194,8 +194,9 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     screens) with that many consecutive rows per lane, each tap row loaded once (measured no faster)
  *   "cascade_band"    1 (default): row-strip shards on strip tables and the fused blur + merge band GI1 / GI2 (see
  *                     rc2dgi_device_buffer); 0: whole textures
- *   "jfa_tab"         1 (default): the float-path JumpFlood steps (non-power-of-two screens, W + H <= 8192) read every
- *                     fragTexCoord from a per-context table of (i + 0.5) / n instead of dividing per tap; 0: divide
+ *   "jfa_tab"         the float-path JumpFlood steps' fragTexCoords (i + 0.5) / n: 2 (default) x * (1/n) plus one
+ *                     fused correction, used where the context proved it equal to the division for every index (else
+ *                     as 1); 1 from a per-context table (W + H <= 8192); 0 divided per tap
  *   "jfa_tail"        0 (default), 2, 3, 4: the last that many JumpFlood steps in one LDS-tiled kernel (square
  *                     power-of-two screens up to 16384)
  *   "strip_tables"    1 (default; f32 storage): row-strip shards build the march's side tables for their own cell rows and exchange

@@ -152,7 +152,9 @@ struct rc2dgi_ctx {
   int jfa_tail = 0;              // tuning "jfa_tail": the last 2..4 steps in one kernel (k_jfa_tail; 0 off)
   unsigned *jtail = nullptr;     // J_{S-jfa_tail-1}, which the fused tail reads (it writes both ping-pong textures)
   float *tc = nullptr;           // texcoords of the W columns and H rows (tc_table) for the float-path JumpFlood
-  int jfa_tab = 1;               // tuning "jfa_tab": the float-path steps read texcoords from tc (0: divide per tap)
+  bool tc_rcp_ok = false;        // tc_rcp equals the division for every column and row (tc_rcp_exact)
+  int jfa_tab = 2;               // tuning "jfa_tab": float-path texcoords 0 divided, 1 from tc, 2 by tc_rcp where
+                                 // exact (else from tc)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
   bool poison = false;           // tuning "poison": 0xFF-fill intermediates before each frame
   bool keep_levels = false;
@@ -654,6 +656,7 @@ int allocate(rc2dgi_ctx *c) {
     tc_table(c->W, c->H, t.data());
     HIPCHK(c, alloc(&c->tc, t.size() * sizeof(float)));
     HIPCHK(c, hipMemcpy(c->tc, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+    c->tc_rcp_ok = tc_rcp_exact(c->W) && tc_rcp_exact(c->H);
   }
   HIPCHK(c, alloc(&c->dirs, dir_table_len(c->N) * sizeof(float2)));
   HIPCHK(c, alloc(&c->dexit, dir_table_len(c->N) * sizeof(float4)));
@@ -1075,6 +1078,9 @@ namespace {
 // JumpFlood ping-pong (RC2DGI.cs:287-326): step t writes jumpRT2 for even t, jumpRT1 for odd t.
 unsigned *jfa_out(rc2dgi_ctx *c, int t) { return (t & 1) ? c->jump1 : c->jump2; }
 
+// how the float-path steps get their texcoords (launch_jfa_step tmode): tuning jfa_tab, tc_rcp only where exact
+int jfa_tmode(const rc2dgi_ctx *c) { return c->jfa_tab == 2 ? (c->tc_rcp_ok ? 2 : 1) : c->jfa_tab; }
+
 int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
   float ox[3], oy[3];
   jfa_offsets(c->W, c->H, t, ox, oy);  // vec2(x, y) * _Aspect.yx * _StepSize
@@ -1106,8 +1112,8 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
     const unsigned *src = t == 0 ? c->occ : out_of(t - 1);
     for (auto &r : plan.jfa[t].iv)
       HIPCHK(c, launch_jfa_step(t == 0, src, t == 0 ? c->mpitch : c->sd.pitch, out, dist, c->sd, ox, oy, st,
-                                r.first, r.second, nullptr, 0, c->jfa_lds, c->jfa_rt, c->jfa_rows,
-                                c->jfa_tab ? c->tc : nullptr));
+                                r.first, r.second, nullptr, 0, c->jfa_lds, c->jfa_rt, c->jfa_rows, c->tc,
+                                jfa_tmode(c)));
     return RC2DGI_OK;
   }
   // row-strip shard: the own strip, into its window (global row y0 - m = local row 0)
@@ -1116,7 +1122,7 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
   const int wrow0 = y0 - c->jx.m;
   if (t == 0) {
     HIPCHK(c, launch_jfa_step(true, c->occ, c->mpitch, jfa_out(c, 0), dist, c->sd, ox, oy, st, y0, y1, nullptr, wrow0,
-                              0, 1, 0, c->jfa_tab ? c->tc : nullptr));
+                              0, 1, 0, c->tc, jfa_tmode(c)));
     return RC2DGI_OK;
   }
   int buf[3], row0[3];
@@ -1128,7 +1134,7 @@ int jfa_launch(rc2dgi_ctx *c, const FramePlan &plan, int t) {
     win.row0[y] = row0[y];
   }
   HIPCHK(c, launch_jfa_step(false, nullptr, c->sd.pitch, jfa_out(c, t), dist, c->sd, ox, oy, st, y0, y1, &win, wrow0,
-                            0, 1, 0, c->jfa_tab ? c->tc : nullptr));
+                            0, 1, 0, c->tc, jfa_tmode(c)));
   return RC2DGI_OK;
 }
 
@@ -2191,7 +2197,7 @@ int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value) {
     return RC2DGI_OK;
   }
   if (k == "jfa_tab") {
-    if (value != 0 && value != 1) return fail(c, RC2DGI_E_ARG, "jfa_tab is 0 or 1");
+    if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "jfa_tab is 0, 1 or 2");
     c->jfa_tab = value;
     return RC2DGI_OK;
   }

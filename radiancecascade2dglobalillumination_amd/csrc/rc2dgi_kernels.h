@@ -62,9 +62,12 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
                            int lds = 0,   // LDS-staged taps for short power-of-two steps (tuning jfa_lds)
                            int small_rt = 1,   // rows per lane of the float-path steps on small screens (tuning jfa_rt)
                            int jrows = 0,
-                           const float *tc = nullptr);  // float path: the W + H texcoord table (tc_table), or nullptr
+                           const float *tc = nullptr,  // float path: the W + H texcoord table (tc_table), or nullptr
+                           int tmode = 0);  // float path texcoords: 0 divide, 1 the table, 2 tc_rcp (tc_rcp_exact)
 // the texcoords (i + 0.5) / W of the W columns, then (j + 0.5) / H of the H rows, as the kernels divide (host)
-void tc_table(int W, int H, float *out);     // short isotropic power-of-two steps (S = 1, 2, 4): JR = 4 / 8
+void tc_table(int W, int H, float *out);
+// x * (1/n) plus one fused correction equals the IEEE quotient (i + 0.5) / n for every i < n (host, exhaustive)
+bool tc_rcp_exact(int n);     // short isotropic power-of-two steps (S = 1, 2, 4): JR = 4 / 8
                                                // consecutive rows per lane, each tap row loaded once (jfa_rows)
 // integer taps of the power-of-two JFA kernel (false: the float path runs); also used by the
 // row-strip planner

@@ -96,7 +96,16 @@ __global__ __launch_bounds__(256) void k_seeds_from_mask(const unsigned *__restr
 // ---------------------------------------------------------------- JumpFlood (+ DistanceField)
 struct JfaOffsets {
   float ox[3], oy[3];
+  float rw, rh;  // 1 / W, 1 / H correctly rounded (TAB 2: tc_rcp)
 };
+
+// (i + 0.5) / n without a division: x * (1/n) and one fused correction, the IEEE quotient for every i < n when
+// tc_rcp_exact(n) (checked on the host per context; the float-path step then uses it, TAB 2)
+__host__ __device__ __forceinline__ float tc_rcp(int i, float n, float rn) {
+  const float x = (float)i + 0.5f;
+  const float t = x * rn;
+  return fmaf(fmaf(-t, n, x), rn, t);
+}
 
 
 // One JumpFlood.fs step.  FIRST: taps read the occupancy mask (the ScreenUV seeds); otherwise the
@@ -107,17 +116,18 @@ constexpr int JT = 4;
 
 // RT: rows per lane (JT on large screens; 1 on small ones, where 4 rows per lane left about one wave per SIMD:
 // 1200 x 900 = 1083 workgroups, each step a few exposed round trips)
-// TAB (non-power-of-two screens with W + H <= kTcTabMax): every fragTexCoord the step needs -- the texel's, each
+// TAB 1 (non-power-of-two screens with W + H <= kTcTabMax): every fragTexCoord the step needs -- the texel's, each
 // tap seed's -- read from a table of the W column and H row texcoords ((i + 0.5) / n, the same correctly rounded
-// division, made once per context: tc_table) staged in LDS, instead of two IEEE divisions per tap.
+// division, made once per context: tc_table) staged in LDS, instead of two IEEE divisions per tap.  TAB 2: computed
+// by tc_rcp (three operations), where the host proved it equal to the division for every index (tc_rcp_exact).
 constexpr int kTcTabMax = 8192;
-template <bool FIRST, bool U8, int RT = JT, bool TAB = false>
+template <bool FIRST, bool U8, int RT = JT, int TAB = 0>
 __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ src, int src_pitch,
                                                   unsigned *__restrict__ dst, unsigned short *__restrict__ dist,
                                                   ScreenDims s, JfaOffsets o, int row0, int row1, JfaSrc win,
                                                   int dst_row0, const float *__restrict__ tc) {
-  extern __shared__ float s_tc[];  // (TAB: W column texcoords, then H row texcoords)
-  if constexpr (TAB) {
+  extern __shared__ float s_tc[];  // (TAB 1: W column texcoords, then H row texcoords)
+  if constexpr (TAB == 1) {
     for (int k = (int)threadIdx.x; k < s.W + s.H; k += 256) s_tc[k] = tc[k];
     __syncthreads();
   }
@@ -125,8 +135,9 @@ __global__ __launch_bounds__(256) void k_jfa_step(const unsigned *__restrict__ s
   const int j0 = row0 + blockIdx.y * (4 * RT) + (threadIdx.x >> 6);
   if (i >= s.W) return;
   const Axis ax{s.W, s.powW}, ay{s.H, s.powH};
-  auto tcx = [&](int q) { return TAB ? s_tc[q] : texcoord(q, ax); };
-  auto tcy = [&](int q) { return TAB ? s_tc[s.W + q] : texcoord(q, ay); };
+  const float fw = (float)s.W, fh = (float)s.H;
+  auto tcx = [&](int q) { return TAB == 1 ? s_tc[q] : (TAB == 2 ? tc_rcp(q, fw, o.rw) : texcoord(q, ax)); };
+  auto tcy = [&](int q) { return TAB == 1 ? s_tc[s.W + q] : (TAB == 2 ? tc_rcp(q, fh, o.rh) : texcoord(q, ay)); };
   const float u = tcx(i);
   int ti[3];
 #pragma unroll
@@ -1423,7 +1434,7 @@ hipError_t launch_seeds_from_mask(const unsigned *mask, int mpitch, unsigned *se
 hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsigned *dst, unsigned short *dist,
                            ScreenDims s, const float off_x[3], const float off_y[3], hipStream_t st, int row0,
                            int row1, const JfaSrc *window, int dst_row0, int lds, int small_rt, int jrows,
-                           const float *tc) {
+                           const float *tc, int tmode) {
   JfaSrc win{};
   if (window && !first) win = *window;
   if (row1 < 0 || row1 > s.H) row1 = s.H;
@@ -1434,6 +1445,8 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     o.ox[k] = off_x[k];
     o.oy[k] = off_y[k];
   }
+  o.rw = 1.0f / (float)s.W;
+  o.rh = 1.0f / (float)s.H;
   const dim3 grid(ceil_div(s.W, 64), ceil_div(row1 - row0, 4 * JT));
   // float-path steps on small screens: one row per lane (k_jfa_step RT)
   const bool small = (size_t)s.W * (size_t)(row1 - row0) <= ((size_t)1 << 21) && small_rt != JT;
@@ -1516,14 +1529,18 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
     }
 #undef RC2DGI_JFA
   } else {
-    // the float path: texcoords from the context's table where it has one (k_jfa_step TAB)
-    const bool tab = tc && s.W + s.H <= kTcTabMax;
-    const size_t lds = tab ? (size_t)(s.W + s.H) * sizeof(float) : 0;
+    // the float path: texcoords by tc_rcp where the host proved it exact (tmode 2), from the context's table
+    // (tmode 1), else divided (k_jfa_step TAB)
+    const int tm = tmode == 2 ? 2 : ((tmode == 1 && tc && s.W + s.H <= kTcTabMax) ? 1 : 0);
+    const size_t lds = tm == 1 ? (size_t)(s.W + s.H) * sizeof(float) : 0;
 #define RC2DGI_JFA_F(G, FV, RV)                                                                                     \
   do {                                                                                                            \
-    if (tab)                                                                                                      \
-      hipLaunchKernelGGL((k_jfa_step<FV, false, RV, true>), G, dim3(256), lds, st, src, src_pitch, dst, dist, s, o, \
+    if (tm == 1)                                                                                                  \
+      hipLaunchKernelGGL((k_jfa_step<FV, false, RV, 1>), G, dim3(256), lds, st, src, src_pitch, dst, dist, s, o,  \
                          row0, row1, win, dst_row0, tc);                                                          \
+    else if (tm == 2)                                                                                             \
+      hipLaunchKernelGGL((k_jfa_step<FV, false, RV, 2>), G, dim3(256), 0, st, src, src_pitch, dst, dist, s, o,    \
+                         row0, row1, win, dst_row0, nullptr);                                                     \
     else                                                                                                          \
       hipLaunchKernelGGL((k_jfa_step<FV, false, RV>), G, dim3(256), 0, st, src, src_pitch, dst, dist, s, o, row0, \
                          row1, win, dst_row0, nullptr);                                                           \
@@ -1538,6 +1555,13 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
 #undef RC2DGI_JFA_F
   }
   return hipGetLastError();
+}
+
+bool tc_rcp_exact(int n) {
+  const float fn = (float)n, rn = 1.0f / fn;
+  for (int i = 0; i < n; ++i)
+    if (tc_rcp(i, fn, rn) != ((float)i + 0.5f) / fn) return false;
+  return true;
 }
 
 void tc_table(int W, int H, float *out) {

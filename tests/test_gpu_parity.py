@@ -603,24 +603,27 @@ def test_jfa_rows_short_steps_are_bit_identical(RC2DGI, W, H, N, storage, scene)
                                       (4000, 96, 4, 1.0), (6000, 2000, 4, 1.0)])
 @pytest.mark.parametrize("scene", ["demo", "rand:63"])
 def test_jfa_texcoord_table_is_bit_identical(RC2DGI, W, H, N, rs, scene):
-    """The float-path JumpFlood steps (non-power-of-two screens) read every fragTexCoord from the context's table of
-    (i + 0.5) / n (tuning jfa_tab, on by default) instead of dividing per tap: jumpRT1 / jumpRT2, the distance field
-    and the frame are unchanged, poisoned intermediates; W + H above the table's limit (6000 + 2000) keeps dividing."""
+    """The float-path JumpFlood steps (non-power-of-two screens) take every fragTexCoord from the context's table of
+    (i + 0.5) / n (tuning jfa_tab 1) or from x * (1/n) with one fused correction, proven equal to the division for
+    every index on the host (jfa_tab 2, the default) instead of dividing per tap: jumpRT1 / jumpRT2, the distance
+    field and the frame are unchanged, poisoned intermediates; W + H above the table's limit (6000 + 2000) divides
+    under jfa_tab 1."""
     color, emis = make_scene(scene, W, H)
     ctx = RC2DGI(W, H, cascade_count=N, ray_range=2.0, render_scale=rs)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
     out = {}
-    for tab in (0, 1):
+    for tab in (0, 1, 2):
         ctx.set_tuning("jfa_tab", tab)
         assert ctx.get_tuning("jfa_tab") == tab
         ctx.set_tuning("poison", 1)
         ctx.do_rc2dgi()
         ctx.sync()
         out[tab] = {k: ctx.download(k) for k in ("jump1", "jump2", "dist", "color")}
-    for k in out[0]:
-        assert np.array_equal(out[0][k].view(np.uint8), out[1][k].view(np.uint8)), \
-            f"jfa_tab {k}: {np.count_nonzero(out[0][k] != out[1][k])}"
+    for tab in (1, 2):
+        for k in out[0]:
+            assert np.array_equal(out[0][k].view(np.uint8), out[tab][k].view(np.uint8)), \
+                f"jfa_tab {tab} {k}: {np.count_nonzero(out[0][k] != out[tab][k])}"
     ctx.close()
 
 
