@@ -194,6 +194,9 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     screens) with that many consecutive rows per lane, each tap row loaded once (measured no faster)
  *   "cascade_band"    1 (default): row-strip shards on strip tables and the fused blur + merge band GI1 / GI2 (see
  *                     rc2dgi_device_buffer); 0: whole textures
+ *   "rc_rdiv"         1 (default): non-power-of-two cascades divide by the cascade resolution as x * (1/n) plus one
+ *                     fused correction on the levels where the context proved that equal to the IEEE quotient for
+ *                     every numerator (get_tuning "rc_rdiv_levels": bit L set when level L does on both axes); 0: divide
  *   "jfa_tab"         the float-path JumpFlood steps' fragTexCoords (i + 0.5) / n: 2 (default) x * (1/n) plus one
  *                     fused correction, used where the context proved it equal to the division for every index (else
  *                     as 1); 1 from a per-context table (W + H <= 8192); 0 divided per tap

@@ -153,6 +153,8 @@ struct rc2dgi_ctx {
   unsigned *jtail = nullptr;     // J_{S-jfa_tail-1}, which the fused tail reads (it writes both ping-pong textures)
   float *tc = nullptr;           // texcoords of the W columns and H rows (tc_table) for the float-path JumpFlood
   bool tc_rcp_ok = false;        // tc_rcp equals the division for every column and row (tc_rcp_exact)
+  std::vector<unsigned char> rdiv_x, rdiv_y;  // per level: rc_div_exact on CW / CH (non-power-of-two cascades)
+  int rc_rdiv = 1;               // tuning "rc_rdiv": use them (0: IEEE divisions)
   int jfa_tab = 2;               // tuning "jfa_tab": float-path texcoords 0 divided, 1 from tc, 2 by tc_rcp where
                                  // exact (else from tc)
   int shade_fused = 1;           // tuning "shade_fused": k_shade_cmin (records + bound table in one pass) where it applies
@@ -657,6 +659,12 @@ int allocate(rc2dgi_ctx *c) {
     HIPCHK(c, alloc(&c->tc, t.size() * sizeof(float)));
     HIPCHK(c, hipMemcpy(c->tc, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
     c->tc_rcp_ok = tc_rcp_exact(c->W) && tc_rcp_exact(c->H);
+  }
+  c->rdiv_x.assign(c->N, 0);
+  c->rdiv_y.assign(c->N, 0);
+  for (int L = 0; L < c->N; ++L) {
+    c->rdiv_x[L] = !c->cd.powW && rc_div_exact(c->CW, L, L == c->N - 1);
+    c->rdiv_y[L] = !c->cd.powH && rc_div_exact(c->CH, L, L == c->N - 1);
   }
   HIPCHK(c, alloc(&c->dirs, dir_table_len(c->N) * sizeof(float2)));
   HIPCHK(c, alloc(&c->dexit, dir_table_len(c->N) * sizeof(float4)));
@@ -1405,6 +1413,8 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
     a.cmin_screen = c->rc_skip == 3 || (c->rc_skip == 1 && rc_ray_end(L, c->N, c->ray_range) >= 0.125f);
     a.tail_k = c->rc_tail[L];
     a.wg_proof = c->rc_wgproof;
+    a.div_x = c->rc_rdiv && c->rdiv_x[L];
+    a.div_y = c->rc_rdiv && c->rdiv_y[L];
     if (c->gband) {  // banded cascade textures (gi_buffers)
       if (!f.st) return fail(c, RC2DGI_E_STATE, "banded cascade textures without strip tables");
       a.out_b0 = c->gb0[L];
@@ -2196,6 +2206,11 @@ int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value) {
     c->cascade_band = value;
     return RC2DGI_OK;
   }
+  if (k == "rc_rdiv") {
+    if (value != 0 && value != 1) return fail(c, RC2DGI_E_ARG, "rc_rdiv is 0 or 1");
+    c->rc_rdiv = value;
+    return RC2DGI_OK;
+  }
   if (k == "jfa_tab") {
     if (value < 0 || value > 2) return fail(c, RC2DGI_E_ARG, "jfa_tab is 0, 1 or 2");
     c->jfa_tab = value;
@@ -2367,6 +2382,17 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "cascade_band") {
     *value = c->cascade_band;
+    return RC2DGI_OK;
+  }
+  if (k == "rc_rdiv") {
+    *value = c->rc_rdiv;
+    return RC2DGI_OK;
+  }
+  if (k == "rc_rdiv_levels") {  // levels whose divisions take the reciprocal form on both non-power-of-two axes (bits)
+    int m = 0;
+    for (int L = 0; L < c->N && L < 31; ++L)
+      if ((c->cd.powW || c->rdiv_x[L]) && (c->cd.powH || c->rdiv_y[L])) m |= 1 << L;
+    *value = m;
     return RC2DGI_OK;
   }
   if (k == "jfa_tab") {

@@ -142,7 +142,12 @@ struct RcLevelArgs {
   // banded cascade textures (with rec_color only): `out` holds, per block row, out_bn block-local rows from out_b0 on
   // (cyclically), `upper` up_bn rows from up_b0 on; 0 rows: the whole texture
   int out_b0 = 0, out_bn = 0, up_b0 = 0, up_bn = 0;
+  int div_x = 0, div_y = 0;  // the level's divisions by CW / CH as x * (1/n) + one fused correction (rc_div_exact)
 };
+// every numerator level `level` divides by the cascade resolution n on one axis (k_rc_level: the probe origins
+// (c + 0.5) 2^L and, below the top, the upper sample positions clamp(c/2 + 1/4, 1/2, bd/2 - 1/2) + k bd/2) has the
+// IEEE quotient under div_res mode 2 (host, exhaustive)
+bool rc_div_exact(int n, int level, bool top);
 
 // The cascade chain (rc2dgi_rc_chain.hip, tuning rc_chain): the levels a[0 .. n) (consecutive, downwards; a[0]
 // is the top level, or the level below it with the top already written to a[0].upper) in one launch of 16x16x1

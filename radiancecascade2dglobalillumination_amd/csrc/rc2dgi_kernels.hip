@@ -1557,6 +1557,25 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   return hipGetLastError();
 }
 
+bool rc_div_exact(int n, int level, bool top) {
+  const float fn = (float)n, inv = 1.0f / fn;
+  const int bsc = 1 << level, bd = n >> level;
+  const float bdf = fn / (float)bsc;  // (RcParams bdxf / bdyf)
+  auto ok = [&](float a) {
+    const float t = a * inv;
+    return std::fma(std::fma(-t, fn, a), inv, t) == a / fn;
+  };
+  for (int c = 0; c < bd; ++c) {
+    if (!ok(((float)c + 0.5f) * (float)bsc)) return false;
+    if (top) continue;
+    float pc = (float)c * 0.5f + 0.25f;
+    pc = std::fmin(std::fmax(pc, 0.5f), bdf * 0.5f - 0.5f);
+    for (int k = 0; k < 2 * bsc; ++k)
+      if (!ok(pc + (float)k * (bdf * 0.5f))) return false;
+  }
+  return true;
+}
+
 bool tc_rcp_exact(int n) {
   const float fn = (float)n, rn = 1.0f / fn;
   for (int i = 0; i < n; ++i)
@@ -1952,6 +1971,8 @@ RcParams rc_level_params(const RcLevelArgs &a, ScreenDims s, CascadeDims c) {
   P.t0 = ((float)start / (float)maxValue) * a.ray_range;
   P.t1 = ((float)end / (float)maxValue) * a.ray_range;
   P.reflectivity = a.reflectivity;
+  P.rdx = a.div_x;
+  P.rdy = a.div_y;
   P.ob0 = a.out_b0;
   P.obn = a.out_bn;
   P.ub0 = a.up_b0;

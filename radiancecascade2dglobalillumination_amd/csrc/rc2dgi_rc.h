@@ -39,6 +39,8 @@ struct RcParams {
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
+  int rdx, rdy;               // non-power-of-two cascades: the level's divisions by CRx / CRy take div_res mode 2
+                              // (host-proven exact, RcLevelArgs div_x / div_y)
   int ob0, obn, ub0, ubn;     // banded G_L / G_{L+1} (RD only; row-strip shards): a level's texture holds, per block
                               // row, the obn (ubn) block-local rows from ob0 (ub0) on, cyclically; 0 rows: whole
 #if defined(RC2DGI_DIAG_STATS) || defined(RC2DGI_DIAG_TIMING)
@@ -115,9 +117,17 @@ __device__ __forceinline__ float decode_dist(unsigned q) {
   return __builtin_fmaf(r, c1, x);
 }
 
-// a / n for the shader's divisions by a resolution: for a power-of-two n the quotient is
-// exactly a * (1/n) (both roundings are exact scalings), otherwise a true IEEE division
-__device__ __forceinline__ float div_res(float a, float n, float inv_n, int pow2) { return pow2 ? a * inv_n : a / n; }
+// a / n for the shader's divisions by a resolution.  mode 1 (a power-of-two n): exactly a * (1/n) (both roundings
+// are exact scalings).  mode 2: a * (1/n) plus one fused correction, which the host proved equal to the IEEE
+// quotient for every numerator the level divides (rc_div_exact).  mode 0: a true IEEE division.
+__device__ __forceinline__ float div_res(float a, float n, float inv_n, int mode) {
+  if (mode == 1) return a * inv_n;
+  if (mode == 2) {
+    const float t = a * inv_n;
+    return __builtin_fmaf(__builtin_fmaf(-t, n, a), inv_n, t);
+  }
+  return a / n;
+}
 
 // Workgroup order.  Hardware deals consecutive workgroup ids round-robin over the 8 XCDs
 // (each with its own L2), so the physical id is remapped so that every XCD walks one
@@ -615,6 +625,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 :
   // terms; below it: the staged upper cascade).  Same arithmetic for every texel it stores.  At 4096^2 N=6 this is
   // 47 % of the top level's workgroups; at rayRange 64 every workgroup of the two top levels (any tile shape: the
   // several-probes-per-lane tiles of C2 / C3 skip their bound table and workgroup proof the same way).
+  // division modes of the level's divisions by the cascade resolution (div_res)
+  const int dmx = (P2S || P.c.powW) ? 1 : (P.rdx ? 2 : 0), dmy = (P2S || P.c.powH) ? 1 : (P.rdy ? 2 : 0);
   bool wg_off = false;
 #ifdef RC2DGI_AB_NO_WGOFF  // (A/B builds: no whole-workgroup far-interval test)
   if constexpr (false) {
@@ -623,11 +635,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 :
 #endif
     if (P.t0 >= 0.25f && !(P.t0 > P.t1)) {
       const int cxl = min(cx0 + TX, P.bdx) - 1, cyl = min(cy0 + THY, P.p1) - 1;
-      const bool pw = P2S || P.c.powW, ph = P2S || P.c.powH;
-      const float oxl = div_res(((float)cx0 + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, pw);
-      const float oxh = div_res(((float)cxl + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, pw);
-      const float oyl = div_res(((float)cy0 + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, ph);
-      const float oyh = div_res(((float)cyl + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, ph);
+      const float oxl = div_res(((float)cx0 + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, dmx);
+      const float oxh = div_res(((float)cxl + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, dmx);
+      const float oyl = div_res(((float)cy0 + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, dmy);
+      const float oyh = div_res(((float)cyl + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, dmy);
       bool off = cxl >= cx0 && cyl >= cy0;
 #pragma unroll
       for (int r = 0; r < ND; ++r) {
@@ -758,14 +769,14 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 :
   };
 
   const float cxf = (float)cx;
-  const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);  // rayOrigin / _CascadeResolution
+  const float ox = div_res((cxf + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, dmx);  // rayOrigin / _CascadeResolution
   float oy[PY];
   bool pok[PY];
 #pragma unroll
   for (int p = 0; p < PY; ++p) {
     const int cy = cyb + p * TY;
     pok[p] = xok && cy < P.p1;
-    oy[p] = div_res(((float)cy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P2S || P.c.powH);
+    oy[p] = div_res(((float)cy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, dmy);
   }
   const Axis sax{P.s.W, P.s.powW}, say{P.s.H, P.s.powH};
 
@@ -1126,8 +1137,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 :
       const int r = (int)(k % ND), p = (int)(k / ND);
       // the owner's origin and direction, by the owner's own expressions
       const int ocx = cx0 + (int)(otid % TX), ocy = cy0 + (int)(otid / TX) + p * TY;
-      const float qox = div_res(((float)ocx + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, P2S || P.c.powW);
-      const float qoy = div_res(((float)ocy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, P2S || P.c.powH);
+      const float qox = div_res(((float)ocx + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, dmx);
+      const float qoy = div_res(((float)ocy + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, dmy);
       float qdx = rdx[0], qdy = rdy[0];
 #pragma unroll
       for (int q2 = 1; q2 < ND; ++q2) {
@@ -1251,8 +1262,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 :
             } else if constexpr (!P2S) {
               // general GL path (mod(float(angleIndex), 2b), floor(float(angleIndex)/2b) are exact integers)
               const float offx = (float)(ai & umask), offy = (float)(ai >> ushift);
-              const float sx = (px + offx * (P.bdxf * 0.5f)) / P.CRx;
-              const float sy = (py + offy * (P.bdyf * 0.5f)) / P.CRy;
+              const float sx = div_res(px + offx * (P.bdxf * 0.5f), P.CRx, P.invCRx, dmx);
+              const float sy = div_res(py + offy * (P.bdyf * 0.5f), P.CRy, P.invCRy, dmy);
               int x0, x1, y0, y1;
               wrap_linear(sx, Axis{P.c.CW, 0}, x0, x1, ux);
               wrap_linear(sy, Axis{P.c.CH, 0}, y0, y1, uy);

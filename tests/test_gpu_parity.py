@@ -599,6 +599,37 @@ def test_jfa_rows_short_steps_are_bit_identical(RC2DGI, W, H, N, storage, scene)
     ctx.close()
 
 
+@pytest.mark.parametrize("W,H,N,rr,rs", [(1200, 900, 6, 2.0, 1.0), (200, 120, 3, 2.0, 1.0), (333, 200, 4, 2.0, 0.5),
+                                         (320, 256, 5, 8.0, 1.7), (1000, 700, 5, 64.0, 1.0)])
+@pytest.mark.parametrize("chain", [0, 1])
+def test_rc_reciprocal_divisions_are_bit_identical(RC2DGI, W, H, N, rr, rs, chain):
+    """Non-power-of-two cascades: the levels' divisions by the cascade resolution as x * (1/n) plus one fused
+    correction, where the host proved that equal to the IEEE quotient for every numerator of the level (tuning
+    rc_rdiv, on by default): every render texture and cascade level is unchanged, with and without the cascade
+    chain.  At C1 (1216 x 960 cascades) every level takes them."""
+    color, emis = make_scene("rand:64", W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr, render_scale=rs)
+    ctx.set_keep_levels(True)
+    if chain:
+        ctx.set_tuning("rc_chain", 1)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    if (W, H, rs) == (1200, 900, 1.0):
+        assert ctx.get_tuning("rc_rdiv_levels") == (1 << N) - 1
+    out = {}
+    for rd in (0, 1):
+        ctx.set_tuning("rc_rdiv", rd)
+        ctx.set_tuning("poison", 1)
+        ctx.do_rc2dgi()
+        ctx.sync()
+        out[rd] = {k: ctx.download(k) for k in ("color", "temp", "gi1", "gi2", "final_gi")}
+        out[rd].update({f"L{L}": ctx.download_level(L) for L in range(N)})
+    for k in out[0]:
+        assert np.array_equal(out[0][k].view(np.uint8), out[1][k].view(np.uint8)), \
+            f"rc_rdiv {k}: {np.count_nonzero(out[0][k] != out[1][k])}"
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,N,rs", [(1200, 900, 6, 1.0), (200, 120, 3, 1.0), (320, 256, 4, 0.5), (96, 4000, 4, 1.0),
                                       (4000, 96, 4, 1.0), (6000, 2000, 4, 1.0)])
 @pytest.mark.parametrize("scene", ["demo", "rand:63"])
