@@ -154,6 +154,13 @@ struct rc2dgi_ctx {
   float *tc = nullptr;           // texcoords of the W columns and H rows (tc_table) for the float-path JumpFlood
   bool tc_rcp_ok = false;        // tc_rcp equals the division for every column and row (tc_rcp_exact)
   std::vector<unsigned char> rdiv_x, rdiv_y;  // per level: rc_div_exact on CW / CH (non-power-of-two cascades)
+  float4 *bconst = nullptr;      // per-direction-block values of the levels no ray samples (k_rc_block_const), level L
+                                 // from (4^L - 1) / 3 on
+  int rc_fill = 1;               // tuning "rc_fill": such levels as per-block fills (0: their usual launch)
+  std::vector<float2> h_dirs;    // the uploaded direction table (rc_level_all_off)
+  std::vector<unsigned char> alloff;  // per level: rc_level_all_off, for ray range alloff_rr (cleared with the tables)
+  float alloff_rr = -1.0f;
+  int fill_mask = 0;             // levels the last frame filled
   int rc_rdiv = 1;               // tuning "rc_rdiv": use them (0: IEEE divisions)
   int jfa_tab = 2;               // tuning "jfa_tab": float-path texcoords 0 divided, 1 from tc, 2 by tc_rcp where
                                  // exact (else from tc)
@@ -299,7 +306,7 @@ void free_buffers(rc2dgi_ctx *c) {
   void *bufs[] = {c->color_in, c->emissive, c->temp, c->color_out, c->jump1, c->jump2, c->dist, c->occ,
                   c->gi1,      c->gi2,      c->blur, c->dirs,      c->sky, c->gi_spare, c->dist_t, c->dist_p, c->dist_n, c->shade,
                   c->cmin,     c->dexit, c->hitc, c->dclr, c->dboxes, c->mfield, c->cell_pal, c->shade_list, c->jtail,
-                  c->tc};
+                  c->tc, c->bconst};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   for (unsigned *&b : c->jblk) {
@@ -320,6 +327,7 @@ void free_buffers(rc2dgi_ctx *c) {
   c->shade_list = nullptr;
   c->jtail = nullptr;
   c->tc = nullptr;
+  c->bconst = nullptr;
   c->built_hitc = c->built_cmin = c->built_dclr = c->built_pal = false;
   c->dboxes = nullptr;
   c->gi1 = c->gi2 = c->blur = c->gi_spare = nullptr;
@@ -660,6 +668,9 @@ int allocate(rc2dgi_ctx *c) {
     HIPCHK(c, hipMemcpy(c->tc, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
     c->tc_rcp_ok = tc_rcp_exact(c->W) && tc_rcp_exact(c->H);
   }
+  if (c->N <= 10)  // (4^L values per level: at most 350 k float4)
+    HIPCHK(c, alloc(&c->bconst, ((((size_t)1 << (2 * c->N)) - 1) / 3) * sizeof(float4)));
+  c->alloff.clear();
   c->rdiv_x.assign(c->N, 0);
   c->rdiv_y.assign(c->N, 0);
   for (int L = 0; L < c->N; ++L) {
@@ -779,6 +790,8 @@ int upload_tables(rc2dgi_ctx *c) {
   HIPCHK(c, hipMemcpyAsync(c->sky, sky.data(), sky.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   // the host vectors die here: make the pageable copies complete first
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->h_dirs = dirs;
+  c->alloff.clear();  // (levels no ray samples: proven again with these directions)
   c->tables_dirty = false;
   return RC2DGI_OK;
 }
@@ -1367,6 +1380,21 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
   // leaves it (N odd: giRT1), level 1 into the other, levels >= 2 into chain_bufs.
   const bool chain = chain_active(c) && c->chain && (int)c->chain_bufs.size() == c->N;
   std::vector<RcLevelArgs> chain_args;
+  // levels no ray samples (rc_level_all_off): per-block values and a fill in place of the level's launch, from the top
+  // down while every level above was one too (k_rc_block_const; unsharded f32 frames without the chain)
+  const bool fill_on = c->rc_fill && c->bconst && c->world == 1 && !chain && c->storage == RC2DGI_STORAGE_F32 &&
+                       c->h_dirs.size() == dir_table_len(c->N);
+  if (fill_on && ((int)c->alloff.size() != c->N || c->alloff_rr != c->ray_range)) {
+    c->alloff.assign(c->N, 0);
+    for (int L = c->N - 1; L >= 0; --L) {
+      c->alloff[L] = rc_level_all_off(c->sd, c->cd, c->N, L, c->ray_range, c->h_dirs.data() + dir_table_offset(L),
+                                      c->rc_rdiv && c->rdiv_x[L], c->rc_rdiv && c->rdiv_y[L]);
+      if (!c->alloff[L]) break;  // (only a run from the top is used)
+    }
+    c->alloff_rr = c->ray_range;
+  }
+  auto boff = [](int L) { return ((((size_t)1) << (2 * L)) - 1) / 3; };
+  int filled = 0;
   float4 *const g0 = (c->N % 2) ? c->gi1 : c->gi2, *const g1 = (c->N % 2) ? c->gi2 : c->gi1;
   auto chain_out = [&](int L) { return L == 0 ? g0 : (L == 1 ? g1 : c->chain_bufs[L]); };
   for (int L = c->N - 1; L >= 0; --L) {
@@ -1425,7 +1453,12 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
       }
     }
 
-    if (chain && (L < c->N - 1 || c->rc_chain == 4)) {
+    const bool top = L == c->N - 1;
+    if (fill_on && c->alloff[L] && (top || (filled >> (L + 1) & 1))) {
+      HIPCHK(c, launch_rc_block_const(top, top ? c->sky : c->bconst + boff(L + 1), c->bconst + boff(L), L, st));
+      HIPCHK(c, launch_rc_fill(dstGI, c->bconst + boff(L), c->cd, L, st));
+      filled |= 1 << L;
+    } else if (chain && (L < c->N - 1 || c->rc_chain == 4)) {
       chain_args.push_back(a);  // (whole levels: one process; rc_chain 4: the top level in the launch too)
     } else {
       for (auto &r : plan.level[L].iv) {
@@ -1450,6 +1483,7 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
         HIPCHK(c, hipMemcpyAsync(c->level_bufs[L], chain_out(L), (size_t)c->cd.pitch * c->CH * gi_bytes(c),
                                  hipMemcpyDeviceToDevice, st));
   }
+  c->fill_mask = filled;
   if (LT) HIPCHK(c, hipEventRecord(c->ev_level[0], st));
   if (T) HIPCHK(c, hipEventRecord(c->ev[3], st));
   float4 *&finalGI = gi1final ? c->gi1 : c->gi2;  // RC2DGI.cs:365
@@ -2206,9 +2240,15 @@ int set_tuning_knob(rc2dgi_ctx *c, const char *key, int value) {
     c->cascade_band = value;
     return RC2DGI_OK;
   }
+  if (k == "rc_fill") {
+    if (value != 0 && value != 1) return fail(c, RC2DGI_E_ARG, "rc_fill is 0 or 1");
+    c->rc_fill = value;
+    return RC2DGI_OK;
+  }
   if (k == "rc_rdiv") {
     if (value != 0 && value != 1) return fail(c, RC2DGI_E_ARG, "rc_rdiv is 0 or 1");
     c->rc_rdiv = value;
+    c->alloff.clear();  // (the no-sample proofs divide as the levels do)
     return RC2DGI_OK;
   }
   if (k == "jfa_tab") {
@@ -2386,6 +2426,14 @@ int rc2dgi_get_tuning(rc2dgi_ctx *c, const char *key, int *value) {
   }
   if (k == "rc_rdiv") {
     *value = c->rc_rdiv;
+    return RC2DGI_OK;
+  }
+  if (k == "rc_fill") {
+    *value = c->rc_fill;
+    return RC2DGI_OK;
+  }
+  if (k == "rc_fill_levels") {  // levels the last frame wrote as per-block fills (bits)
+    *value = c->fill_mask;
     return RC2DGI_OK;
   }
   if (k == "rc_rdiv_levels") {  // levels whose divisions take the reciprocal form on both non-power-of-two axes (bits)

@@ -264,6 +264,14 @@ inline float rc_ray_end(int level, int N, float ray_range) {
 
 // one RadianceCascades.fs level
 hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hipStream_t st);
+// Levels no ray samples (k_rc_block_const / k_rc_fill): rc_level_all_off (host) proves that every ray of level L
+// starts off screen (dirs: the level's 4^(L+1) directions as uploaded; div_x / div_y as RcLevelArgs); then
+// launch_rc_block_const writes the level's per-direction-block value (4^L float4) from the sky terms (top level) or
+// the upper level's per-block values, and launch_rc_fill writes the f32 texture from them.
+bool rc_level_all_off(ScreenDims s, CascadeDims c, int N, int level, float ray_range, const float2 *dirs, int div_x,
+                      int div_y);
+hipError_t launch_rc_block_const(bool top, const float4 *src, float4 *dst, int level, hipStream_t st);
+hipError_t launch_rc_fill(float4 *out, const float4 *cst, CascadeDims c, int level, hipStream_t st);
 
 // Blur.fs into blur_out, then the default-shader blended copy-back into gi (RC2DGI.cs:367-387)
 hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st,

@@ -1558,6 +1558,111 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- cascade levels no ray samples
+// A ray whose first position is off screen takes no sample and returns (0,0,0,1) (RadianceCascades.fs:65-69).  When
+// that holds for every ray of a level, each texel is the merge of four such rays with the sky terms (top level) or
+// with the upper level at the texel's sample positions; and when the upper level is such a level too, its texture is
+// constant over each direction block, so the bilinear sample is that constant (the taps are block-local; a weight-0
+// tap across a block edge leaves it so) and this level is constant per block as well.  The upper block of
+// angleIndex ai is block ai of level L + 1.  k_rc_block_const evaluates k_rc_level's own merge expressions (f32
+// cascades) once per block; k_rc_fill writes the texture: a store-bound pass in place of the level's launch.
+template <bool TOP>
+__global__ __launch_bounds__(256) void k_rc_block_const(const float4 *__restrict__ src, float4 *__restrict__ dst,
+                                                        int nblk) {
+  const int bi = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (bi >= nblk) return;
+  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const int ai = bi * 4 + r4;
+    float4 rad = make_float4(0.0f, 0.0f, 0.0f, 1.0f);  // the ray that takes no sample
+    if constexpr (TOP) {
+      const float4 sk = src[ai];
+      rad.x = rad.x + sk.x;
+      rad.y = rad.y + sk.y;
+      rad.z = rad.z + sk.z;
+    } else {
+      const float4 cu = src[ai];
+      const float4 up = GiF32::bilerp(cu, cu, cu, cu, 0.5f, 0.5f);  // (as k_rc_level filters its staged taps)
+      const f2v_t rxy = f2v_t{rad.x, rad.y} + f2v_t{up.x, up.y} * f2v_t{rad.w, rad.w};
+      rad.x = rxy.x;
+      rad.y = rxy.y;
+      rad.z = rad.z + up.z * rad.w;
+      rad.w = rad.w * up.w;
+    }
+    const f2v_t q = {0.25f, 0.25f};
+    const f2v_t axy = f2v_t{acc.x, acc.y} + f2v_t{rad.x, rad.y} * q;
+    const f2v_t azw = f2v_t{acc.z, acc.w} + f2v_t{rad.z, rad.w} * q;
+    acc = make_float4(axy.x, axy.y, azw.x, azw.y);
+  }
+  dst[bi] = GiF32::blend_black(acc);
+}
+
+// every texel of the level's texture from its direction block's value (4 rows per thread)
+__global__ __launch_bounds__(256) void k_rc_fill(float4 *__restrict__ out, const float4 *__restrict__ cst,
+                                                 CascadeDims c, int level) {
+  const int bdx = c.CW >> level, bdy = c.CH >> level;
+  const int i = (int)(blockIdx.x * 64 + (threadIdx.x & 63));
+  const int j0 = (int)(blockIdx.y * 16 + (threadIdx.x >> 6) * 4);
+  if (i >= c.CW) return;
+  const int bx = i / bdx;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = j0 + t;
+    if (j < c.CH) out[(size_t)j * c.pitch + i] = cst[((j / bdy) << level) + bx];
+  }
+}
+
+bool rc_level_all_off(ScreenDims s, CascadeDims c, int N, int level, float ray_range, const float2 *dirs, int div_x,
+                      int div_y) {
+  RcLevelArgs a{};
+  a.level = level;
+  a.N = N;
+  a.ray_range = ray_range;
+  a.div_x = div_x;
+  a.div_y = div_y;
+  const RcParams P = rc_level_params(a, s, c);
+  if (!(P.t0 <= P.t1)) return false;
+  // k_rc_level's whole-workgroup far-interval test (wg_off) with the block's extreme probes: the first positions
+  // are monotone in the probe index, so these bound every probe's (the same float operations, on the host)
+  auto dv = [](float x, float n, float inv, int mode) {
+    if (mode == 1) return x * inv;
+    if (mode == 2) {
+      const float t = x * inv;
+      return std::fma(std::fma(-t, n, x), inv, t);
+    }
+    return x / n;
+  };
+  const int dmx = c.powW ? 1 : (div_x ? 2 : 0), dmy = c.powH ? 1 : (div_y ? 2 : 0);
+  const float oxl = dv(0.5f * (float)P.bsc, P.CRx, P.invCRx, dmx);
+  const float oxh = dv(((float)(P.bdx - 1) + 0.5f) * (float)P.bsc, P.CRx, P.invCRx, dmx);
+  const float oyl = dv(0.5f * (float)P.bsc, P.CRy, P.invCRy, dmy);
+  const float oyh = dv(((float)(P.bdy - 1) + 0.5f) * (float)P.bsc, P.CRy, P.invCRy, dmy);
+  const int nd = 4 << (2 * level);
+  for (int k = 0; k < nd; ++k) {
+    const float sx = (P.t0 * dirs[k].x) * P.aspy, sy = (P.t0 * dirs[k].y) * P.aspx;
+    if (!((oxh + sx) < 0.0f || (oxl + sx) > 1.0f || (oyh + sy) < 0.0f || (oyl + sy) > 1.0f)) return false;
+  }
+  return true;
+}
+
+hipError_t launch_rc_block_const(bool top, const float4 *src, float4 *dst, int level, hipStream_t st) {
+  const int nblk = 1 << (2 * level);
+  const dim3 grid((unsigned)ceil_div(nblk, 256));
+  if (top)
+    hipLaunchKernelGGL(k_rc_block_const<true>, grid, dim3(256), 0, st, src, dst, nblk);
+  else
+    hipLaunchKernelGGL(k_rc_block_const<false>, grid, dim3(256), 0, st, src, dst, nblk);
+  return hipGetLastError();
+}
+
+hipError_t launch_rc_fill(float4 *out, const float4 *cst, CascadeDims c, int level, hipStream_t st) {
+  if (c.gi_f16 || c.gi_u8) return hipErrorInvalidValue;  // (f32 cascades: the values are stored as computed)
+  hipLaunchKernelGGL(k_rc_fill, dim3((unsigned)ceil_div(c.CW, 64), (unsigned)ceil_div(c.CH, 16)), dim3(256), 0, st, out,
+                     cst, c, level);
+  return hipGetLastError();
+}
+
 bool rc_div_exact(int n, int level, bool top) {
   const float fn = (float)n, inv = 1.0f / fn;
   const int bsc = 1 << level, bd = n >> level;

@@ -599,6 +599,37 @@ def test_jfa_rows_short_steps_are_bit_identical(RC2DGI, W, H, N, storage, scene)
     ctx.close()
 
 
+@pytest.mark.parametrize("W,H,N,rr,filled", [(4096, 4096, 8, 64.0, 0b11000000), (512, 512, 8, 64.0, 0b11000000),
+                                             (1000, 700, 6, 64.0, None), (256, 256, 5, 2.0, 0), (300, 300, 6, 200.0, None)])
+@pytest.mark.parametrize("scene", ["demo", "rand:65"])
+def test_rc_levels_no_ray_samples_as_block_fills(RC2DGI, W, H, N, rr, filled, scene):
+    """Levels whose every ray starts off screen (rc_level_all_off, on the host: the whole-workgroup far test with
+    each block's extreme probes) are written as per-direction-block values (k_rc_block_const: k_rc_level's merge
+    expressions, from the sky or the upper level's block values) and a fill (tuning rc_fill, on by default): every
+    level, render texture and the frame are unchanged.  C2's knobs (rayRange 64, N = 8) fill levels 6 and 7."""
+    color, emis = make_scene(scene, W, H)
+    ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
+    ctx.set_keep_levels(True)
+    ctx.upload("color", color)
+    ctx.upload("emissive", emis)
+    out = {}
+    for fl in (0, 1):
+        ctx.set_tuning("rc_fill", fl)
+        ctx.set_tuning("poison", 1)
+        ctx.do_rc2dgi()
+        ctx.sync()
+        if fl and filled is not None:
+            assert ctx.get_tuning("rc_fill_levels") == filled
+        if fl and filled is None:
+            assert ctx.get_tuning("rc_fill_levels") != 0  # (the top levels of these start off screen)
+        out[fl] = {k: ctx.download(k) for k in ("color", "temp", "gi1", "gi2", "final_gi")}
+        out[fl].update({f"L{L}": ctx.download_level(L) for L in range(N)})
+    for k in out[0]:
+        assert np.array_equal(out[0][k].view(np.uint8), out[1][k].view(np.uint8)), \
+            f"rc_fill {k}: {np.count_nonzero(out[0][k] != out[1][k])}"
+    ctx.close()
+
+
 @pytest.mark.parametrize("W,H,N,rr,rs", [(1200, 900, 6, 2.0, 1.0), (200, 120, 3, 2.0, 1.0), (333, 200, 4, 2.0, 0.5),
                                          (320, 256, 5, 8.0, 1.7), (1000, 700, 5, 64.0, 1.0)])
 @pytest.mark.parametrize("chain", [0, 1])
