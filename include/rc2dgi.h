@@ -196,8 +196,8 @@ int rc2dgi_set_sky_table(rc2dgi_ctx *ctx, const float *rgb, int n);
  *                     rc2dgi_device_buffer); 0: whole textures
  *   "rc_fill"         1 (default): a level whose every ray starts off screen (proven on the host from the uploaded
  *                     directions; with every level above it such a level too) is written as its per-direction-block
- *                     values (the merge of rays that take no sample with the sky or the upper block values) -- unsharded
- *                     f32 frames without rc_chain; get_tuning "rc_fill_levels": the levels the last frame filled (bits)
+ *                     values (the merge of rays that take no sample with the sky or the upper block values) -- f32
+ *                     frames without rc_chain; get_tuning "rc_fill_levels": the levels the last frame filled (bits)
  *   "rc_rdiv"         1 (default): non-power-of-two cascades divide by the cascade resolution as x * (1/n) plus one
  *                     fused correction on the levels where the context proved that equal to the IEEE quotient for
  *                     every numerator (get_tuning "rc_rdiv_levels": bit L set when level L does on both axes); 0: divide

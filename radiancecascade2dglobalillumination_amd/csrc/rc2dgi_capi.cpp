@@ -1381,8 +1381,8 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
   const bool chain = chain_active(c) && c->chain && (int)c->chain_bufs.size() == c->N;
   std::vector<RcLevelArgs> chain_args;
   // levels no ray samples (rc_level_all_off): per-block values and a fill in place of the level's launch, from the top
-  // down while every level above was one too (k_rc_block_const; unsharded f32 frames without the chain)
-  const bool fill_on = c->rc_fill && c->bconst && c->world == 1 && !chain && c->storage == RC2DGI_STORAGE_F32 &&
+  // down while every level above was one too (k_rc_block_const; f32 frames without the chain)
+  const bool fill_on = c->rc_fill && c->bconst && !chain && c->storage == RC2DGI_STORAGE_F32 &&
                        c->h_dirs.size() == dir_table_len(c->N);
   if (fill_on && ((int)c->alloff.size() != c->N || c->alloff_rr != c->ray_range)) {
     c->alloff.assign(c->N, 0);
@@ -1456,7 +1456,9 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
     const bool top = L == c->N - 1;
     if (fill_on && c->alloff[L] && (top || (filled >> (L + 1) & 1))) {
       HIPCHK(c, launch_rc_block_const(top, top ? c->sky : c->bconst + boff(L + 1), c->bconst + boff(L), L, st));
-      HIPCHK(c, launch_rc_fill(dstGI, c->bconst + boff(L), c->cd, L, st));
+      for (auto &r : plan.level[L].iv)  // (a row-strip shard: its rows, into the banded texture when banded)
+        HIPCHK(c, launch_rc_fill(dstGI, c->bconst + boff(L), c->cd, L, st, r.first, r.second,
+                                 c->gband ? c->gb0[L] : 0, c->gband ? c->gbn[L] : 0));
       filled |= 1 << L;
     } else if (chain && (L < c->N - 1 || c->rc_chain == 4)) {
       chain_args.push_back(a);  // (whole levels: one process; rc_chain 4: the top level in the launch too)

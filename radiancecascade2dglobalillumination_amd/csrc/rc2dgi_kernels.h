@@ -271,7 +271,8 @@ hipError_t launch_rc_level(const RcLevelArgs &a, ScreenDims s, CascadeDims c, hi
 bool rc_level_all_off(ScreenDims s, CascadeDims c, int N, int level, float ray_range, const float2 *dirs, int div_x,
                       int div_y);
 hipError_t launch_rc_block_const(bool top, const float4 *src, float4 *dst, int level, hipStream_t st);
-hipError_t launch_rc_fill(float4 *out, const float4 *cst, CascadeDims c, int level, hipStream_t st);
+hipError_t launch_rc_fill(float4 *out, const float4 *cst, CascadeDims c, int level, hipStream_t st, int p0 = 0,
+                          int p1 = -1, int b0 = 0, int bn = 0);  // (rows [p0, p1) of every block; bn > 0: banded)
 
 // Blur.fs into blur_out, then the default-shader blended copy-back into gi (RC2DGI.cs:367-387)
 hipError_t launch_blur(const float4 *gi, float4 *blur_out, CascadeDims c, float radius, hipStream_t st,

@@ -1598,18 +1598,23 @@ __global__ __launch_bounds__(256) void k_rc_block_const(const float4 *__restrict
   dst[bi] = GiF32::blend_black(acc);
 }
 
-// every texel of the level's texture from its direction block's value (4 rows per thread)
+// the level's texels from their direction block's value (4 rows per thread): probe rows [p0, p1) of every block (a
+// row-strip shard's plan; else all), into a banded texture when bn > 0 (the block's band of bn rows from b0, as the
+// RD marches store)
 __global__ __launch_bounds__(256) void k_rc_fill(float4 *__restrict__ out, const float4 *__restrict__ cst,
-                                                 CascadeDims c, int level) {
-  const int bdx = c.CW >> level, bdy = c.CH >> level;
+                                                 CascadeDims c, int level, int p0, int p1, int b0, int bn) {
+  const int bdx = c.CW >> level, bdy = c.CH >> level, np = p1 - p0;
   const int i = (int)(blockIdx.x * 64 + (threadIdx.x & 63));
-  const int j0 = (int)(blockIdx.y * 16 + (threadIdx.x >> 6) * 4);
+  const int q0 = (int)(blockIdx.y * 16 + (threadIdx.x >> 6) * 4);
   if (i >= c.CW) return;
   const int bx = i / bdx;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int j = j0 + t;
-    if (j < c.CH) out[(size_t)j * c.pitch + i] = cst[((j / bdy) << level) + bx];
+    const int q = q0 + t;  // (block row, probe row) pairs, block rows outer
+    if (q >= (np << level)) break;
+    const int br = q / np, y = p0 + (q - br * np);
+    const int j = bn > 0 ? br * bn + ((y - b0) & (bdy - 1)) : br * bdy + y;
+    out[(size_t)j * c.pitch + i] = cst[(br << level) + bx];
   }
 }
 
@@ -1656,10 +1661,16 @@ hipError_t launch_rc_block_const(bool top, const float4 *src, float4 *dst, int l
   return hipGetLastError();
 }
 
-hipError_t launch_rc_fill(float4 *out, const float4 *cst, CascadeDims c, int level, hipStream_t st) {
+hipError_t launch_rc_fill(float4 *out, const float4 *cst, CascadeDims c, int level, hipStream_t st, int p0, int p1,
+                          int b0, int bn) {
   if (c.gi_f16 || c.gi_u8) return hipErrorInvalidValue;  // (f32 cascades: the values are stored as computed)
-  hipLaunchKernelGGL(k_rc_fill, dim3((unsigned)ceil_div(c.CW, 64), (unsigned)ceil_div(c.CH, 16)), dim3(256), 0, st, out,
-                     cst, c, level);
+  const int bdy = c.CH >> level;
+  if (p1 < 0 || p1 > bdy) p1 = bdy;
+  if (p0 < 0) p0 = 0;
+  if (p0 >= p1) return hipSuccess;
+  const long rows = (long)(p1 - p0) << level;
+  hipLaunchKernelGGL(k_rc_fill, dim3((unsigned)ceil_div(c.CW, 64), (unsigned)ceil_div((int)rows, 16)), dim3(256), 0, st,
+                     out, cst, c, level, p0, p1, b0, bn);
   return hipGetLastError();
 }
 
