@@ -1454,6 +1454,10 @@ int phase2_levels(rc2dgi_ctx *c, const FramePlan &plan, const SidePass &f) {
     }
 
     const bool top = L == c->N - 1;
+    // below a filled level: merge with its block values instead of staging its texture (the 32x8x2 tiles)
+    if (fill_on && !top && (filled >> (L + 1) & 1) && c->rc_variant[L] == 6 && c->sd.powW && c->sd.powH &&
+        c->cd.powW && c->cd.powH && L > 0)
+      a.upper_const = c->bconst + boff(L + 1);
     if (fill_on && c->alloff[L] && (top || (filled >> (L + 1) & 1))) {
       HIPCHK(c, launch_rc_block_const(top, top ? c->sky : c->bconst + boff(L + 1), c->bconst + boff(L), L, st));
       for (auto &r : plan.level[L].iv)  // (a row-strip shard: its rows, into the banded texture when banded)

@@ -143,6 +143,8 @@ struct RcLevelArgs {
   // (cyclically), `upper` up_bn rows from up_b0 on; 0 rows: the whole texture
   int out_b0 = 0, out_bn = 0, up_b0 = 0, up_bn = 0;
   int div_x = 0, div_y = 0;  // the level's divisions by CW / CH as x * (1/n) + one fused correction (rc_div_exact)
+  const float4 *upper_const = nullptr;  // the upper level is constant per direction block: its values (k_rc_level UC;
+                                        // 32x8x2 tiles, power-of-two f32 frames)
 };
 // every numerator level `level` divides by the cascade resolution n on one axis (k_rc_level: the probe origins
 // (c + 0.5) 2^L and, below the top, the upper sample positions clamp(c/2 + 1/4, 1/2, bd/2 - 1/2) + k bd/2) has the

@@ -39,6 +39,7 @@ struct RcParams {
   const float4 *cpal;         // surface palettes (kCellPal per bound-table cell): `dist` is the march field
                               // (launch_shade_cmin), and a hit carries its palette entry (pal_mark); nullptr: off
   int lgw;                    // log2 of the screen pitch (palettes: power-of-two screens)
+  const float4 *ucst;         // UC: the upper level's per-direction-block values (k_rc_block_const)
   int rdx, rdy;               // non-power-of-two cascades: the level's divisions by CRx / CRy take div_res mode 2
                               // (host-proven exact, RcLevelArgs div_x / div_y)
   int ob0, obn, ub0, ubn;     // banded G_L / G_{L+1} (RD only; row-strip shards): a level's texture holds, per block
@@ -424,7 +425,7 @@ __device__ __forceinline__ void st_sc1(float4 *base, unsigned off, float4 v) {
 // instantiations, since the derivation's registers and code cost the other marches ~1 %; with the
 // banded textures' row map they get seven waves per SIMD's registers (at eight they spilled)
 template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false, bool CH = false,
-          bool RD = false>
+          bool RD = false, bool UC = false>
 __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 : 8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
@@ -554,8 +555,8 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 :
 #else
   constexpr bool STG = !TOP;  // stage and merge the level-(L+1) cascade
 #endif
-  const bool stg = STG && !ch_top;
-  __shared__ typename GI::S s_up[STG ? NSTAGE : 1];
+  const bool stg = STG && !ch_top && !UC;
+  __shared__ typename GI::S s_up[(STG && !UC) ? NSTAGE : 1];
   // Exit proofs.  The march's last sample of a ray that misses only decides that the ray ends: it
   // is not a hit and t + d leaves the interval or (further along the ray) the screen.  A coarse
   // lower bound dl <= d of the sample's cell (k_dist_cmin) proves both when dl passes the hit test
@@ -572,6 +573,10 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 :
   // the only ones strip tables run (strip_tables_apply); the other instantiations keep the record texture's single load
   constexpr bool RDR = RD;
   static_assert(!RD || (DL == 0 && !CH), "derived records: the plain-field marches");
+  // UC: the upper level is constant over each direction block (a level no ray samples, written as block values:
+  // k_rc_block_const), so the bilinear sample of every ray is its upper block's value, P.ucst[angleIndex] -- no
+  // staging of the upper footprint (the weight-0 taps across a block edge leave a constant so)
+  static_assert(!UC || (!TOP && !Z0 && !CH && std::is_same<GI, GiF32>::value), "block-constant upper: f32 levels");
   constexpr bool PALC = TLC && !TILED && !PACKED;  // surface palettes (P.cpal): the one-probe tiles of the plain field
   // Tail compaction.  A lane marches its NR rays in lockstep and a wave runs until its longest ray
   // ends, so the few rays that pass close to a surface (steps shrink, then grow geometrically) set
@@ -1249,11 +1254,13 @@ __global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 :
         const int r = dblk * 4 + r4;  // index into the 4*PD directions
         float4 rad = hr[p * ND + r];
         const int ai = bi * 4 + r4;  // angleIndex
-        if (rad.w != 0.0f && (stg || TOP || ch_top)) {
+        if (rad.w != 0.0f && (stg || UC || TOP || ch_top)) {
           if (!TOP && !ch_top) {
             typename GI::S t00, t10, t01, t11;
             float ux = wx, uy = wy;
-            if (pow2c) {
+            if constexpr (UC) {
+              t00 = t10 = t01 = t11 = ld_uniform(P.ucst + ai);
+            } else if (pow2c) {
               const typename GI::S *sr = s_up + r * RH * RW;
               t00 = sr[ly0 * RW + lx0];
               t10 = sr[ly0 * RW + lx0 + 1];
@@ -1411,6 +1418,20 @@ static inline hipError_t launch_rc_tiles(const RcLevelArgs &a, RcParams P, hipSt
   const int nwg = rc_tile_params<TX, TY, PY, PD, DL>(a, P);
   if (nwg == 0) return hipErrorOutOfMemory;
   if (nwg < 0) return hipErrorInvalidValue;
+  if (a.upper_const) {  // block-constant upper level (UC): the 32x8x2 plain-field tiles of power-of-two f32 frames
+    if constexpr (TX == 32 && TY == 8 && PY == 2 && PD == 1 && UNR == 1 && DL == 0 && std::is_same<GI, GiF32>::value) {
+      if (!p2s || a.level == a.N - 1 || (a.level == 0 && P.t0 == 0.0f)) return hipErrorInvalidValue;
+      P.ucst = a.upper_const;
+#define RC2DGI_RC_UC(RDV)                                                                                          \
+  hipLaunchKernelGGL((k_rc_level<32, 8, 2, 1, false, true, 1, 0, GiF32, false, false, RDV, true>), dim3(nwg),     \
+                     dim3(256), 0, st, P, a.upper, a.out, a.dist, a.shade, a.dirs, a.sky, a.dist_packed)
+      if (P.rcol) RC2DGI_RC_UC(true); else RC2DGI_RC_UC(false);
+#undef RC2DGI_RC_UC
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
+  }
 #define RC2DGI_RC_RD(TOPV, P2V, Z0V, RDV)                                                                          \
   hipLaunchKernelGGL((k_rc_level<TX, TY, PY, PD, TOPV, P2V, UNR, (P2V ? DL : (DL >= 2 ? 0 : DL)), GI, Z0V, false, RDV>), \
                      dim3(nwg), dim3(TX * TY), 0, st, P, reinterpret_cast<const typename GI::T *>(a.upper),          \

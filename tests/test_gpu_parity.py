@@ -610,6 +610,8 @@ def test_rc_levels_no_ray_samples_as_block_fills(RC2DGI, W, H, N, rr, filled, sc
     color, emis = make_scene(scene, W, H)
     ctx = RC2DGI(W, H, cascade_count=N, ray_range=rr)
     ctx.set_keep_levels(True)
+    if N == 8:  # (the level below the fills on 32x8x2 tiles: it merges with their block values, k_rc_level UC)
+        ctx.set_tuning("rc_variant_L5", 6)
     ctx.upload("color", color)
     ctx.upload("emissive", emis)
     out = {}
