@@ -1798,6 +1798,31 @@ int rc2dgi_autotune(rc2dgi_ctx *c, int frames) {
   return RC2DGI_OK;
 }
 
+namespace {
+// device-to-device copies on a context's stream: gathered into launch_copy_batch launches where the pieces allow it
+// (one device, 16-byte aligned), else one hipMemcpyAsync each; flush() before anything else is enqueued
+struct Copier {
+  rc2dgi_ctx *c;
+  bool batch;
+  CopyBatch b;
+  Copier(rc2dgi_ctx *ctx, bool one_device) : c(ctx), batch(one_device) {}
+  hipError_t add(void *dst, const void *src, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    if (!batch || !copy_piece_ok(src, dst, bytes))
+      return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream);
+    if (b.n == kCopyBatchMax)
+      if (hipError_t e = flush()) return e;
+    b.p[b.n++] = CopyPiece{src, dst, bytes};
+    return hipSuccess;
+  }
+  hipError_t flush() {
+    const hipError_t e = launch_copy_batch(b, c->stream);
+    b.n = 0;
+    return e;
+  }
+};
+}  // namespace
+
 int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
   if (!cs || n < 1) return RC2DGI_E_ARG;
   for (int k = 0; k < n; ++k) {
@@ -1812,6 +1837,10 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
     HIPCHK(cs[k], hipSetDevice(cs[k]->device));
     if (int rc = out_buffers(cs[k])) return rc;
   }
+  // the shards' exchange copies as batched copy kernels when every shard is on one device (in-process rehearsal),
+  // else one hipMemcpyAsync each (Copier)
+  bool one_device = true;
+  for (int k = 1; k < n; ++k) one_device = one_device && cs[k]->device == cs[0]->device;
   // a peer may still be copying our previous distRT strip: wait for every peer's last frame
   for (int k = 0; k < n; ++k) {
     HIPCHK(cs[k], hipSetDevice(cs[k]->device));
@@ -1843,11 +1872,12 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
         for (int q : senders)
           if (std::find(readers.begin(), readers.end(), q) == readers.end())
             HIPCHK(c, hipStreamWaitEvent(c->stream, cs[q]->ev_jfa[(t - 1) & 1], 0));
+        Copier cp(c, one_device);
         for (const JfaXfer &x : c->jx.steps[t].xfers) {
           if (x.dst != k) continue;
-          HIPCHK(c, hipMemcpyAsync(jfa_xbuf(c, t, x.dst_buf, x.dst_row), jfa_xbuf(cs[x.src], t, 0, x.src_row),
-                                   x.rows * rowb, hipMemcpyDeviceToDevice, c->stream));
+          HIPCHK(c, cp.add(jfa_xbuf(c, t, x.dst_buf, x.dst_row), jfa_xbuf(cs[x.src], t, 0, x.src_row), x.rows * rowb));
         }
+        HIPCHK(c, cp.flush());
       }
       int rc = jfa_launch(c, plans[k], t);
       if (rc != RC2DGI_OK) return rc;
@@ -1899,15 +1929,17 @@ int rc2dgi_do_group(rc2dgi_ctx **cs, int n) {
     for (int k = 0; k < n; ++k) {
       rc2dgi_ctx *c = cs[k];
       HIPCHK(c, hipSetDevice(c->device));
+      for (int q = 0; q < n; ++q)
+        if (q != k) HIPCHK(c, hipStreamWaitEvent(c->stream, cs[q]->ev_side, 0));
+      Copier cp(c, one_device);
       for (int q = 0; q < n; ++q) {
         if (q == k) continue;
-        HIPCHK(c, hipStreamWaitEvent(c->stream, cs[q]->ev_side, 0));
         StripPiece pc[4];
         strip_table_pieces(c, q, pc);
         for (int i = 0; i < 4; ++i)
-          HIPCHK(c, hipMemcpyAsync(strip_table_base(c, i) + pc[i].off, strip_table_base(cs[q], i) + pc[i].off, pc[i].bytes,
-                                   hipMemcpyDeviceToDevice, c->stream));
+          HIPCHK(c, cp.add(strip_table_base(c, i) + pc[i].off, strip_table_base(cs[q], i) + pc[i].off, pc[i].bytes));
       }
+      HIPCHK(c, cp.flush());
     }
   }
   for (int k = 0; k < n; ++k) {

@@ -1,6 +1,8 @@
 // rc2dgi_kernels.h -- host-side launchers for the DoRC2DGI() pass kernels (gfx950).
 #pragma once
 
+#include <cstdint>
+
 #include <vector>
 #include <hip/hip_runtime.h>
 
@@ -64,6 +66,23 @@ hipError_t launch_jfa_step(bool first, const unsigned *src, int src_pitch, unsig
                            int jrows = 0,
                            const float *tc = nullptr,  // float path: the W + H texcoord table (tc_table), or nullptr
                            int tmode = 0);  // float path texcoords: 0 divide, 1 the table, 2 tc_rcp (tc_rcp_exact)
+// Several device-to-device copies of one device in one launch (the in-process shard exchanges of rc2dgi_do_group:
+// a copy each is a blit launch, and a frame of 8 shards made about 420 of them): pieces whose addresses and sizes
+// are multiples of 16 bytes (copy_piece_ok), at most kCopyBatchMax per launch.
+struct CopyPiece {
+  const void *src;
+  void *dst;
+  size_t bytes;
+};
+constexpr int kCopyBatchMax = 32;
+struct CopyBatch {
+  CopyPiece p[kCopyBatchMax];
+  int n = 0;
+};
+inline bool copy_piece_ok(const void *src, const void *dst, size_t bytes) {
+  return ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | bytes) & 15u) == 0;
+}
+hipError_t launch_copy_batch(const CopyBatch &b, hipStream_t st);
 // the texcoords (i + 0.5) / W of the W columns, then (j + 0.5) / H of the H rows, as the kernels divide (host)
 void tc_table(int W, int H, float *out);
 // x * (1/n) plus one fused correction equals the IEEE quotient (i + 0.5) / n for every i < n (host, exhaustive)

@@ -1700,6 +1700,30 @@ bool tc_rcp_exact(int n) {
   return true;
 }
 
+// ---------------------------------------------------------------- batched device copies
+// piece blockIdx.y, 16-byte words strided over the x workgroups
+__global__ __launch_bounds__(256) void k_copy_batch(CopyBatch b) {
+  if ((int)blockIdx.y >= b.n) return;
+  const CopyPiece d = b.p[blockIdx.y];
+  const uint4 *__restrict__ src = static_cast<const uint4 *>(d.src);
+  uint4 *__restrict__ dst = static_cast<uint4 *>(d.dst);
+  const size_t n16 = d.bytes >> 4;
+  for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < n16; e += (size_t)gridDim.x * 256) dst[e] = src[e];
+}
+
+hipError_t launch_copy_batch(const CopyBatch &b, hipStream_t st) {
+  if (b.n <= 0) return hipSuccess;
+  if (b.n > kCopyBatchMax) return hipErrorInvalidValue;
+  size_t most = 0;
+  for (int k = 0; k < b.n; ++k) {
+    if (!copy_piece_ok(b.p[k].src, b.p[k].dst, b.p[k].bytes)) return hipErrorInvalidValue;
+    most = std::max(most, b.p[k].bytes);
+  }
+  const size_t wg = std::min<size_t>(std::max<size_t>((most / 16 + 255) / 256, 1), 2048);
+  hipLaunchKernelGGL(k_copy_batch, dim3((unsigned)wg, (unsigned)b.n), dim3(256), 0, st, b);
+  return hipGetLastError();
+}
+
 void tc_table(int W, int H, float *out) {
   for (int i = 0; i < W; ++i) out[i] = ((float)i + 0.5f) / (float)W;  // (IEEE division: texcoord's, bit for bit)
   for (int j = 0; j < H; ++j) out[W + j] = ((float)j + 0.5f) / (float)H;
