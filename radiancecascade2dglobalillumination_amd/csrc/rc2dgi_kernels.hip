@@ -113,7 +113,10 @@ __host__ __device__ __forceinline__ float tc_rcp(int i, float n, float rn) {
 // packed seeds of the previous step.  dist != nullptr fuses DistanceField.fs.  U8: RGBA8 jumpRT
 // (quantized seed uv, pack_seed_u8).
 // A 256-thread workgroup covers 64 x (4*JT) texels; each lane owns JT texels 4 rows apart and issues all 9*JT tap loads before the first compare (latency-bound gathers).
-constexpr int JT = 4;
+#ifndef RC2DGI_JFA_JT
+#define RC2DGI_JFA_JT 4
+#endif
+constexpr int JT = RC2DGI_JFA_JT;
 
 // RT: rows per lane (JT on large screens; 1 on small ones, where 4 rows per lane left about one wave per SIMD:
 // 1200 x 900 = 1083 workgroups, each step a few exposed round trips)
