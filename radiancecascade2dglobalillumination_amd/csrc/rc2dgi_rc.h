@@ -265,6 +265,9 @@ __device__ __forceinline__ int cvt_floor(float x) {
 // so the nearly parallel rays of a lane (and vertical-ish steps) share lines.
 // GI: storage of the cascade textures (GiF32 / GiF16 / GiU8, rc2dgi_device.h).
 // the 16-bit distance q at byte offset `off` (32-bit offsets from the scalar base)
+#ifndef RC2DGI_RC_WPE
+#define RC2DGI_RC_WPE 8  // (A/B builds only)
+#endif
 __device__ __forceinline__ unsigned ld_dist(const unsigned short *dist, unsigned off) {
   return *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(dist) + off);
 }
@@ -426,7 +429,7 @@ __device__ __forceinline__ void st_sc1(float4 *base, unsigned off, float4 v) {
 // banded textures' row map they get seven waves per SIMD's registers (at eight they spilled)
 template <int TX, int TY, int PY, int PD, bool TOP, bool P2S, int UNR, int DL, class GI, bool Z0 = false, bool CH = false,
           bool RD = false, bool UC = false>
-__global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 : 8))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
+__global__ __launch_bounds__(TX *TY) __attribute__((amdgpu_waves_per_eu(RD ? 7 : RC2DGI_RC_WPE))) void k_rc_level(RcParams P, const typename GI::T *__restrict__ upper,
                                                      typename GI::T *__restrict__ out,
                                                      const unsigned short *__restrict__ dist,
                                                      const float4 *__restrict__ shade,
